@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident batched CRC32 on MI355X.
+
+Workload (BASELINE.json configs[1], "config B"): 65,536 independent 4 KiB payloads,
+one CRC32 each, bit-exact with the reference's client/checksum.cc. One step = one
+launch of the batched kernel over one 256 MiB batch already resident in HBM. Four
+distinct batches are rotated so the 256 MiB Infinity Cache cannot serve re-reads
+(every step reads HBM). The payloads are synthetic (SURVEY.md 8d generator),
+generated on device before timing.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...    (one rank per GPU, weak scaling:
+                                                        every rank checksums its own
+                                                        65,536-message shard per step)
+
+Prints ONE JSON line (rank 0). `value` = aggregate GiB/s over all ranks (bytes of all
+ranks / max-over-ranks time). `roofline` is for the CRC kernel itself (HIP events
+around each launch on its stream; algorithmic bytes = 65,536 x 4,096 per launch).
+`cpu_baseline` times the oracle (a C restatement of the reference table path) on this
+host's cores over a bounded sample of the same batches.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "GiB/s CRC32 over batched payloads (device-resident); % of HBM3E read peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md chip table
+MSGS, MSG_BYTES = 65536, 4096
+BATCH_BYTES = MSGS * MSG_BYTES
+ROTATE = 4
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="budget for the CPU baseline legs")
+    return ap.parse_args()
+
+
+def cpu_baseline(batches_host: list[np.ndarray], seconds: float) -> dict:
+    """Oracle (reference table path restated in C) on this host's cores."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _oracle
+    orc = _oracle.load()
+    offs = np.arange(MSGS, dtype=np.uint64) * np.uint64(MSG_BYTES)
+    lens = np.full(MSGS, MSG_BYTES, dtype=np.uint64)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+
+    def rate(nthreads, budget):
+        done, t0 = 0, time.perf_counter()
+        i = 0
+        while True:
+            orc.crc32_batch(batches_host[i % len(batches_host)], offs, lens, threads=nthreads)
+            done += BATCH_BYTES
+            i += 1
+            if time.perf_counter() - t0 >= budget:
+                break
+        return done / (time.perf_counter() - t0) / 2**30, done
+
+    r1, b1 = rate(1, seconds / 2)
+    rn, bn = rate(threads, seconds / 2)
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(rn, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "value_1core": round(r1, 3),
+            "sample": f"config-B batches (65,536 x 4 KiB, host copies of the device batches): "
+                      f"{bn / 2**30:.2f} GiB on {threads} threads, {b1 / 2**30:.2f} GiB on 1 thread; "
+                      f"oracle/crc32_oracle.c byte-table loop (reference client/checksum.cc:125-130), "
+                      f"gcc -O2, CPU: {cpu_model}"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from subspace_amd import gpu
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world > 1:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    ctx = gpu.CrcContext(local)
+    stream = torch.cuda.current_stream()
+
+    # ---- inputs: ROTATE distinct 256 MiB batches; rank r owns message ids r, r+world, ...
+    bufs, outs = [], []
+    for k in range(ROTATE):
+        b = torch.empty(BATCH_BYTES, dtype=torch.uint8, device=dev)
+        gpu.fill_uniform(b, MSG_BYTES, MSG_BYTES, MSGS, seed=0x5EED000B, first_id=rank + k * MSGS * world,
+                         id_stride=world)
+        bufs.append(b)
+        outs.append(torch.empty(MSGS, dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+
+    def step(i):
+        k = i % ROTATE
+        ctx.crc32_uniform(bufs[k], MSG_BYTES, MSG_BYTES, MSGS, outs[k])
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+
+    # ---- timed region: K steps, barrier + sync on both sides, max over ranks
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step(i)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    avg_kern_ms = float(np.mean(kern_ms))
+
+    # ---- bit-exactness of what was timed: batch 0 of rank 0 at world 1 is exactly config B
+    golden = json.loads((ROOT / "tests" / "golden" / "configs.json").read_text())["B"]
+    bitexact = None
+    if world == 1:
+        crc0 = outs[0].cpu().numpy().view(np.uint32)
+        bitexact = hashlib.sha256(crc0.astype("<u4").tobytes()).hexdigest() == golden["sha256_le_u32"]
+
+    # ---- end-to-end (host shared-memory slots -> pinned H2D -> kernel -> D2H), not `value`
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        host = torch.empty(BATCH_BYTES, dtype=torch.uint8, pin_memory=True)
+        host.copy_(bufs[0].cpu())
+        hout = torch.empty(MSGS, dtype=torch.int32, pin_memory=True)
+        dbuf = torch.empty(BATCH_BYTES, dtype=torch.uint8, device=dev)
+        dout = torch.empty(MSGS, dtype=torch.int32, device=dev)
+        for _ in range(2):
+            dbuf.copy_(host, non_blocking=True)
+        torch.cuda.synchronize()
+        n = 10
+        t1 = time.perf_counter()
+        for _ in range(n):
+            dbuf.copy_(host, non_blocking=True)
+            ctx.crc32_uniform(dbuf, MSG_BYTES, MSG_BYTES, MSGS, dout)
+            hout.copy_(dout, non_blocking=True)
+        torch.cuda.synchronize()
+        e2e_s = (time.perf_counter() - t1) / n
+        e2e = {"value": round(BATCH_BYTES / e2e_s / 2**30, 2), "unit": "GiB/s",
+               "path": "pinned host batch -> H2D -> kernel -> D2H of CRCs, serial, one stream"}
+        del host, hout, dbuf, dout
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline([b.cpu().numpy() for b in bufs], args.cpu_seconds)
+
+    traffic = None
+    tfile = ROOT / "profiles" / "traffic_uniform4k.json"
+    if tfile.exists():
+        try:
+            traffic = json.loads(tfile.read_text()).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        total_bytes = BATCH_BYTES * args.steps * world
+        value = total_bytes / elapsed / 2**30
+        achieved = BATCH_BYTES / (avg_kern_ms * 1e-3) / 1e9
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (deterministic splitmix64 payloads generated on device; 4 rotated 256 MiB batches)",
+            "config": {"workload": "B: 65,536 x 4 KiB payloads per GPU per step, one CRC32 (IEEE, "
+                                   "client/checksum.cc default build) each", "messages_per_gpu": MSGS,
+                       "message_bytes": MSG_BYTES, "batches_rotated": ROTATE,
+                       "parallelism": f"independent message shards x{world}"},
+            "pct_of_hbm_peak": round(100.0 * value * 2**30 / 1e9 / HBM_PEAK_GBS, 2),
+            "bitexact_vs_golden": bitexact,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "crc32_uniform4k_kernel<768>", "avg_launch_ms": round(avg_kern_ms, 4)},
+            "cpu_baseline": cpu,
+            "e2e_pcie": e2e,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,79 @@
+/*
+ * subspace_crc.h -- C ABI of libsubspace_crc.so: the MI355X batched CRC32 path.
+ *
+ * Boundary (reference paths relative to dallison/subspace):
+ *   SubspaceCRC32            replaces client/checksum.cc:125-130 (and declares the
+ *                            same symbol as client/checksum.h:18-20). Host code,
+ *                            per-message, bit-exact IEEE (0xEDB88320, raw state).
+ *   subspace_crc32_batch*    NEW batch entry points. Each computes, for every message
+ *                            i of a device-resident batch, exactly
+ *                              out[i] = SubspaceCRC32(init, msg_i, len_i)
+ *                            (or its complement with SUBSPACE_CRC_FINALIZE, i.e. the
+ *                            value CalculateCRC32Checksum stores, client/checksum.h:36).
+ *                            They are what a batched publish (client/publisher.cc:664-675)
+ *                            or a bulk subscriber drain (client/client.cc:344-397,
+ *                            verify at :1346-1356) would call instead of one host CRC
+ *                            per message. Stream-ordered, asynchronous, int status.
+ *
+ * Conventions: plain pointers and sizes only; device pointers are HIP device memory
+ * on the context's device; `stream` is a hipStream_t (NULL = default stream). Calls
+ * return SUBSPACE_CRC_OK or a negative code, never throw, and set a thread-local
+ * message readable with subspace_crc_last_error(). A context is used by one host
+ * thread at a time (like the reference client's per-channel state); distinct
+ * contexts are independent.
+ */
+#ifndef SUBSPACE_CRC_H_
+#define SUBSPACE_CRC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SUBSPACE_CRC_OK 0
+#define SUBSPACE_CRC_EINVAL (-1)  /* bad argument (null pointer, misaligned stride, ...) */
+#define SUBSPACE_CRC_EHIP (-2)    /* a HIP runtime call failed */
+#define SUBSPACE_CRC_ENOMEM (-3)  /* device workspace allocation failed */
+#define SUBSPACE_CRC_ENODEV (-4)  /* no usable gfx950 device */
+
+/* flags */
+#define SUBSPACE_CRC_FINALIZE 0x1u /* store ~crc (the stored checksum) instead of the raw state */
+
+typedef struct subspace_crc_ctx subspace_crc_ctx;
+
+/* Reference-compatible host CRC (client/checksum.h:18-20). */
+uint32_t SubspaceCRC32(uint32_t crc, const uint8_t* data, size_t length);
+
+/* Library version (major*10000 + minor*100 + patch). */
+int subspace_crc_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char* subspace_crc_last_error(void);
+
+/* Create a context on HIP device `device` (uploads the CRC tables once). */
+int subspace_crc_ctx_create(int device, subspace_crc_ctx** out);
+void subspace_crc_ctx_destroy(subspace_crc_ctx* ctx);
+
+/* Pre-size the ragged-batch workspace for up to `max_messages` messages and
+ * `max_tiles` 8 KiB tiles so later subspace_crc32_batch calls never allocate
+ * (required before capturing them into a hipGraph). */
+int subspace_crc_ctx_reserve(subspace_crc_ctx* ctx, uint64_t max_messages, uint64_t max_tiles);
+
+/* Fixed-size batch: message i is the `length` bytes at dev_base + i*stride.
+ * stride >= length. Any length (0 allowed); any stride. */
+int subspace_crc32_batch_uniform(subspace_crc_ctx* ctx, const void* dev_base, uint64_t stride, uint64_t length,
+                                 uint64_t count, uint32_t init, uint32_t flags, uint32_t* dev_out, void* stream);
+
+/* Ragged batch: message i is the dev_lengths[i] bytes at dev_base + dev_offsets[i].
+ * arena_bytes = bytes readable from dev_base (every message must lie inside it).
+ * dev_offsets / dev_lengths are device arrays of `count` uint64. */
+int subspace_crc32_batch(subspace_crc_ctx* ctx, const void* dev_base, uint64_t arena_bytes,
+                         const uint64_t* dev_offsets, const uint64_t* dev_lengths, uint64_t count, uint32_t init,
+                         uint32_t flags, uint32_t* dev_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SUBSPACE_CRC_H_ */

@@ -1,0 +1,72 @@
+"""Loader for the in-tree C-ABI library ``subspace_amd/libsubspace_crc.so``.
+
+The library is built by ``make`` (or ``__graft_entry__.build()``) with hipcc for
+gfx950. There is deliberately no fallback: if the library is missing or does not
+load, every entry point raises, so a GPU run can never silently compute on a CPU
+path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libsubspace_crc.so"
+
+# Every symbol include/subspace_crc.h declares (tests check they are all exported).
+EXPORTED_SYMBOLS = (
+    "SubspaceCRC32",
+    "subspace_crc_version",
+    "subspace_crc_last_error",
+    "subspace_crc_ctx_create",
+    "subspace_crc_ctx_destroy",
+    "subspace_crc_ctx_reserve",
+    "subspace_crc32_batch_uniform",
+    "subspace_crc32_batch",
+)
+
+_lib = None
+
+
+class LibraryNotBuilt(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the library with argtypes configured."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise LibraryNotBuilt(f"{LIB_PATH} not found: run `make` (or __graft_entry__.build()) first")
+    lib = ctypes.CDLL(os.fspath(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+    u32, u64, vp, i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int
+
+    lib.SubspaceCRC32.restype = u32
+    lib.SubspaceCRC32.argtypes = [u32, ctypes.c_void_p, ctypes.c_size_t]
+    lib.subspace_crc_version.restype = i32
+    lib.subspace_crc_version.argtypes = []
+    lib.subspace_crc_last_error.restype = ctypes.c_char_p
+    lib.subspace_crc_last_error.argtypes = []
+    lib.subspace_crc_ctx_create.restype = i32
+    lib.subspace_crc_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
+    lib.subspace_crc_ctx_destroy.restype = None
+    lib.subspace_crc_ctx_destroy.argtypes = [vp]
+    lib.subspace_crc_ctx_reserve.restype = i32
+    lib.subspace_crc_ctx_reserve.argtypes = [vp, u64, u64]
+    lib.subspace_crc32_batch_uniform.restype = i32
+    lib.subspace_crc32_batch_uniform.argtypes = [vp, vp, u64, u64, u64, u32, u32, vp, vp]
+    lib.subspace_crc32_batch.restype = i32
+    lib.subspace_crc32_batch.argtypes = [vp, vp, u64, vp, vp, u64, u32, u32, vp, vp]
+    lib.subspace_crc_testutil_fill_uniform.restype = i32
+    lib.subspace_crc_testutil_fill_uniform.argtypes = [vp, u64, u64, u64, u64, u64, u64, vp]
+    lib.subspace_crc_testutil_fill_ragged.restype = i32
+    lib.subspace_crc_testutil_fill_ragged.argtypes = [vp, vp, vp, u64, u64, u64, u64, vp]
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    msg = load().subspace_crc_last_error()
+    return msg.decode() if msg else ""

@@ -1,0 +1,307 @@
+// C ABI of libsubspace_crc.so (include/subspace_crc.h): contexts, table upload,
+// workspace management and kernel launches. No torch, no Python: plain pointers,
+// sizes, int status codes, thread-local error strings.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/subspace_crc.h"
+#include "crc_device.h"
+#include "crc_math.h"
+
+namespace subspace_amd {
+
+template <int WG>
+__global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*);
+
+struct TileDesc;
+__global__ void crc32_ragged_count_kernel(const u64*, u64, u32, u32, u64*, u32*);
+__global__ void crc32_ragged_desc_kernel(const u64*, const u64*, const u64*, u64, u64, TileDesc*, u32*);
+template <int WG>
+__global__ void crc32_ragged_kernel(const uint8_t*, const u64*, const u64*, const u64*, u64, const TileDesc*,
+                                    const u32*, const u32*, const u32*, const u32*, u32, u32*);
+hipError_t ragged_scan(void* temp, size_t& temp_bytes, const u64* in, u64* out, u64 n, hipStream_t stream);
+__global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* offsets, u64* lengths);
+
+}  // namespace subspace_amd
+
+using namespace subspace_amd;
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+  return fail(SUBSPACE_CRC_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+#define HIP_TRY(call)                                   \
+  do {                                                  \
+    hipError_t e_ = (call);                             \
+    if (e_ != hipSuccess) return hip_fail(e_, #call);   \
+  } while (0)
+
+constexpr int kUniformWG = 768;
+constexpr int kRaggedWG = 768;
+constexpr size_t kTileDescBytes = 32;
+
+}  // namespace
+
+struct subspace_crc_ctx {
+  int device = 0;
+  int num_cus = 256;
+  u32* d_tab = nullptr;  // 4 x 256 slice tables
+  u32* d_ops = nullptr;  // kNumOps nibble operators
+  // zinv[r] = Z_r^{-1}(init), r = 0..127, cached per init value
+  std::unordered_map<u32, u32*> zinv;
+  Tables host_tab;
+  Mat32 zinv1;  // Z_1^{-1}
+  // ragged workspace
+  u64* d_ntiles = nullptr;   // count + 1
+  u64* d_tbase = nullptr;    // count + 1
+  void* d_scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+  u64 ws_messages = 0;
+  uint8_t* d_desc = nullptr;
+  u64 desc_capacity = 0;
+  u32* d_overflow = nullptr;
+  u64* d_uoff = nullptr;  // offsets/lengths materialised for non-4K uniform batches
+  u64* d_ulen = nullptr;
+  u64 u_capacity = 0;
+};
+
+namespace {
+
+int get_zinv(subspace_crc_ctx* c, u32 init, const u32** out) {
+  auto it = c->zinv.find(init);
+  if (it != c->zinv.end()) {
+    *out = it->second;
+    return SUBSPACE_CRC_OK;
+  }
+  u32 h[128];
+  u32 v = init;
+  for (int r = 0; r < 128; r++) {  // h[r] = Z_1^{-r}(init)
+    h[r] = v;
+    v = apply(c->zinv1, v);
+  }
+  u32* d = nullptr;
+  HIP_TRY(hipMalloc(&d, sizeof(h)));
+  HIP_TRY(hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice));
+  c->zinv.emplace(init, d);
+  *out = d;
+  return SUBSPACE_CRC_OK;
+}
+
+int ensure_ragged_ws(subspace_crc_ctx* c, u64 messages, u64 tiles) {
+  if (messages > c->ws_messages) {
+    (void)hipFree(c->d_ntiles);
+    (void)hipFree(c->d_tbase);
+    (void)hipFree(c->d_scan_tmp);
+    c->d_ntiles = c->d_tbase = nullptr;
+    c->d_scan_tmp = nullptr;
+    c->ws_messages = 0;
+    const u64 n = messages + 1;
+    HIP_TRY(hipMalloc(&c->d_ntiles, n * sizeof(u64)));
+    HIP_TRY(hipMalloc(&c->d_tbase, n * sizeof(u64)));
+    size_t tmp = 0;
+    HIP_TRY(ragged_scan(nullptr, tmp, c->d_ntiles, c->d_tbase, n, nullptr));
+    HIP_TRY(hipMalloc(&c->d_scan_tmp, tmp));
+    c->scan_tmp_bytes = tmp;
+    c->ws_messages = messages;
+  }
+  if (tiles > c->desc_capacity) {
+    (void)hipFree(c->d_desc);
+    c->d_desc = nullptr;
+    c->desc_capacity = 0;
+    HIP_TRY(hipMalloc(&c->d_desc, tiles * kTileDescBytes));
+    c->desc_capacity = tiles;
+  }
+  if (!c->d_overflow) HIP_TRY(hipMalloc(&c->d_overflow, 16));
+  return SUBSPACE_CRC_OK;
+}
+
+int grid_for(subspace_crc_ctx* c, u64 work_units, int waves_per_block) {
+  const u64 waves = (work_units + 0) ? work_units : 1;
+  u64 blocks = (waves + waves_per_block - 1) / waves_per_block;
+  if (blocks > (u64)c->num_cus) blocks = c->num_cus;
+  return (int)(blocks ? blocks : 1);
+}
+
+}  // namespace
+
+extern "C" {
+
+int subspace_crc_version(void) { return 100; }  // 0.1.0
+
+const char* subspace_crc_last_error(void) { return g_err; }
+
+int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
+  g_err[0] = 0;
+  if (!out) return fail(SUBSPACE_CRC_EINVAL, "out is null");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(SUBSPACE_CRC_ENODEV, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(SUBSPACE_CRC_EINVAL, "device %d out of range [0,%d)", device, ndev);
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(SUBSPACE_CRC_ENODEV, "device %d is %s, this library is built for gfx950", device, prop.gcnArchName);
+  HIP_TRY(hipSetDevice(device));
+
+  auto* c = new subspace_crc_ctx();
+  c->device = device;
+  c->num_cus = prop.multiProcessorCount;
+  c->host_tab = make_tables();
+  c->zinv1 = inverse(z_one(c->host_tab));
+
+  std::vector<u32> tab(1024), ops((size_t)kNumOps * 128, 0u);
+  for (int k = 0; k < 4; k++)
+    for (int b = 0; b < 256; b++) tab[k * 256 + b] = c->host_tab.t[k][b];
+  for (int k = 0; k < 6; k++) nibble_tables(z_bytes(c->host_tab, 128ull << k), &ops[(size_t)(kOpZ128 + k) * 128]);
+  for (int k = 0; k < kNumTileOps; k++)
+    nibble_tables(z_bytes(c->host_tab, 8192ull << k), &ops[(size_t)(kOpZTile + k) * 128]);
+
+  hipError_t e = hipMalloc(&c->d_tab, tab.size() * 4);
+  if (e == hipSuccess) e = hipMalloc(&c->d_ops, ops.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(c->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->d_ops, ops.data(), ops.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<kUniformWG>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(kUniformWG / 64));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_ragged_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds_bytes(kRaggedWG / 64));
+  if (e != hipSuccess) {
+    subspace_crc_ctx_destroy(c);
+    return hip_fail(e, "context setup");
+  }
+  *out = c;
+  return SUBSPACE_CRC_OK;
+}
+
+void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
+  if (!c) return;
+  (void)hipFree(c->d_tab);
+  (void)hipFree(c->d_ops);
+  for (auto& kv : c->zinv) hipFree(kv.second);
+  (void)hipFree(c->d_ntiles);
+  (void)hipFree(c->d_tbase);
+  (void)hipFree(c->d_scan_tmp);
+  (void)hipFree(c->d_desc);
+  (void)hipFree(c->d_overflow);
+  (void)hipFree(c->d_uoff);
+  (void)hipFree(c->d_ulen);
+  delete c;
+}
+
+int subspace_crc_ctx_reserve(subspace_crc_ctx* c, uint64_t max_messages, uint64_t max_tiles) {
+  g_err[0] = 0;
+  if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  HIP_TRY(hipSetDevice(c->device));
+  const u32* z;
+  int rc = get_zinv(c, 0xFFFFFFFFu, &z);
+  if (rc) return rc;
+  return ensure_ragged_ws(c, max_messages, max_tiles);
+}
+
+int subspace_crc32_batch(subspace_crc_ctx* c, const void* dev_base, uint64_t arena_bytes, const uint64_t* dev_offsets,
+                         const uint64_t* dev_lengths, uint64_t count, uint32_t init, uint32_t flags,
+                         uint32_t* dev_out, void* stream) {
+  g_err[0] = 0;
+  if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  if (count == 0) return SUBSPACE_CRC_OK;
+  if (!dev_base || !dev_offsets || !dev_lengths || !dev_out)
+    return fail(SUBSPACE_CRC_EINVAL, "null device pointer");
+  if (flags & ~SUBSPACE_CRC_FINALIZE) return fail(SUBSPACE_CRC_EINVAL, "unknown flags 0x%x", flags);
+  if (count >= (1ull << 32)) return fail(SUBSPACE_CRC_EINVAL, "count %llu exceeds 2^32-1", (unsigned long long)count);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const u32 final_xor = (flags & SUBSPACE_CRC_FINALIZE) ? 0xFFFFFFFFu : 0u;
+  const u32* zinv;
+  int rc = get_zinv(c, init, &zinv);
+  if (rc) return rc;
+  // Tile capacity: exact for non-overlapping messages inside the arena; if the device
+  // finds more tiles (overlapping messages) the kernel falls back to per-tile search.
+  const u64 cap = arena_bytes / 8192 + count + 1;
+  rc = ensure_ragged_ws(c, count, cap);
+  if (rc) return rc;
+
+  const u64 n1 = count + 1;
+  crc32_ragged_count_kernel<<<(unsigned)((n1 + 255) / 256), 256, 0, st>>>(dev_lengths, count, init, final_xor,
+                                                                           c->d_ntiles, dev_out);
+  HIP_TRY(hipGetLastError());
+  size_t tmp = c->scan_tmp_bytes;
+  HIP_TRY(ragged_scan(c->d_scan_tmp, tmp, c->d_ntiles, c->d_tbase, n1, st));
+  const u64 desc_threads = cap;
+  crc32_ragged_desc_kernel<<<(unsigned)((desc_threads + 255) / 256), 256, 0, st>>>(
+      dev_offsets, dev_lengths, c->d_tbase, count, cap, reinterpret_cast<TileDesc*>(c->d_desc), c->d_overflow);
+  HIP_TRY(hipGetLastError());
+  const int blocks = c->num_cus;  // persistent: one 12-wave workgroup per CU
+  crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, lds_bytes(kRaggedWG / 64), st>>>(
+      static_cast<const uint8_t*>(dev_base), dev_offsets, dev_lengths, c->d_tbase, count,
+      reinterpret_cast<const TileDesc*>(c->d_desc), c->d_overflow, c->d_tab, c->d_ops, zinv, final_xor, dev_out);
+  HIP_TRY(hipGetLastError());
+  return SUBSPACE_CRC_OK;
+}
+
+int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint64_t stride, uint64_t length,
+                                 uint64_t count, uint32_t init, uint32_t flags, uint32_t* dev_out, void* stream) {
+  g_err[0] = 0;
+  if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  if (count == 0) return SUBSPACE_CRC_OK;
+  if (!dev_base || !dev_out) return fail(SUBSPACE_CRC_EINVAL, "null device pointer");
+  if (flags & ~SUBSPACE_CRC_FINALIZE) return fail(SUBSPACE_CRC_EINVAL, "unknown flags 0x%x", flags);
+  if (stride < length && count > 1) return fail(SUBSPACE_CRC_EINVAL, "stride %llu < length %llu",
+                                                (unsigned long long)stride, (unsigned long long)length);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const u32 final_xor = (flags & SUBSPACE_CRC_FINALIZE) ? 0xFFFFFFFFu : 0u;
+  const bool fast = length == 4096 && (stride % 16) == 0 && ((uintptr_t)dev_base % 16) == 0;
+  if (fast) {
+    const u64 tiles = (count + 1) / 2;
+    const int blocks = grid_for(c, tiles, kUniformWG / 64);
+    crc32_uniform4k_kernel<kUniformWG><<<blocks, kUniformWG, lds_bytes(kUniformWG / 64), st>>>(
+        static_cast<const uint8_t*>(dev_base), stride, count, c->d_tab, c->d_ops, init, final_xor, dev_out);
+    HIP_TRY(hipGetLastError());
+    return SUBSPACE_CRC_OK;
+  }
+  // Any other shape: materialise offsets/lengths and take the ragged path.
+  if (count > c->u_capacity) {
+    (void)hipFree(c->d_uoff);
+    (void)hipFree(c->d_ulen);
+    c->d_uoff = c->d_ulen = nullptr;
+    c->u_capacity = 0;
+    HIP_TRY(hipMalloc(&c->d_uoff, count * sizeof(u64)));
+    HIP_TRY(hipMalloc(&c->d_ulen, count * sizeof(u64)));
+    c->u_capacity = count;
+  }
+  uniform_offsets_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(stride, length, count, c->d_uoff,
+                                                                           c->d_ulen);
+  HIP_TRY(hipGetLastError());
+  const u64 arena = stride * (count - 1) + length;
+  return subspace_crc32_batch(c, dev_base, arena, c->d_uoff, c->d_ulen, count, init, flags, dev_out, stream);
+}
+
+}  // extern "C"
+
+namespace subspace_amd {
+__global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* offsets, u64* lengths) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) {
+    offsets[i] = i * stride;
+    lengths[i] = length;
+  }
+}
+}  // namespace subspace_amd

@@ -1,0 +1,93 @@
+// Device-side building blocks shared by the CRC32 kernels (gfx950 / CDNA4).
+//
+// LDS layout of every CRC kernel (one workgroup per CU):
+//   [0, 128 KiB)       slice-by-4 byte tables, 32-way replicated: table k (k = 0..3 for
+//                      byte k of the step word) entry e copy b at byte address
+//                      ((k>>1)<<16) | (e<<8) | ((k&1)<<7) | (b<<2). Lane l reads copy
+//                      (l & 31), i.e. LDS bank (l & 31), so the 4 data-dependent lookups
+//                      of a step are bank-conflict-free for any data (ds_read_b32 banks
+//                      lanes in two groups of 32, bank = dword address mod 32).
+//   [128 KiB, +16 KiB) 32 GF(2) operator slots, each 8 nibble tables x 16 dwords (512 B).
+//                      A 16-entry table spans 16 distinct banks, so nibble lookups are
+//                      conflict-free without replication.
+//   [144 KiB, ...)     1 KiB per wave: transpose buffer for the combine tree.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace subspace_amd {
+
+using u32 = uint32_t;
+using u64 = uint64_t;
+using i64 = int64_t;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+
+constexpr u32 kLdsTables = 0;
+constexpr u32 kLdsOps = 128u * 1024u;
+constexpr int kNumOps = 32;
+constexpr u32 kLdsXpose = kLdsOps + kNumOps * 512u;
+constexpr u32 kLdsXposePerWave = 1024u;
+constexpr size_t lds_bytes(int waves) { return kLdsXpose + (size_t)waves * kLdsXposePerWave; }
+
+// operator slots
+constexpr int kOpZ128 = 0;    // slots 0..5: Z_{128 * 2^k}, k = 0..5 (128 B .. 4 KiB)
+constexpr int kOpZTile = 6;   // slots 6..26: Z_{8192 * 2^k}, k = 0..20 (8 KiB .. 8 GiB)
+constexpr int kNumTileOps = 21;
+
+typedef __attribute__((address_space(3))) u32 lds_u32_t;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
+
+__device__ __forceinline__ u32 lds_ld(u32 addr) { return *reinterpret_cast<const lds_u32_t*>((uintptr_t)addr); }
+__device__ __forceinline__ void lds_st(u32 addr, u32 v) { *reinterpret_cast<lds_u32_t*>((uintptr_t)addr) = v; }
+__device__ __forceinline__ u32x4 lds_ld4(u32 addr) { return *reinterpret_cast<const lds_u32x4_t*>((uintptr_t)addr); }
+__device__ __forceinline__ void lds_st4(u32 addr, u32x4 v) { *reinterpret_cast<lds_u32x4_t*>((uintptr_t)addr) = v; }
+
+// Fill the replicated step tables and the operator slots from global memory.
+// gtab: 4 x 256 dwords, gtab[k*256 + b] = CRC of byte b followed by k zero bytes.
+// gops: kNumOps * 128 dwords of nibble tables.
+__device__ __forceinline__ void fill_lds(u32 sbase, const u32* __restrict__ gtab, const u32* __restrict__ gops) {
+  for (int t = threadIdx.x; t < 1024; t += blockDim.x) {
+    const int k = t & 3, e = t >> 2;
+    // step-table k serves byte k of the word, i.e. the byte followed by 3-k zero bytes
+    const u32 v = gtab[(3 - k) * 256 + e];
+    const u32x4 vv = {v, v, v, v};
+    const u32 dst = sbase + (((u32)(k >> 1) << 16) | ((u32)e << 8) | ((u32)(k & 1) << 7));
+#pragma unroll
+    for (int i = 0; i < 8; i++) lds_st4(dst + 16 * i, vv);
+  }
+  for (int t = threadIdx.x; t < kNumOps * 128; t += blockDim.x) lds_st(sbase + kLdsOps + 4 * t, gops[t]);
+}
+
+// One slice-by-4 step: crc_raw(0, LE bytes of x) = T4(x), via 4 conflict-free lookups.
+// lc0 = sbase | (lane&31)<<2, lc1 = lc0 + 64 KiB. v_perm_b32 builds each address in one
+// instruction: byte0 = lane bank offset, byte1 = the data byte, byte2 = region, byte3 = 0.
+__device__ __forceinline__ u32 step4(u32 x, u32 lc0, u32 lc1) {
+  const u32 a0 = __builtin_amdgcn_perm(x, lc0, 0x0c020400u);
+  const u32 a1 = __builtin_amdgcn_perm(x, lc0, 0x0c020500u);
+  const u32 a2 = __builtin_amdgcn_perm(x, lc1, 0x0c020600u);
+  const u32 a3 = __builtin_amdgcn_perm(x, lc1, 0x0c020700u);
+  return lds_ld(a0) ^ lds_ld(a1 + 128) ^ lds_ld(a2) ^ lds_ld(a3 + 128);
+}
+
+// Apply GF(2) operator `slot` to v: 8 conflict-free nibble lookups.
+__device__ __forceinline__ u32 opmul(u32 sbase, int slot, u32 v) {
+  const u32 op = sbase + kLdsOps + 512u * (u32)slot;
+  u32 r = lds_ld(op + ((v << 2) & 0x3Cu));
+#pragma unroll
+  for (int k = 1; k < 8; k++) r ^= lds_ld(op + 64u * k + ((v >> (4 * k - 2)) & 0x3Cu));
+  return r;
+}
+
+// Byte step with the k=3 step table (plain byte table): crc = (crc >> 8) ^ T[(crc ^ b) & 0xFF].
+__device__ __forceinline__ u32 step1(u32 crc, u32 b, u32 lc1) {
+  const u32 x = (crc ^ b) & 0xFFu;
+  return (crc >> 8) ^ lds_ld(__builtin_amdgcn_perm(x, lc1, 0x0c020400u) + 128);
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+}  // namespace subspace_amd

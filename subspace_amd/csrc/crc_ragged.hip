@@ -1,0 +1,284 @@
+// Ragged-batch kernels: one CRC32 per message for arbitrary offsets, lengths and
+// alignment (BASELINE configs C and D; any subspace_crc32_batch call).
+//
+// Decomposition (DESIGN.md "Ragged kernel"):
+//  * Message m = bytes [s, e). Its n = ceil(L/128) "virtual lines" are aligned to the
+//    message END: line g covers [e - 128(n-g), e - 128(n-1-g)). Only line 0 can start
+//    before s; its r = 128n - L leading bytes are zero-masked and its lane starts from
+//    zinv[r] = Z_r^{-1}(init), so after the r zero bytes the state is exactly init:
+//      crc_raw(zinv[r], 0^r || D) = crc_raw(init, D).
+//    Every line is a full 128-byte unit, so the combine is uniform:
+//      crc(m) = XOR_g Z_{128(n-1-g)}(line_g)                       (linearity)
+//  * A tile is 64 consecutive virtual lines of ONE message (end-aligned, so only a
+//    message's first tile is partial). Lane i <-> line i of the tile, exactly like the
+//    uniform kernel: 64 consecutive 128-B lines per wave load instruction.
+//  * Waves stream the global tile list in sweep order (tau = k*nw + w), one tile of
+//    loads in flight ahead. Per-tile descriptors (tile end, message start, message id,
+//    tiles after) are precomputed by crc32_ragged_desc_kernel.
+//  * Every 4 tiles the 256 line CRCs are transposed through LDS (16 lanes per tile),
+//    tree-combined (Z_128..Z_4096), multiplied by Z_{8192*T} (T = tiles after this one
+//    in the message, binary decomposition over nibble operators) and written: a plain
+//    store for single-tile messages, atomicXor into a pre-zeroed word otherwise.
+//  * End-aligned lines are 16-B misaligned when e is: each lane then loads the 9
+//    aligned 16-B blocks covering its line and realigns with v_alignbyte_b32 (the
+//    dword shift e&15 >> 2 is wave-uniform, so it is a 4-way uniform switch).
+//    Loads never touch a 16-B block that contains no message byte, so nothing outside
+//    the messages' own aligned blocks is read.
+#include <hipcub/hipcub.hpp>
+
+#include "crc_device.h"
+
+namespace subspace_amd {
+
+struct TileDesc {
+  u64 tile_end;   // absolute offset (from base) one past the tile's last byte
+  u64 msg_start;  // offset of the message's first byte
+  u32 msg;        // message index
+  u32 after;      // tiles after this one in the message
+  u64 pad;
+};
+static_assert(sizeof(TileDesc) == 32, "TileDesc is 32 B");
+
+__host__ __device__ inline u64 tiles_for_length(u64 len) { return (len + 8191) >> 13; }
+
+// Per message: tile count; zero-length messages get their (constant) result here,
+// multi-tile messages get their output word zeroed for the tiles' atomicXor.
+__global__ void crc32_ragged_count_kernel(const u64* __restrict__ lengths, u64 count, u32 init, u32 final_xor,
+                                          u64* __restrict__ ntiles, u32* __restrict__ out) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > count) return;
+  if (i == count) {
+    ntiles[i] = 0;  // scan sentinel: tile_base[count] = total tiles
+    return;
+  }
+  const u64 len = lengths[i];
+  const u64 nt = tiles_for_length(len);
+  ntiles[i] = nt;
+  if (nt == 0) out[i] = init ^ final_xor;
+  else if (nt > 1) out[i] = 0u;
+}
+
+__device__ inline u64 find_msg(const u64* __restrict__ tile_base, u64 count, u64 tau) {
+  // last m with tile_base[m] <= tau (skips zero-tile messages, whose base equals the next one's)
+  u64 lo = 0, hi = count;  // invariant: tile_base[lo] <= tau < tile_base[hi]
+  while (hi - lo > 1) {
+    const u64 mid = (lo + hi) >> 1;
+    if (tile_base[mid] <= tau) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ inline TileDesc make_desc(const u64* __restrict__ offsets, const u64* __restrict__ lengths,
+                                     const u64* __restrict__ tile_base, u64 m, u64 tau) {
+  const u64 nt = tile_base[m + 1] - tile_base[m];
+  const u64 j = tau - tile_base[m];
+  const u64 s = offsets[m];
+  const u64 e = s + lengths[m];
+  TileDesc d;
+  d.tile_end = e - ((nt - 1 - j) << 13);
+  d.msg_start = s;
+  d.msg = (u32)m;
+  d.after = (u32)(nt - 1 - j);
+  d.pad = 0;
+  return d;
+}
+
+// Per tile (up to `capacity`): its descriptor. Sets *overflow if the batch has more tiles.
+__global__ void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, const u64* __restrict__ lengths,
+                                         const u64* __restrict__ tile_base, u64 count, u64 capacity,
+                                         TileDesc* __restrict__ desc, u32* __restrict__ overflow) {
+  const u64 total = tile_base[count];
+  const u64 tau = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tau == 0) *overflow = total > capacity ? 1u : 0u;
+  if (tau >= total || tau >= capacity) return;
+  desc[tau] = make_desc(offsets, lengths, tile_base, find_msg(tile_base, count, tau), tau);
+}
+
+// ------------------------------------------------------------------ main kernel
+struct LineState {
+  u32x4 d[9];  // aligned 16-B blocks covering the lane's line (9th only when misaligned)
+};
+
+template <int Q>
+__device__ __forceinline__ u32 word_at(const LineState& L, int j, u32 m3) {
+  // word j of the realigned line: bytes [4(j+Q) + m3, +4) of the aligned window
+  const int x = j + Q;
+  const u32 lo = L.d[x >> 2][x & 3];
+  const u32 hi = L.d[(x + 1) >> 2][(x + 1) & 3];
+  return __builtin_amdgcn_alignbyte(hi, lo, m3);
+}
+
+template <int Q, bool MIS>
+__device__ __forceinline__ u32 crc_line(const LineState& L, u32 crc, u32 m3, u32 lc0, u32 lc1) {
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    const u32 w = MIS ? word_at<Q>(L, j, m3) : L.d[j >> 2][j & 3];
+    crc = step4(crc ^ w, lc0, lc1);
+  }
+  return crc;
+}
+
+template <int WG>
+__global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restrict__ base,
+                                                          const u64* __restrict__ offsets,
+                                                          const u64* __restrict__ lengths,
+                                                          const u64* __restrict__ tile_base, u64 count,
+                                                          const TileDesc* __restrict__ desc,
+                                                          const u32* __restrict__ overflow,
+                                                          const u32* __restrict__ gtab, const u32* __restrict__ gops,
+                                                          const u32* __restrict__ zinv, u32 final_xor,
+                                                          u32* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) u32 smem[];
+  const u32 sbase = (u32)(uintptr_t)smem;
+  fill_lds(sbase, gtab, gops);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const u32 wid = (u32)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
+  const u32 lc1 = lc0 + 0x10000u;
+  const u32 xb = sbase + kLdsXpose + wid * kLdsXposePerWave;
+  const u64 total = tile_base[count];
+  const bool use_desc = *overflow == 0u;
+  const u64 w = (u64)blockIdx.x * (WG / 64) + wid;
+  const u64 nw = (u64)gridDim.x * (WG / 64);
+  if (w >= total) return;
+  const u64 nk = (total - w + nw - 1) / nw;
+
+  auto get_desc = [&](u64 k) -> TileDesc {
+    const u64 tau = k * nw + w;
+    if (use_desc) return desc[tau];
+    return make_desc(offsets, lengths, tile_base, find_msg(tile_base, count, tau), tau);
+  };
+  // Issue the loads of this lane's line for tile descriptor d.
+  // Positions are signed: a message's first tile can start before the arena start.
+  auto load_line = [&](const TileDesc& d, LineState& L) {
+    const i64 line_start = (i64)d.tile_end - 8192 + (i64)lane * 128;
+    const i64 a0 = line_start & ~(i64)15;
+    const i64 s = (i64)d.msg_start;
+    const bool mis = (d.tile_end & 15) != 0;
+    const bool partial = (i64)d.tile_end - 8192 < s;  // first tile of its message
+#pragma unroll
+    for (int b = 0; b < 9; b++) {
+      const i64 blk = a0 + 16 * b;
+      // only blocks that hold at least one byte of the message are ever read
+      const bool need = (b < 8 || mis) && (!partial || blk + 16 > s);
+      if (need) L.d[b] = *reinterpret_cast<const u32x4*>(base + blk);
+      else L.d[b] = u32x4{0, 0, 0, 0};
+    }
+  };
+
+  // descriptors run two tiles ahead of the compute, line loads one tile ahead
+  TileDesc dcur = get_desc(0);
+  TileDesc dnext = nk > 1 ? get_desc(1) : dcur;
+  LineState cur;
+  load_line(dcur, cur);
+  u32 part[4] = {0, 0, 0, 0};
+  u32 gmsg[4] = {0, 0, 0, 0}, gafter[4] = {0, 0, 0, 0};
+  u32 gfirst = 0;  // bit t: tile t of the group is its message's first tile
+  for (u64 k = 0; k < nk; k++) {
+    const bool more = k + 1 < nk;
+    const TileDesc dnext2 = (k + 2 < nk) ? get_desc(k + 2) : dnext;
+    LineState nxt;
+    if (more) load_line(dnext, nxt);
+    // ---- compute the current tile's line CRC
+    const i64 tile_start = (i64)dcur.tile_end - 8192;
+    const i64 line_start = tile_start + (i64)lane * 128;
+    const i64 s = (i64)dcur.msg_start;
+    const bool partial = tile_start < s;
+    const bool active = line_start + 128 > s;
+    u32 crc = 0;
+    if (partial) {
+      // zero every byte below the message start, seed the first line with zinv[r]
+      const i64 a0 = line_start & ~(i64)15;
+#pragma unroll
+      for (int b = 0; b < 9; b++) {
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+          const i64 addr = a0 + 16 * b + 4 * x;
+          u32 keep = 0xFFFFFFFFu;
+          if (addr + 4 <= s) keep = 0;
+          else if (addr < s) keep = 0xFFFFFFFFu << (8 * (u32)(s - addr));
+          cur.d[b][x] &= keep;
+        }
+      }
+      if (active && line_start <= s) crc = zinv[s - line_start];
+    } else if (lane == 0 && line_start == s) {
+      crc = zinv[0];
+    }
+    const u32 mis = (u32)(dcur.tile_end & 15);
+    const u32 m3 = mis & 3;
+    switch (mis >> 2) {  // wave-uniform
+      case 0: crc = mis ? crc_line<0, true>(cur, crc, m3, lc0, lc1) : crc_line<0, false>(cur, crc, m3, lc0, lc1); break;
+      case 1: crc = crc_line<1, true>(cur, crc, m3, lc0, lc1); break;
+      case 2: crc = crc_line<2, true>(cur, crc, m3, lc0, lc1); break;
+      default: crc = crc_line<3, true>(cur, crc, m3, lc0, lc1); break;
+    }
+    if (!active) crc = 0;
+
+    const int t = (int)(k & 3);
+    // static-index stores keep part[] / gmsg[] / gafter[] in registers
+#pragma unroll
+    for (int tt = 0; tt < 4; tt++)
+      if (tt == t) {
+        part[tt] = crc;
+        gmsg[tt] = dcur.msg;
+        gafter[tt] = dcur.after;
+      }
+    gfirst = (partial || tile_start == s) ? (gfirst | (1u << t)) : (gfirst & ~(1u << t));
+
+    if (t == 3 || !more) {
+#pragma unroll
+      for (int tt = 0; tt < 4; tt++) lds_st(xb + tt * 256 + lane * 4, part[tt]);
+      wave_lds_sync();
+      const int T = lane >> 4, q = lane & 15;
+      const u32x4 s = lds_ld4(xb + T * 256 + q * 16);  // lines 4q..4q+3 of group tile T
+      const u32 a = opmul(sbase, kOpZ128 + 0, s[0]) ^ s[1];
+      const u32 b = opmul(sbase, kOpZ128 + 0, s[2]) ^ s[3];
+      u32 c = opmul(sbase, kOpZ128 + 1, a) ^ b;               // 512 B
+      c = opmul(sbase, kOpZ128 + 2, c) ^ __shfl_down(c, 1);   // 1 KiB
+      c = opmul(sbase, kOpZ128 + 3, c) ^ __shfl_down(c, 2);   // 2 KiB
+      c = opmul(sbase, kOpZ128 + 4, c) ^ __shfl_down(c, 4);   // 4 KiB
+      c = opmul(sbase, kOpZ128 + 5, c) ^ __shfl_down(c, 8);   // 8 KiB: tile result at q == 0
+      const bool valid = (u64)T <= (u64)t;                     // group slot holds a tile
+      u32 after = 0, msg = 0;
+#pragma unroll
+      for (int tt = 0; tt < 4; tt++)
+        if (tt == T) { after = gafter[tt]; msg = gmsg[tt]; }
+      // shift to the message end: Z_{8192 * after}, binary decomposition (wave-uniform loop)
+      u32 rem = (q == 0 && valid) ? after : 0u;
+      for (int bit = 0; bit < kNumTileOps && __any(rem != 0u); bit++) {
+        const u32 cm = opmul(sbase, kOpZTile + bit, c);
+        c = (rem & 1u) ? cm : c;
+        rem >>= 1;
+      }
+      if (q == 0 && valid) {
+        const bool first = (gfirst >> T) & 1u;
+        const u32 contrib = first ? (c ^ final_xor) : c;
+        if (first && after == 0) out[msg] = contrib;  // single-tile message
+        else atomicXor(&out[msg], contrib);
+      }
+      wave_lds_sync();
+    }
+    if (more) {
+      dcur = dnext;
+      dnext = dnext2;
+      cur = nxt;
+    }
+  }
+}
+
+template __global__ void crc32_ragged_kernel<768>(const uint8_t*, const u64*, const u64*, const u64*, u64,
+                                                  const TileDesc*, const u32*, const u32*, const u32*, const u32*,
+                                                  u32, u32*);
+template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, const u64*, const u64*, u64,
+                                                  const TileDesc*, const u32*, const u32*, const u32*, const u32*,
+                                                  u32, u32*);
+
+// hipcub scan wrapper (exclusive prefix sum of per-message tile counts).
+hipError_t ragged_scan(void* temp, size_t& temp_bytes, const u64* in, u64* out, u64 n, hipStream_t stream) {
+  return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, stream);
+}
+
+}  // namespace subspace_amd

@@ -1,0 +1,68 @@
+// Deterministic synthetic-payload generators (device side) for tests and bench.py.
+// Not part of the reference API; exported with a subspace_crc_testutil_ prefix.
+//
+// Byte j of message `id` = byte (j mod 8), little-endian, of
+//   splitmix64(seed ^ (id << 32) ^ (j >> 3))                 
+// oracle/crc32_oracle.c:oracle_synth_fill is the host twin of this generator.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// One message per block iteration (grid-stride over messages), threads over 8-B units.
+__global__ void synth_fill_kernel(uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
+                                  const uint64_t* __restrict__ lengths, uint64_t stride, uint64_t length,
+                                  uint64_t count, uint64_t first_id, uint64_t id_stride, uint64_t seed) {
+  for (uint64_t m = blockIdx.x; m < count; m += gridDim.x) {
+    const uint64_t off = offsets ? offsets[m] : m * stride;
+    const uint64_t len = lengths ? lengths[m] : length;
+    const uint64_t id = first_id + m * id_stride;
+    const uint64_t key = seed ^ (id << 32);
+    uint8_t* dst = base + off;
+    const uint64_t units = (len + 7) >> 3;
+    const bool aligned8 = (off & 7) == 0;
+    for (uint64_t u = threadIdx.x; u < units; u += blockDim.x) {
+      const uint64_t w = splitmix64(key ^ u);
+      const uint64_t j = u << 3;
+      if (aligned8 && j + 8 <= len) {
+        *reinterpret_cast<uint64_t*>(dst + j) = w;
+      } else {
+        for (uint64_t b = 0; b < 8 && j + b < len; b++) dst[j + b] = (uint8_t)(w >> (8 * b));
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int subspace_crc_testutil_fill_uniform(void* dev_base, uint64_t stride, uint64_t length, uint64_t count,
+                                       uint64_t first_id, uint64_t id_stride, uint64_t seed, void* stream) {
+  if (!dev_base && count) return -1;
+  if (!count) return 0;
+  const unsigned blocks = (unsigned)(count < 65536 ? count : 65536);
+  synth_fill_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(static_cast<uint8_t*>(dev_base), nullptr, nullptr,
+                                                              stride, length, count, first_id, id_stride, seed);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int subspace_crc_testutil_fill_ragged(void* dev_base, const uint64_t* dev_offsets, const uint64_t* dev_lengths,
+                                      uint64_t count, uint64_t first_id, uint64_t id_stride, uint64_t seed,
+                                      void* stream) {
+  if ((!dev_base || !dev_offsets || !dev_lengths) && count) return -1;
+  if (!count) return 0;
+  const unsigned blocks = (unsigned)(count < 65536 ? count : 65536);
+  synth_fill_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(static_cast<uint8_t*>(dev_base), dev_offsets,
+                                                              dev_lengths, 0, 0, count, first_id, id_stride, seed);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // extern "C"

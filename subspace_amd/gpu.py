@@ -1,0 +1,98 @@
+"""Batched device CRC32 through the C ABI (include/subspace_crc.h).
+
+``CrcContext`` owns one ``subspace_crc_ctx`` (tables uploaded once per device).
+Batches are torch tensors on that device -- torch is only the device-memory and
+stream plumbing here; every CRC is computed by the HIP kernels in
+``libsubspace_crc.so``. There is no CPU fallback: without the library or a gfx950
+device the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib
+
+FINALIZE = 0x1  # SUBSPACE_CRC_FINALIZE: store ~crc (the checksum CalculateCRC32Checksum writes)
+
+
+class CrcError(RuntimeError):
+    pass
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise CrcError(f"{what} failed ({rc}): {_lib.last_error()}")
+
+
+def _ptr(t) -> int:
+    return int(t.data_ptr())
+
+
+def _stream_ptr(stream) -> int | None:
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream) if stream.cuda_stream else None
+
+
+class CrcContext:
+    """Per-device context (reference analogue: the client library's per-process state)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _lib.load()
+        self.device = device
+        h = ctypes.c_void_p()
+        _check(self._lib.subspace_crc_ctx_create(device, ctypes.byref(h)), "subspace_crc_ctx_create")
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.subspace_crc_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def reserve(self, max_messages: int, max_tiles: int) -> None:
+        _check(self._lib.subspace_crc_ctx_reserve(self._h, max_messages, max_tiles), "subspace_crc_ctx_reserve")
+
+    def crc32_uniform(self, buf, stride: int, length: int, count: int, out, *, init: int = 0xFFFFFFFF,
+                      finalize: bool = False, stream=None, base_offset: int = 0) -> None:
+        """out[i] = SubspaceCRC32(init, buf[base_offset + i*stride :][:length]) for i < count."""
+        _check(self._lib.subspace_crc32_batch_uniform(
+            self._h, _ptr(buf) + base_offset, stride, length, count, init & 0xFFFFFFFF,
+            FINALIZE if finalize else 0, _ptr(out), _stream_ptr(stream)), "subspace_crc32_batch_uniform")
+
+    def crc32_ragged(self, buf, offsets, lengths, out, *, init: int = 0xFFFFFFFF, finalize: bool = False,
+                     arena_bytes: int | None = None, stream=None) -> None:
+        """out[i] = SubspaceCRC32(init, buf[offsets[i]:][:lengths[i]]) (int64 device tensors)."""
+        n = int(offsets.numel())
+        if int(lengths.numel()) != n or int(out.numel()) < n:
+            raise ValueError("offsets, lengths and out must describe the same number of messages")
+        arena = int(buf.numel() * buf.element_size()) if arena_bytes is None else arena_bytes
+        _check(self._lib.subspace_crc32_batch(
+            self._h, _ptr(buf), arena, _ptr(offsets), _ptr(lengths), n, init & 0xFFFFFFFF,
+            FINALIZE if finalize else 0, _ptr(out), _stream_ptr(stream)), "subspace_crc32_batch")
+
+
+# ---------------------------------------------------------------- synthetic inputs (device)
+def fill_uniform(buf, stride: int, length: int, count: int, *, seed: int, first_id: int = 0, id_stride: int = 1,
+                 stream=None) -> None:
+    """Deterministic payloads (SURVEY.md 8d generator) for a fixed-size batch, on device."""
+    _check(_lib.load().subspace_crc_testutil_fill_uniform(
+        _ptr(buf), stride, length, count, first_id, id_stride, seed, _stream_ptr(stream)), "fill_uniform")
+
+
+def fill_ragged(buf, offsets, lengths, *, seed: int, first_id: int = 0, id_stride: int = 1, stream=None) -> None:
+    _check(_lib.load().subspace_crc_testutil_fill_ragged(
+        _ptr(buf), _ptr(offsets), _ptr(lengths), int(offsets.numel()), first_id, id_stride, seed,
+        _stream_ptr(stream)), "fill_ragged")

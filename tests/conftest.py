@@ -1,0 +1,41 @@
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    """The CPU checker (oracle/, test infrastructure only)."""
+    import _oracle
+    return _oracle.load()
+
+
+@pytest.fixture(scope="session")
+def lib():
+    from subspace_amd import _lib
+    if not _lib.LIB_PATH.exists():
+        subprocess.run(["make", "-C", str(ROOT)], check=True)
+    return _lib.load()
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from subspace_amd.gpu import CrcContext
+    ctx = CrcContext(0)
+    yield ctx
+    ctx.close()

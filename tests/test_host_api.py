@@ -1,0 +1,148 @@
+"""The host drop-in (libsubspace_crc.so SubspaceCRC32 + include/subspace/checksum.h)
+against the oracle and the golden fixtures. CPU only: these are product host paths,
+not GPU fallbacks (the batch API has none)."""
+import json
+import shutil
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from subspace_amd import checksum as ck
+
+ROOT = Path(__file__).resolve().parent.parent
+GOLDEN = json.loads((Path(__file__).parent / "golden" / "golden.json").read_text())
+M32 = 0xFFFFFFFF
+
+
+def test_kats(lib):
+    for k in GOLDEN["kat"]:
+        d = bytes.fromhex(k["data_hex"])
+        assert ck.subspace_crc32(M32, d) == k["raw"]
+
+
+def test_reference_literal_tests(lib):
+    assert ck.subspace_crc32(M32, b"") == 0xFFFFFFFF                          # client_test.rs:169-173
+    assert (~ck.subspace_crc32(M32, b"hello")) & M32 == 0x3610A686           # :175-180
+    assert ck.subspace_crc32(ck.subspace_crc32(M32, b"hello "), b"world") == ck.subspace_crc32(M32, b"hello world")
+    assert ck.calculate_crc32_checksum([b"foobar"]) == ck.calculate_crc32_checksum([b"foo", b"bar"])
+    c = ck.calculate_crc32_checksum([b"subspace", b"ipc"])
+    assert c != b"\0\0\0\0"
+    assert ck.verify_crc32_checksum([b"subspace", b"ipc"], c)
+    bad = (int.from_bytes(c, "little") ^ 1).to_bytes(4, "little")
+    assert not ck.verify_crc32_checksum([b"subspace", b"ipc"], bad)
+    assert ck.calculate_crc32_checksum([b"aaa"]) != ck.calculate_crc32_checksum([b"bbb"])
+
+
+def test_prefix_lengths(lib):
+    g = GOLDEN["prefix_lengths"]
+    buf = bytes.fromhex(g["buffer_hex"])
+    for n, raw in enumerate(g["raw"]):
+        assert ck.subspace_crc32(M32, buf[:n]) == raw, n
+
+
+def test_long_and_raw_states(lib):
+    from subspace_amd import synth
+    for g in GOLDEN["long_lengths"]:
+        assert ck.subspace_crc32(M32, synth.synth_bytes(g["seed"], g["msg"], g["length"])) == g["raw"]
+    for g in GOLDEN["raw_states"]:
+        assert ck.subspace_crc32(g["state"], bytes.fromhex(g["data_hex"])) == g["raw"]
+
+
+def test_any_alignment(lib, oracle):
+    rng = np.random.default_rng(11)
+    blob = rng.integers(0, 256, 5000, dtype=np.uint8).tobytes()
+    mv = memoryview(bytearray(blob))
+    for off in range(0, 17):
+        for n in (0, 1, 3, 15, 16, 17, 31, 100, 1000, 4000):
+            assert ck.subspace_crc32(M32, mv[off:off + n]) == oracle.crc32(M32, blob[off:off + n])
+
+
+def test_three_span_and_message_helpers(lib):
+    for g in GOLDEN["three_span"]:
+        prefix = bytearray.fromhex(g["prefix_hex"])
+        payload = bytes.fromhex(g["payload_hex"])
+        cs, ms = g["checksum_size"], g["metadata_size"]
+        assert len(prefix) == ck.compute_prefix_size(cs, ms)
+        spans = ck.get_message_checksum_data(prefix, payload, len(payload), cs, ms)
+        assert [len(s) for s in spans] == [44, ms, len(payload)]
+        region = memoryview(prefix)[48:48 + cs]
+        out = ck.calculate_crc32_checksum(spans, region)
+        assert out.hex() == g["checksum_le_hex"]
+        assert bytes(prefix[48:52]).hex() == g["checksum_le_hex"]
+        assert ck.verify_crc32_checksum(ck.get_message_checksum_data(prefix, payload, len(payload), cs, ms),
+                                        prefix[48:52])
+        # corrupt one payload byte -> verification fails (client_test.cc ChecksumVerification)
+        if payload:
+            bad = bytearray(payload)
+            bad[len(bad) // 2] ^= 0x40
+            assert not ck.verify_crc32_checksum(ck.get_message_checksum_data(prefix, bad, len(bad), cs, ms),
+                                                prefix[48:52])
+
+
+def test_prefix_sizes():
+    # docs/checksums-and-metadata.md "Prefix Size Calculation" table
+    assert ck.compute_prefix_size(4, 0) == 64
+    assert ck.compute_prefix_size(20, 0) == 128
+    assert ck.compute_prefix_size(4, 12) == 64
+    assert ck.compute_prefix_size(4, 13) == 128
+    assert ck.compute_prefix_size(32, 64) == 192
+
+
+def test_bit_flips_change_crc(lib):
+    from subspace_amd import synth
+    d = bytearray(synth.synth_bytes(1, 2, 4096))
+    base = ck.subspace_crc32(M32, d)
+    for pos in range(0, 4096 * 8, 997):
+        d[pos // 8] ^= 1 << (pos % 8)
+        assert ck.subspace_crc32(M32, d) != base
+        d[pos // 8] ^= 1 << (pos % 8)
+
+
+CPP_TEST = r"""
+#include <cstdio>
+#include <cstring>
+#include <cstddef>
+#include "subspace/checksum.h"
+int main() {
+  const char* msg = "hello";
+  // client_test.cc Checksum20Byte style: the raw-state API with non-standard seeds
+  uint32_t a = subspace::SubspaceCRC32(0xFFFFFFFF, reinterpret_cast<const uint8_t*>(msg), 5);
+  if ((~a) != 0x3610A686u) { std::printf("KAT fail %08x\n", ~a); return 1; }
+  uint8_t p1[] = {'f', 'o', 'o'}, p2[] = {'b', 'a', 'r'}, p3[] = {'f', 'o', 'o', 'b', 'a', 'r'};
+  std::array<absl::Span<const uint8_t>, 3> split = {absl::Span<const uint8_t>(p1, 3),
+      absl::Span<const uint8_t>(p2, 3), absl::Span<const uint8_t>(nullptr, 0)};
+  std::array<absl::Span<const uint8_t>, 1> whole = {absl::Span<const uint8_t>(p3, 6)};
+  std::byte c1[20] = {}, c2[4] = {};
+  subspace::CalculateCRC32Checksum<3>(split, absl::Span<std::byte>(c1, 20));
+  subspace::CalculateCRC32Checksum<1>(whole, absl::Span<std::byte>(c2, 4));
+  if (std::memcmp(c1, c2, 4) != 0) { std::printf("span mismatch\n"); return 2; }
+  if (!subspace::VerifyCRC32Checksum<3>(split, absl::Span<const std::byte>(c1, 20))) return 3;
+  c1[0] ^= std::byte{1};
+  if (subspace::VerifyCRC32Checksum<3>(split, absl::Span<const std::byte>(c1, 20))) return 4;
+  subspace::ChecksumCallback cb = [](const std::array<absl::Span<const uint8_t>, 3>& d, absl::Span<std::byte> out) {
+    subspace::CalculateCRC32Checksum<3>(d, out);
+  };
+  std::byte c3[4];
+  cb(split, absl::Span<std::byte>(c3, 4));
+  if (std::memcmp(c3, c2, 4) != 0) return 5;
+  std::printf("ok\n");
+  return 0;
+}
+"""
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_header_drop_in_compiles_and_links(lib, tmp_path):
+    """A publisher-style C++ program compiles against include/subspace/checksum.h unchanged
+    and links SubspaceCRC32 from libsubspace_crc.so."""
+    src = tmp_path / "t.cc"
+    src.write_text(CPP_TEST)
+    exe = tmp_path / "t"
+    libdir = ROOT / "subspace_amd"
+    subprocess.run(["g++", "-std=c++17", "-O1", f"-I{ROOT / 'include'}", str(src), "-o", str(exe),
+                    f"-L{libdir}", "-lsubspace_crc", f"-Wl,-rpath,{libdir}"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip() == "ok"

@@ -1,0 +1,51 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 summaries.
+# Each GPU step has its own time limit; the script stops at the first fault,
+# abort, segfault or timeout (exit status >= 124 or > 128) and never retries.
+#   usage: bash tools/gpu_session.sh [tag] [steps...]   steps: test smoke bench prof pmc
+set -u
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-"test smoke bench prof pmc"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+stop_if_fault() {  # $1 = exit status, $2 = step name
+  local rc=$1
+  echo "step $2 rc=$rc" >> "$OUT/status.txt"
+  if [ "$rc" -ge 124 ] || [ "$rc" -gt 128 ]; then
+    echo "stopping after $2 (rc=$rc)" >> "$OUT/status.txt"
+    exit "$rc"
+  fi
+}
+
+for s in $STEPS; do
+  case $s in
+    test)
+      timeout -k 10 1200 python -m pytest tests/ -q -m gpu -p no:cacheprovider --timeout 600 -rf \
+        > "$OUT/pytest_gpu.log" 2>&1
+      stop_if_fault $? test ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      stop_if_fault $? smoke ;;
+    bench)
+      timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+      stop_if_fault $? bench ;;
+    prof)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run \
+        --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline \
+        --no-e2e > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
+      stop_if_fault $? prof ;;
+    pmc)
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $ctr -d "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr" -o run \
+          --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline \
+          --no-e2e > "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.json" 2> "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.err")
+        stop_if_fault $? "pmc_$ctr"
+      done ;;
+    *)
+      echo "unknown step $s" >> "$OUT/status.txt" ;;
+  esac
+done
+echo done >> "$OUT/status.txt"
