@@ -38,7 +38,7 @@ METRIC = "GiB/s CRC32 over batched payloads (device-resident); % of HBM3E read p
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md chip table
 MSGS, MSG_BYTES = 65536, 4096
 BATCH_BYTES = MSGS * MSG_BYTES
-ROTATE = 4
+ROTATE = 4  # 4 x 256 MiB > the 256 MiB Infinity Cache: every step reads HBM
 
 
 def parse():
@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="budget for the CPU baseline legs")
+    ap.add_argument("--workload", default="B", choices=["B", "E"],
+                    help="B: 65,536 x 4 KiB per GPU per step (weak scaling, default); "
+                         "E: 8 Mi x 4 KiB sharded round-robin over the GPUs (strong scaling) + RCCL gather")
     return ap.parse_args()
 
 
@@ -110,19 +113,32 @@ def main():
     ctx = gpu.CrcContext(local)
     stream = torch.cuda.current_stream()
 
-    # ---- inputs: ROTATE distinct 256 MiB batches; rank r owns message ids r, r+world, ...
+    from subspace_amd import shard
+
+    # ---- inputs. B: ROTATE distinct 256 MiB batches per rank (message ids r, r+world, ...).
+    #      E: this rank's round-robin shard of the 8 Mi-message batch, one buffer.
     bufs, outs = [], []
-    for k in range(ROTATE):
-        b = torch.empty(BATCH_BYTES, dtype=torch.uint8, device=dev)
-        gpu.fill_uniform(b, MSG_BYTES, MSG_BYTES, MSGS, seed=0x5EED000B, first_id=rank + k * MSGS * world,
-                         id_stride=world)
+    if args.workload == "B":
+        nmsg, nbuf = MSGS, ROTATE
+        for k in range(nbuf):
+            b = torch.empty(nmsg * MSG_BYTES, dtype=torch.uint8, device=dev)
+            gpu.fill_uniform(b, MSG_BYTES, MSG_BYTES, nmsg, seed=0x5EED000B, first_id=rank + k * nmsg * world,
+                             id_stride=world)
+            bufs.append(b)
+            outs.append(torch.empty(nmsg, dtype=torch.int32, device=dev))
+    else:
+        total_e = 8 << 20
+        nmsg, nbuf = shard.shard_count(total_e, rank, world), 1
+        b = torch.empty(nmsg * MSG_BYTES, dtype=torch.uint8, device=dev)
+        gpu.fill_uniform(b, MSG_BYTES, MSG_BYTES, nmsg, seed=0x5EED000E, first_id=rank, id_stride=world)
         bufs.append(b)
-        outs.append(torch.empty(MSGS, dtype=torch.int32, device=dev))
+        outs.append(torch.empty(nmsg, dtype=torch.int32, device=dev))
+    step_bytes = nmsg * MSG_BYTES
     torch.cuda.synchronize()
 
     def step(i):
-        k = i % ROTATE
-        ctx.crc32_uniform(bufs[k], MSG_BYTES, MSG_BYTES, MSGS, outs[k])
+        k = i % nbuf
+        ctx.crc32_uniform(bufs[k], MSG_BYTES, MSG_BYTES, nmsg, outs[k])
 
     for i in range(args.warmup):
         step(i)
@@ -149,16 +165,31 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     avg_kern_ms = float(np.mean(kern_ms))
 
-    # ---- bit-exactness of what was timed: batch 0 of rank 0 at world 1 is exactly config B
-    golden = json.loads((ROOT / "tests" / "golden" / "configs.json").read_text())["B"]
-    bitexact = None
-    if world == 1:
+    # ---- bit-exactness of what was timed. B at world 1: batch 0 is exactly config B.
+    #      E: gather every rank's CRCs to rank 0 over RCCL (timed separately) and compare the
+    #      whole 8 Mi list with the fixture.
+    goldens = json.loads((ROOT / "tests" / "golden" / "configs.json").read_text())
+    bitexact, gather_ms = None, None
+    if args.workload == "B" and world == 1:
         crc0 = outs[0].cpu().numpy().view(np.uint32)
-        bitexact = hashlib.sha256(crc0.astype("<u4").tobytes()).hexdigest() == golden["sha256_le_u32"]
+        bitexact = hashlib.sha256(crc0.astype("<u4").tobytes()).hexdigest() == goldens["B"]["sha256_le_u32"]
+    if args.workload == "E":
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        if world > 1:
+            full = shard.gather_crcs(outs[0], 8 << 20, rank, world, dist)
+        else:
+            full = outs[0].cpu().numpy().view(np.uint32)
+        gather_ms = (time.perf_counter() - tg) * 1e3
+        if rank == 0:
+            bitexact = hashlib.sha256(np.asarray(full, dtype="<u4").tobytes()).hexdigest() == \
+                goldens["E"]["sha256_le_u32"]
 
     # ---- end-to-end (host shared-memory slots -> pinned H2D -> kernel -> D2H), not `value`
     e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e:
+    if rank == 0 and world == 1 and not args.no_e2e and args.workload == "B":
         host = torch.empty(BATCH_BYTES, dtype=torch.uint8, pin_memory=True)
         host.copy_(bufs[0].cpu())
         hout = torch.empty(MSGS, dtype=torch.int32, pin_memory=True)
@@ -180,7 +211,7 @@ def main():
         del host, hout, dbuf, dout
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "B":
         cpu = cpu_baseline([b.cpu().numpy() for b in bufs], args.cpu_seconds)
 
     traffic = None
@@ -192,9 +223,22 @@ def main():
             traffic = None
 
     if rank == 0:
-        total_bytes = BATCH_BYTES * args.steps * world
+        if args.workload == "B":
+            total_bytes = step_bytes * args.steps * world  # every rank: its own 65,536-message batch
+            workload = {"workload": "B: 65,536 x 4 KiB payloads per GPU per step, one CRC32 (IEEE, "
+                                    "client/checksum.cc default build) each", "messages_per_gpu": nmsg,
+                        "message_bytes": MSG_BYTES, "batches_rotated": ROTATE,
+                        "parallelism": f"independent message shards x{world}"}
+            scaling = "weak"
+        else:
+            total_bytes = (8 << 20) * MSG_BYTES * args.steps  # the whole 8 Mi batch per step
+            workload = {"workload": "E: 8 Mi x 4 KiB payloads per step, round-robin over the GPUs, one CRC32 each",
+                        "messages_total": 8 << 20, "messages_per_gpu": nmsg, "message_bytes": MSG_BYTES,
+                        "parallelism": f"round-robin message shards x{world}, RCCL all_gather of CRCs (untimed)",
+                        "gather_ms": round(gather_ms, 3) if gather_ms is not None else None}
+            scaling = "strong"
         value = total_bytes / elapsed / 2**30
-        achieved = BATCH_BYTES / (avg_kern_ms * 1e-3) / 1e9
+        achieved = step_bytes / (avg_kern_ms * 1e-3) / 1e9
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -204,19 +248,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (deterministic splitmix64 payloads generated on device; 4 rotated 256 MiB batches)",
-            "config": {"workload": "B: 65,536 x 4 KiB payloads per GPU per step, one CRC32 (IEEE, "
-                                   "client/checksum.cc default build) each", "messages_per_gpu": MSGS,
-                       "message_bytes": MSG_BYTES, "batches_rotated": ROTATE,
-                       "parallelism": f"independent message shards x{world}"},
-            "pct_of_hbm_peak": round(100.0 * value * 2**30 / 1e9 / HBM_PEAK_GBS, 2),
+            "data": "synthetic (deterministic splitmix64 payloads generated on device"
+                    + ("; 4 rotated 256 MiB batches per GPU)" if args.workload == "B" else ")"),
+            "config": workload,
+            "pct_of_hbm_peak": round(100.0 * value * 2**30 / 1e9 / (HBM_PEAK_GBS * world), 2),
             "bitexact_vs_golden": bitexact,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "crc32_uniform4k_kernel<768>", "avg_launch_ms": round(avg_kern_ms, 4)},
+                         "kernel": "subspace_amd::crc32_uniform4k_kernel<512>", "avg_launch_ms": round(avg_kern_ms, 4)},
             "cpu_baseline": cpu,
             "e2e_pcie": e2e,
         }

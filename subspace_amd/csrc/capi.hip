@@ -17,11 +17,11 @@
 namespace subspace_amd {
 
 template <int WG>
-__global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*);
+__global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
 
 struct TileDesc;
 __global__ void crc32_ragged_count_kernel(const u64*, u64, u32, u32, u64*, u32*);
-__global__ void crc32_ragged_desc_kernel(const u64*, const u64*, const u64*, u64, u64, TileDesc*, u32*);
+__global__ void crc32_ragged_desc_kernel(const u64*, const u64*, const u64*, const u32*, u64, u64, TileDesc*, u32*);
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, const u64*, const u64*, u64, const TileDesc*,
                                     const u32*, const u32*, const u32*, const u32*, u32, u32*);
@@ -52,8 +52,7 @@ int hip_fail(hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail(e_, #call);   \
   } while (0)
 
-constexpr int kUniformWG = 768;
-constexpr int kRaggedWG = 768;
+constexpr int kRaggedWG = 512;
 constexpr size_t kTileDescBytes = 32;
 
 }  // namespace
@@ -76,6 +75,9 @@ struct subspace_crc_ctx {
   uint8_t* d_desc = nullptr;
   u64 desc_capacity = 0;
   u32* d_overflow = nullptr;
+  int uniform_wg = 512;    // workgroup size of the uniform kernel (256/512/640/768/1024)
+  int uniform_blocks = 0;  // 0 = one workgroup per CU
+  int uniform_order = 0;   // tile order: 0 sweep, 1 per-workgroup region
   u64* d_uoff = nullptr;  // offsets/lengths materialised for non-4K uniform batches
   u64* d_ulen = nullptr;
   u64 u_capacity = 0;
@@ -177,9 +179,12 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_ops, ops.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(c->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_ops, ops.data(), ops.size() * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<kUniformWG>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(kUniformWG / 64));
+#define SET_LDS(WGV)                                                                                   \
+  if (e == hipSuccess)                                                                                 \
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                            (int)lds_bytes(WGV / 64));
+  SET_LDS(256) SET_LDS(512) SET_LDS(640) SET_LDS(768) SET_LDS(1024)
+#undef SET_LDS
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_ragged_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds_bytes(kRaggedWG / 64));
@@ -246,7 +251,7 @@ int subspace_crc32_batch(subspace_crc_ctx* c, const void* dev_base, uint64_t are
   HIP_TRY(ragged_scan(c->d_scan_tmp, tmp, c->d_ntiles, c->d_tbase, n1, st));
   const u64 desc_threads = cap;
   crc32_ragged_desc_kernel<<<(unsigned)((desc_threads + 255) / 256), 256, 0, st>>>(
-      dev_offsets, dev_lengths, c->d_tbase, count, cap, reinterpret_cast<TileDesc*>(c->d_desc), c->d_overflow);
+      dev_offsets, dev_lengths, c->d_tbase, zinv, count, cap, reinterpret_cast<TileDesc*>(c->d_desc), c->d_overflow);
   HIP_TRY(hipGetLastError());
   const int blocks = c->num_cus;  // persistent: one 12-wave workgroup per CU
   crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, lds_bytes(kRaggedWG / 64), st>>>(
@@ -271,9 +276,22 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
   const bool fast = length == 4096 && (stride % 16) == 0 && ((uintptr_t)dev_base % 16) == 0;
   if (fast) {
     const u64 tiles = (count + 1) / 2;
-    const int blocks = grid_for(c, tiles, kUniformWG / 64);
-    crc32_uniform4k_kernel<kUniformWG><<<blocks, kUniformWG, lds_bytes(kUniformWG / 64), st>>>(
-        static_cast<const uint8_t*>(dev_base), stride, count, c->d_tab, c->d_ops, init, final_xor, dev_out);
+    const int wg = c->uniform_wg;
+    int blocks = grid_for(c, tiles, wg / 64);
+    if (c->uniform_blocks > 0 && (u64)c->uniform_blocks < (u64)blocks) blocks = c->uniform_blocks;
+    const auto* b = static_cast<const uint8_t*>(dev_base);
+    const int ord = c->uniform_order;
+#define LAUNCH(WGV)                                                                                    \
+  crc32_uniform4k_kernel<WGV><<<blocks, WGV, lds_bytes(WGV / 64), st>>>(b, stride, count, c->d_tab, c->d_ops, init, \
+                                                                        final_xor, dev_out, ord)
+    switch (wg) {
+      case 256: LAUNCH(256); break;
+      case 640: LAUNCH(640); break;
+      case 768: LAUNCH(768); break;
+      case 1024: LAUNCH(1024); break;
+      default: LAUNCH(512); break;
+    }
+#undef LAUNCH
     HIP_TRY(hipGetLastError());
     return SUBSPACE_CRC_OK;
   }
@@ -292,6 +310,18 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
   HIP_TRY(hipGetLastError());
   const u64 arena = stride * (count - 1) + length;
   return subspace_crc32_batch(c, dev_base, arena, c->d_uoff, c->d_ulen, count, init, flags, dev_out, stream);
+}
+
+// Tuning hook for experiments (not part of the public header): uniform-kernel workgroup
+// size (512/768/1024) and an optional cap on the number of workgroups.
+int subspace_crc_testutil_tune(subspace_crc_ctx* c, int uniform_wg, int uniform_blocks, int uniform_order) {
+  if (!c) return SUBSPACE_CRC_EINVAL;
+  if (uniform_wg != 256 && uniform_wg != 512 && uniform_wg != 640 && uniform_wg != 768 && uniform_wg != 1024)
+    return SUBSPACE_CRC_EINVAL;
+  c->uniform_wg = uniform_wg;
+  c->uniform_blocks = uniform_blocks;
+  c->uniform_order = uniform_order;
+  return SUBSPACE_CRC_OK;
 }
 
 }  // extern "C"

@@ -42,21 +42,60 @@ __device__ __forceinline__ void lds_st(u32 addr, u32 v) { *reinterpret_cast<lds_
 __device__ __forceinline__ u32x4 lds_ld4(u32 addr) { return *reinterpret_cast<const lds_u32x4_t*>((uintptr_t)addr); }
 __device__ __forceinline__ void lds_st4(u32 addr, u32x4 v) { *reinterpret_cast<lds_u32x4_t*>((uintptr_t)addr) = v; }
 
-// Fill the replicated step tables and the operator slots from global memory.
+// Fill of the replicated step tables and the first NOPS operator slots, split into a
+// load phase and a store phase so a kernel can issue its first tile's global loads in
+// between: vmcnt retires in issue order, so the table loads (older) can be waited for
+// while the tile loads (younger) stay in flight across the LDS stores and the barrier.
 // gtab: 4 x 256 dwords, gtab[k*256 + b] = CRC of byte b followed by k zero bytes.
 // gops: kNumOps * 128 dwords of nibble tables.
-__device__ __forceinline__ void fill_lds(u32 sbase, const u32* __restrict__ gtab, const u32* __restrict__ gops) {
-  for (int t = threadIdx.x; t < 1024; t += blockDim.x) {
-    const int k = t & 3, e = t >> 2;
-    // step-table k serves byte k of the word, i.e. the byte followed by 3-k zero bytes
-    const u32 v = gtab[(3 - k) * 256 + e];
-    const u32x4 vv = {v, v, v, v};
-    const u32 dst = sbase + (((u32)(k >> 1) << 16) | ((u32)e << 8) | ((u32)(k & 1) << 7));
+template <int WG, int NOPS>
+struct LdsFill {
+  static constexpr int kTabIters = (1024 + WG - 1) / WG;
+  static constexpr int kOpWords = NOPS * 128;
+  static constexpr int kOpIters = (kOpWords + WG - 1) / WG;
+  u32 tv[kTabIters], ov[kOpIters];
+
+  __device__ __forceinline__ void load(const u32* __restrict__ gtab, const u32* __restrict__ gops) {
+    // Unconditional loads (indices clamped; surplus values are never stored): a load in a
+    // divergent branch would make hipcc wait vmcnt(0) here instead of a counted wait.
+    const int tid = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < 8; i++) lds_st4(dst + 16 * i, vv);
+    for (int i = 0; i < kTabIters; i++) {
+      const int t = min(tid + i * WG, 1023);
+      // step-table k serves byte k of the word, i.e. the byte followed by 3-k zero bytes
+      tv[i] = gtab[(3 - (t & 3)) * 256 + (t >> 2)];
+    }
+#pragma unroll
+    for (int i = 0; i < kOpIters; i++) ov[i] = gops[min(tid + i * WG, kOpWords - 1)];
   }
-  for (int t = threadIdx.x; t < kNumOps * 128; t += blockDim.x) lds_st(sbase + kLdsOps + 4 * t, gops[t]);
-}
+
+  __device__ __forceinline__ void store(u32 sbase) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < kTabIters; i++) {
+      const int t = tid + i * WG;
+      if (t < 1024) {
+        const int k = t & 3, e = t >> 2;
+        const u32x4 vv = {tv[i], tv[i], tv[i], tv[i]};
+        const u32 dst = sbase + (((u32)(k >> 1) << 16) | ((u32)e << 8) | ((u32)(k & 1) << 7));
+#pragma unroll
+        for (int j = 0; j < 8; j++) lds_st4(dst + 16 * j, vv);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kOpIters; i++) {
+      const int t = tid + i * WG;
+      if (t < kOpWords) lds_st(sbase + kLdsOps + 4 * t, ov[i]);
+    }
+    // Consume every fill load on every path: otherwise hipcc's waitcnt pass treats the
+    // skipped ones as possibly pending at the main loop's header and drains the tile
+    // prefetch with vmcnt(0) on every iteration.
+#pragma unroll
+    for (int i = 0; i < kTabIters; i++) asm volatile("" ::"v"(tv[i]));
+#pragma unroll
+    for (int i = 0; i < kOpIters; i++) asm volatile("" ::"v"(ov[i]));
+  }
+};
 
 // One slice-by-4 step: crc_raw(0, LE bytes of x) = T4(x), via 4 conflict-free lookups.
 // lc0 = sbase | (lane&31)<<2, lc1 = lc0 + 64 KiB. v_perm_b32 builds each address in one

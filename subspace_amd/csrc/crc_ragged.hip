@@ -35,7 +35,8 @@ struct TileDesc {
   u64 msg_start;  // offset of the message's first byte
   u32 msg;        // message index
   u32 after;      // tiles after this one in the message
-  u64 pad;
+  u32 seed;       // first tile only: zinv[r], the start state of the line holding msg_start
+  u32 pad;
 };
 static_assert(sizeof(TileDesc) == 32, "TileDesc is 32 B");
 
@@ -70,7 +71,8 @@ __device__ inline u64 find_msg(const u64* __restrict__ tile_base, u64 count, u64
 }
 
 __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, const u64* __restrict__ lengths,
-                                     const u64* __restrict__ tile_base, u64 m, u64 tau) {
+                                     const u64* __restrict__ tile_base, const u32* __restrict__ zinv, u64 m,
+                                     u64 tau) {
   const u64 nt = tile_base[m + 1] - tile_base[m];
   const u64 j = tau - tile_base[m];
   const u64 s = offsets[m];
@@ -80,19 +82,24 @@ __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, const u64*
   d.msg_start = s;
   d.msg = (u32)m;
   d.after = (u32)(nt - 1 - j);
+  // the line holding byte s starts r = (s - tile_start) mod 128 bytes before it (lines are
+  // end-aligned, so tile_start == e - 8192*(nt-j) and r only depends on e - s mod 128)
+  const i64 tile_start = (i64)d.tile_end - 8192;
+  const u64 r = (u64)((i64)s - tile_start) & 127u;
+  d.seed = j == 0 ? zinv[r] : 0u;
   d.pad = 0;
   return d;
 }
 
 // Per tile (up to `capacity`): its descriptor. Sets *overflow if the batch has more tiles.
 __global__ void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, const u64* __restrict__ lengths,
-                                         const u64* __restrict__ tile_base, u64 count, u64 capacity,
-                                         TileDesc* __restrict__ desc, u32* __restrict__ overflow) {
+                                         const u64* __restrict__ tile_base, const u32* __restrict__ zinv, u64 count,
+                                         u64 capacity, TileDesc* __restrict__ desc, u32* __restrict__ overflow) {
   const u64 total = tile_base[count];
   const u64 tau = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (tau == 0) *overflow = total > capacity ? 1u : 0u;
   if (tau >= total || tau >= capacity) return;
-  desc[tau] = make_desc(offsets, lengths, tile_base, find_msg(tile_base, count, tau), tau);
+  desc[tau] = make_desc(offsets, lengths, tile_base, zinv, find_msg(tile_base, count, tau), tau);
 }
 
 // ------------------------------------------------------------------ main kernel
@@ -119,8 +126,8 @@ __device__ __forceinline__ u32 crc_line(const LineState& L, u32 crc, u32 m3, u32
   return crc;
 }
 
-template <int WG>
-__global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restrict__ base,
+template <int WG, bool DESC>
+__device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
                                                           const u64* __restrict__ offsets,
                                                           const u64* __restrict__ lengths,
                                                           const u64* __restrict__ tile_base, u64 count,
@@ -128,69 +135,84 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
                                                           const u32* __restrict__ overflow,
                                                           const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                           const u32* __restrict__ zinv, u32 final_xor,
-                                                          u32* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) u32 smem[];
-  const u32 sbase = (u32)(uintptr_t)smem;
-  fill_lds(sbase, gtab, gops);
-  __syncthreads();
-
+                                                          u32* __restrict__ out, u32 sbase) {
   const int lane = threadIdx.x & 63;
   const u32 wid = (u32)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
   const u32 xb = sbase + kLdsXpose + wid * kLdsXposePerWave;
   const u64 total = tile_base[count];
-  const bool use_desc = *overflow == 0u;
   const u64 w = (u64)blockIdx.x * (WG / 64) + wid;
   const u64 nw = (u64)gridDim.x * (WG / 64);
-  if (w >= total) return;
-  const u64 nk = (total - w + nw - 1) / nw;
+  const u64 nk = w < total ? (total - w + nw - 1) / nw : 0;  // tiles tau = k*nw + w, k < nk
+  if (total == 0) return;  // every message empty: all waves of all blocks leave before any load
+  // An opaque zero in a VGPR: descriptor loads indexed with it are vector loads, so they
+  // retire in order with the line loads (vmcnt) instead of coupling with LDS (lgkmcnt).
+  u32 vzero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
 
-  auto get_desc = [&](u64 k) -> TileDesc {
-    const u64 tau = k * nw + w;
-    if (use_desc) return desc[tau];
-    return make_desc(offsets, lengths, tile_base, find_msg(tile_base, count, tau), tau);
+  // Descriptor of tile k as raw dwords (a vector load). Past the wave's last tile it is
+  // clamped to that tile; a wave without tiles uses the batch's last tile, so every load
+  // the kernel issues stays inside a real message.
+  auto fetch_desc = [&](u64 k, u32x4 (&d)[2]) {
+    const u64 tau = nk ? (k < nk ? k : nk - 1) * nw + w : total - 1;
+    if (DESC) {
+      const u32x4* p = reinterpret_cast<const u32x4*>(desc + tau + vzero);
+      d[0] = p[0];
+      d[1] = p[1];
+    } else {
+      const TileDesc t = make_desc(offsets, lengths, tile_base, zinv, find_msg(tile_base, count, tau), tau);
+      d[0] = u32x4{(u32)t.tile_end, (u32)(t.tile_end >> 32), (u32)t.msg_start, (u32)(t.msg_start >> 32)};
+      d[1] = u32x4{t.msg, t.after, t.seed, 0u};
+    }
   };
-  // Issue the loads of this lane's line for tile descriptor d.
-  // Positions are signed: a message's first tile can start before the arena start.
+  auto unpack = [&](const u32x4 (&d)[2]) {
+    TileDesc t;
+    t.tile_end = ((u64)__builtin_amdgcn_readfirstlane(d[0][1]) << 32) | __builtin_amdgcn_readfirstlane(d[0][0]);
+    t.msg_start = ((u64)__builtin_amdgcn_readfirstlane(d[0][3]) << 32) | __builtin_amdgcn_readfirstlane(d[0][2]);
+    t.msg = __builtin_amdgcn_readfirstlane(d[1][0]);
+    t.after = __builtin_amdgcn_readfirstlane(d[1][1]);
+    t.seed = __builtin_amdgcn_readfirstlane(d[1][2]);
+    t.pad = 0;
+    return t;
+  };
+  // Issue the loads of this lane's line for tile descriptor d. Positions are signed: a
+  // message's first tile can start before the arena start. Every lane issues all 9 loads
+  // unconditionally (a load in a divergent branch would make hipcc drain with vmcnt(0));
+  // blocks holding no byte of the message are redirected to the block of the message's
+  // first byte and zeroed at use.
   auto load_line = [&](const TileDesc& d, LineState& L) {
     const i64 line_start = (i64)d.tile_end - 8192 + (i64)lane * 128;
     const i64 a0 = line_start & ~(i64)15;
     const i64 s = (i64)d.msg_start;
+    const i64 safe = s & ~(i64)15;
     const bool mis = (d.tile_end & 15) != 0;
-    const bool partial = (i64)d.tile_end - 8192 < s;  // first tile of its message
 #pragma unroll
     for (int b = 0; b < 9; b++) {
       const i64 blk = a0 + 16 * b;
-      // only blocks that hold at least one byte of the message are ever read
-      const bool need = (b < 8 || mis) && (!partial || blk + 16 > s);
-      if (need) L.d[b] = *reinterpret_cast<const u32x4*>(base + blk);
-      else L.d[b] = u32x4{0, 0, 0, 0};
+      // block 8 exists only for misaligned lines (an aligned line's 9th block lies past it,
+      // past the message end for the message's last line)
+      const bool need = (b < 8 || mis) && blk + 16 > s;
+      const i64 src = need ? blk : safe;
+      L.d[b] = *reinterpret_cast<const u32x4*>(base + src);
     }
+    __builtin_amdgcn_sched_barrier(0);
   };
 
-  // descriptors run two tiles ahead of the compute, line loads one tile ahead
-  TileDesc dcur = get_desc(0);
-  TileDesc dnext = nk > 1 ? get_desc(1) : dcur;
-  LineState cur;
-  load_line(dcur, cur);
   u32 part[4] = {0, 0, 0, 0};
   u32 gmsg[4] = {0, 0, 0, 0}, gafter[4] = {0, 0, 0, 0};
   u32 gfirst = 0;  // bit t: tile t of the group is its message's first tile
-  for (u64 k = 0; k < nk; k++) {
-    const bool more = k + 1 < nk;
-    const TileDesc dnext2 = (k + 2 < nk) ? get_desc(k + 2) : dnext;
-    LineState nxt;
-    if (more) load_line(dnext, nxt);
-    // ---- compute the current tile's line CRC
+
+  auto process = [&](LineState& cur, const TileDesc& dcur, u64 k) {
     const i64 tile_start = (i64)dcur.tile_end - 8192;
     const i64 line_start = tile_start + (i64)lane * 128;
     const i64 s = (i64)dcur.msg_start;
-    const bool partial = tile_start < s;
+    const bool partial = tile_start < s;  // wave-uniform
     const bool active = line_start + 128 > s;
-    u32 crc = 0;
+    u32 crc;
     if (partial) {
-      // zero every byte below the message start, seed the first line with zinv[r]
+      // zero every byte below the message start (this also clears redirected blocks),
+      // seed the first line with zinv[r]
       const i64 a0 = line_start & ~(i64)15;
 #pragma unroll
       for (int b = 0; b < 9; b++) {
@@ -203,10 +225,9 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
           cur.d[b][x] &= keep;
         }
       }
-      if (active && line_start <= s) crc = zinv[s - line_start];
-    } else if (lane == 0 && line_start == s) {
-      crc = zinv[0];
     }
+    // the line holding the message's first byte starts from zinv[r] (precomputed seed)
+    crc = (active && line_start <= s) ? dcur.seed : 0u;
     const u32 mis = (u32)(dcur.tile_end & 15);
     const u32 m3 = mis & 3;
     switch (mis >> 2) {  // wave-uniform
@@ -228,14 +249,14 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
       }
     gfirst = (partial || tile_start == s) ? (gfirst | (1u << t)) : (gfirst & ~(1u << t));
 
-    if (t == 3 || !more) {
+    if (t == 3 || k + 1 == nk) {
 #pragma unroll
       for (int tt = 0; tt < 4; tt++) lds_st(xb + tt * 256 + lane * 4, part[tt]);
       wave_lds_sync();
       const int T = lane >> 4, q = lane & 15;
-      const u32x4 s = lds_ld4(xb + T * 256 + q * 16);  // lines 4q..4q+3 of group tile T
-      const u32 a = opmul(sbase, kOpZ128 + 0, s[0]) ^ s[1];
-      const u32 b = opmul(sbase, kOpZ128 + 0, s[2]) ^ s[3];
+      const u32x4 sv = lds_ld4(xb + T * 256 + q * 16);  // lines 4q..4q+3 of group tile T
+      const u32 a = opmul(sbase, kOpZ128 + 0, sv[0]) ^ sv[1];
+      const u32 b = opmul(sbase, kOpZ128 + 0, sv[2]) ^ sv[3];
       u32 c = opmul(sbase, kOpZ128 + 1, a) ^ b;               // 512 B
       c = opmul(sbase, kOpZ128 + 2, c) ^ __shfl_down(c, 1);   // 1 KiB
       c = opmul(sbase, kOpZ128 + 3, c) ^ __shfl_down(c, 2);   // 2 KiB
@@ -261,17 +282,60 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
       }
       wave_lds_sync();
     }
-    if (more) {
-      dcur = dnext;
-      dnext = dnext2;
-      cur = nxt;
-    }
+  };
+
+  // Prologue: table loads, then descriptors 0 and 1 and tile 0's line loads, then the LDS
+  // stores and the barrier (tile 0's latency hides behind the fill).
+  LdsFill<WG, kOpZTile + kNumTileOps> fill;
+  fill.load(gtab, gops);
+  u32x4 dA[2], dB[2];
+  fetch_desc(0, dA);
+  fetch_desc(1, dB);
+  TileDesc dcur = unpack(dA);
+  LineState A, B;
+  load_line(dcur, A);
+  fill.store(sbase);
+  __syncthreads();
+  if (nk == 0) return;
+
+  // Ping-pong line buffers, loop unrolled by two; descriptors two tiles ahead.
+  for (u64 k = 0; k < nk; k += 2) {
+    const TileDesc d1 = unpack(dB);   // tile k+1 (clamped)
+    fetch_desc(k + 2, dA);            // tile k+2
+    load_line(d1, B);
+    process(A, dcur, k);
+    if (k + 1 >= nk) break;
+    const TileDesc d2 = unpack(dA);   // tile k+2
+    fetch_desc(k + 3, dB);            // tile k+3
+    load_line(d2, A);
+    process(B, d1, k + 1);
+    dcur = d2;
   }
 }
 
-template __global__ void crc32_ragged_kernel<768>(const uint8_t*, const u64*, const u64*, const u64*, u64,
-                                                  const TileDesc*, const u32*, const u32*, const u32*, const u32*,
-                                                  u32, u32*);
+
+template <int WG>
+__global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restrict__ base,
+                                                          const u64* __restrict__ offsets,
+                                                          const u64* __restrict__ lengths,
+                                                          const u64* __restrict__ tile_base, u64 count,
+                                                          const TileDesc* __restrict__ desc,
+                                                          const u32* __restrict__ overflow,
+                                                          const u32* __restrict__ gtab, const u32* __restrict__ gops,
+                                                          const u32* __restrict__ zinv, u32 final_xor,
+                                                          u32* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) u32 smem[];
+  const u32 sbase = (u32)(uintptr_t)smem;
+  // Precomputed descriptors unless the batch had more tiles than the workspace holds
+  // (overlapping messages); then every tile is located by binary search.
+  if (*overflow == 0u)
+    ragged_body<WG, true>(base, offsets, lengths, tile_base, count, desc, overflow, gtab, gops, zinv, final_xor, out,
+                          sbase);
+  else
+    ragged_body<WG, false>(base, offsets, lengths, tile_base, count, desc, overflow, gtab, gops, zinv, final_xor, out,
+                           sbase);
+}
+
 template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, const u64*, const u64*, u64,
                                                   const TileDesc*, const u32*, const u32*, const u32*, const u32*,
                                                   u32, u32*);

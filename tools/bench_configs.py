@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""Device-resident throughput of every BASELINE config through the production C ABI
+(one JSON line per config). Not the driver's headline (that is bench.py, config B);
+these are the secondary numbers recorded in DESIGN.md.
+
+  C: 1 Mi ragged messages, 64 B - 1 MiB (~110 GiB), 64-B aligned packing (and --unaligned)
+  D: 256 x 64 MiB
+  E: one GPU's shard of 8 Mi x 4 KiB (1 Mi messages = 4 GiB, ids r, r+8, ...)
+The whole call (tile prep kernels + CRC kernel) is timed with HIP events; every run is
+checked against tests/golden/configs.json (CRC-list SHA-256) where the fixture covers it.
+"""
+import argparse
+import hashlib
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+from subspace_amd import gpu, synth  # noqa: E402
+
+GOLD = json.loads((ROOT / "tests" / "golden" / "configs.json").read_text())
+
+
+def u64t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(dev)
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def report(name, nbytes, ms, crcs, gold_key, extra=None):
+    ok = None
+    if gold_key:
+        ok = hashlib.sha256(crcs.astype("<u4").tobytes()).hexdigest() == GOLD[gold_key]["sha256_le_u32"]
+    line = {"config": name, "bytes": int(nbytes), "ms": round(ms, 4), "GiBps": round(nbytes / ms / 1e-3 / 2**30, 1),
+            "TBps": round(nbytes / ms / 1e9, 3), "pct_of_8TBps": round(100 * nbytes / ms / 1e9 / 8000, 1),
+            "bitexact_vs_golden": ok}
+    if extra:
+        line.update(extra)
+    print(json.dumps(line), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C,D,E")
+    ap.add_argument("--iters", type=int, default=5)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    ctx = gpu.CrcContext(0)
+    for cfg in args.configs.split(","):
+        if cfg in ("C", "Cu"):
+            lengths = synth.ragged_lengths(synth.SEED_C, GOLD["C"]["count"])
+            offsets, total = synth.packed_offsets(lengths, 1 if cfg == "Cu" else 64)
+            buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+            d_off, d_len = u64t(offsets, dev), u64t(lengths, dev)
+            gpu.fill_ragged(buf, d_off, d_len, seed=synth.SEED_C)
+            out = torch.empty(len(lengths), dtype=torch.int32, device=dev)
+            ms = timed(lambda: ctx.crc32_ragged(buf, d_off, d_len, out), args.iters)
+            report("C" + (" unaligned" if cfg == "Cu" else ""), int(lengths.sum()), ms,
+                   out.cpu().numpy().view(np.uint32), "C", {"messages": len(lengths)})
+            del buf, d_off, d_len, out
+        elif cfg == "D":
+            n, L = GOLD["D"]["count"], 64 << 20
+            buf = torch.empty(n * L, dtype=torch.uint8, device=dev)
+            gpu.fill_uniform(buf, L, L, n, seed=synth.SEED_D)
+            offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
+            lens = np.full(n, L, dtype=np.uint64)
+            d_off, d_len = u64t(offs, dev), u64t(lens, dev)
+            out = torch.empty(n, dtype=torch.int32, device=dev)
+            ms = timed(lambda: ctx.crc32_ragged(buf, d_off, d_len, out), args.iters)
+            report("D", n * L, ms, out.cpu().numpy().view(np.uint32), "D", {"messages": n})
+            ms_u = timed(lambda: ctx.crc32_uniform(buf, L, L, n, out), args.iters)
+            report("D via batch_uniform", n * L, ms_u, out.cpu().numpy().view(np.uint32), "D")
+            del buf, d_off, d_len, out
+        elif cfg == "E":
+            n, G = GOLD["E"]["count"], 8
+            per = n // G
+            buf = torch.empty(per * 4096, dtype=torch.uint8, device=dev)
+            gpu.fill_uniform(buf, 4096, 4096, per, seed=synth.SEED_E, first_id=0, id_stride=G)
+            out = torch.empty(per, dtype=torch.int32, device=dev)
+            ms = timed(lambda: ctx.crc32_uniform(buf, 4096, 4096, per, out), args.iters * 4)
+            report("E shard (1 of 8)", per * 4096, ms, out.cpu().numpy().view(np.uint32), None,
+                   {"messages": per})
+            del buf, out
+        torch.cuda.empty_cache()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -23,9 +23,12 @@ stop_if_fault() {  # $1 = exit status, $2 = step name
 for s in $STEPS; do
   case $s in
     test)
-      timeout -k 10 1200 python -m pytest tests/ -q -m gpu -p no:cacheprovider --timeout 600 -rf \
+      timeout -k 10 1200 python -m pytest tests/ -x -q -m gpu -p no:cacheprovider --timeout 600 -rf \
         > "$OUT/pytest_gpu.log" 2>&1
-      stop_if_fault $? test ;;
+      rc=$?
+      # any failed GPU test ends the session: a fault must not be followed by more GPU work
+      if [ $rc -ne 0 ]; then echo "step test rc=$rc (stop)" >> "$OUT/status.txt"; exit $rc; fi
+      stop_if_fault $rc test ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
       stop_if_fault $? smoke ;;
@@ -44,6 +47,10 @@ for s in $STEPS; do
           --no-e2e > "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.json" 2> "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.err")
         stop_if_fault $? "pmc_$ctr"
       done ;;
+    configs)
+      timeout -k 10 600 python tools/bench_configs.py --configs C,Cu,D,E > "$OUT/configs.log" 2>&1
+      rc=$?
+      if [ $rc -ne 0 ]; then echo "step configs rc=$rc (stop)" >> "$OUT/status.txt"; exit $rc; fi ;;
     *)
       echo "unknown step $s" >> "$OUT/status.txt" ;;
   esac
