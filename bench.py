@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="budget for the CPU baseline legs")
+    ap.add_argument("--event-every", type=int, default=1,
+                    help="bracket every N-th launch of the timed region with HIP events (kernel duration)")
     ap.add_argument("--workload", default="B", choices=["B", "E"],
                     help="B: 65,536 x 4 KiB per GPU per step (weak scaling, default); "
                          "E: 8 Mi x 4 KiB sharded round-robin over the GPUs (strong scaling) + RCCL gather")
@@ -145,15 +147,20 @@ def main():
     torch.cuda.synchronize()
 
     # ---- timed region: K steps, barrier + sync on both sides, max over ranks
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    every = max(1, args.event_every)
+    ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for i in range(0, args.steps, every)}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
+        e = ev.get(i)
+        if e:
+            e[0].record(stream)
         step(i)
-        ev[i][1].record(stream)
+        if e:
+            e[1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -162,7 +169,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_ms = [a.elapsed_time(b) for a, b in ev.values()]
     avg_kern_ms = float(np.mean(kern_ms))
 
     # ---- bit-exactness of what was timed. B at world 1: batch 0 is exactly config B.

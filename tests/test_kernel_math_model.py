@@ -1,0 +1,150 @@
+"""CPU model of the kernels' CRC decomposition (the algebra, not the HIP code):
+the ragged kernel's end-aligned virtual lines, zero-masked first line seeded with
+zinv[r], per-tile tree, Z_{8192*T} shift and XOR combine; the uniform kernel's per-line
+CRCs and transposed tree. Each must equal the reference CRC (zlib) bit for bit."""
+import zlib
+
+import numpy as np
+import pytest
+
+M32 = 0xFFFFFFFF
+POLY = 0xEDB88320
+TABLE = []
+for b in range(256):
+    c = b
+    for _ in range(8):
+        c = (c >> 1) ^ POLY if c & 1 else c >> 1
+    TABLE.append(c)
+
+
+def crc_raw(c, data):
+    for x in data:
+        c = (c >> 8) ^ TABLE[(c ^ x) & 0xFF]
+    return c
+
+
+def apply(m, v):
+    r = 0
+    i = 0
+    while v:
+        if v & 1:
+            r ^= m[i]
+        v >>= 1
+        i += 1
+    return r
+
+
+def mul(a, b):
+    return [apply(a, col) for col in b]
+
+
+Z1 = [((1 << i) >> 8) ^ TABLE[(1 << i) & 0xFF] for i in range(32)]
+IDENT = [1 << i for i in range(32)]
+
+
+def zbytes(n):
+    r, p = IDENT, Z1
+    while n:
+        if n & 1:
+            r = mul(p, r)
+        p = mul(p, p)
+        n >>= 1
+    return r
+
+
+def inverse(m):
+    rows = [sum(((m[c] >> r) & 1) << c for c in range(32)) for r in range(32)]
+    inv = [1 << r for r in range(32)]
+    for c in range(32):
+        p = next(i for i in range(c, 32) if (rows[i] >> c) & 1)
+        rows[c], rows[p] = rows[p], rows[c]
+        inv[c], inv[p] = inv[p], inv[c]
+        for r in range(32):
+            if r != c and (rows[r] >> c) & 1:
+                rows[r] ^= rows[c]
+                inv[r] ^= inv[c]
+    return [sum(((inv[r] >> c) & 1) << r for r in range(32)) for c in range(32)]
+
+
+ZINV1 = inverse(Z1)
+ZTREE = [zbytes(128 << k) for k in range(6)]
+ZTILE = [zbytes(8192 << k) for k in range(8)]
+
+
+def ragged_model(buf: bytes, s: int, L: int, init: int) -> int:
+    e = s + L
+    if L == 0:
+        return init
+    zinv = []
+    v = init
+    for _ in range(128):
+        zinv.append(v)
+        v = apply(ZINV1, v)
+    nt = (L + 8191) >> 13
+    out = 0
+    for j in range(nt):
+        tile_end = e - ((nt - 1 - j) << 13)
+        tile_start = tile_end - 8192
+        lines = []
+        for lane in range(64):
+            ls = tile_start + 128 * lane
+            if ls + 128 <= s:
+                lines.append(0)
+                continue
+            data = bytes(buf[max(ls, 0):ls + 128]) if ls >= 0 else bytes(-ls) + bytes(buf[0:ls + 128])
+            data = bytearray(data)
+            for i in range(128):  # zero bytes below the message start
+                if ls + i < s:
+                    data[i] = 0
+            seed = zinv[s - ls] if ls <= s else 0
+            lines.append(crc_raw(seed, data))
+        # tree: level k combines pairs 2^k lines apart with Z_{128*2^k}
+        cur = lines
+        for k in range(6):
+            cur = [apply(ZTREE[k], cur[2 * i]) ^ cur[2 * i + 1] for i in range(len(cur) // 2)]
+        t = cur[0]
+        after = nt - 1 - j
+        k = 0
+        while after:
+            if after & 1:
+                t = apply(ZTILE[k], t)
+            after >>= 1
+            k += 1
+        out ^= t
+    return out
+
+
+def uniform_model(msg: bytes, init: int) -> int:
+    assert len(msg) == 4096
+    lines = [crc_raw(init if i == 0 else 0, msg[128 * i:128 * i + 128]) for i in range(32)]
+    # lane q holds lines 4q..4q+3: a = Z128(s0)^s1, b = Z128(s2)^s3, c = Z256(a)^b
+    quads = []
+    for q in range(8):
+        s0, s1, s2, s3 = lines[4 * q:4 * q + 4]
+        a = apply(ZTREE[0], s0) ^ s1
+        b = apply(ZTREE[0], s2) ^ s3
+        quads.append(apply(ZTREE[1], a) ^ b)
+    cur = quads
+    for k in (2, 3, 4):
+        cur = [apply(ZTREE[k], cur[2 * i]) ^ cur[2 * i + 1] for i in range(len(cur) // 2)]
+    return cur[0]
+
+
+def ref(state, data):
+    return (~zlib.crc32(bytes(data), (~state) & M32)) & M32
+
+
+@pytest.mark.parametrize("init", [M32, 0, 0x12345678])
+def test_uniform_decomposition(init):
+    rng = np.random.default_rng(init & 0xFFFF)
+    msg = rng.integers(0, 256, 4096, dtype=np.uint8).tobytes()
+    assert uniform_model(msg, init) == ref(init, msg)
+
+
+@pytest.mark.parametrize("s,L", [(0, 1), (0, 100), (3, 128), (5, 129), (16, 8192), (7, 8191), (1, 8193),
+                                 (100, 20000), (0, 3 * 8192), (13, 2 * 8192 + 300)])
+def test_ragged_decomposition(s, L):
+    rng = np.random.default_rng(s * 7 + L)
+    buf = rng.integers(0, 256, s + L + 64, dtype=np.uint8).tobytes()
+    for init in (M32, 0xA5A5A5A5):
+        assert ragged_model(buf, s, L, init) == ref(init, buf[s:s + L]), (s, L, hex(init))

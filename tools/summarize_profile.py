@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Summarise a GPU session's rocprofv3 output into profiles/<tag>/.
+
+  python tools/summarize_profile.py <session-dir> <tag>
+
+Reads <session-dir>/prof/run_kernel_stats.csv (--kernel-trace --stats) and the separate
+PMC passes <session-dir>/pmc_FETCH_SIZE/, pmc_WRITE_SIZE/ (one counter per pass), and writes
+  profiles/<tag>/kernel_stats.csv        copy of the rocprofv3 summary
+  profiles/<tag>/summary.md              per-kernel averages + HBM traffic per launch
+  profiles/traffic_uniform4k.json        read by bench.py (roofline.traffic)
+
+HBM bytes per launch follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane) streaming read, so it is
+doubled; WRITE_SIZE is exact for 16-B stores and uncalibrated for our 4-B result stores
+(4 B per message, 0.1 % of the traffic), reported as measured.
+"""
+import csv
+import json
+import shutil
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def per_dispatch(pmc_dir: Path, counter: str):
+    f = pmc_dir / "run_counter_collection.csv"
+    if not f.exists():
+        return {}
+    vals = defaultdict(float)
+    names = {}
+    for r in csv.DictReader(open(f)):
+        if r["Counter_Name"] != counter:
+            continue
+        key = r["Dispatch_Id"]
+        vals[key] += float(r["Counter_Value"])
+        names[key] = r["Kernel_Name"]
+    by_kernel = defaultdict(list)
+    for k, v in vals.items():
+        by_kernel[names[k]].append(v)
+    return by_kernel
+
+
+def main():
+    sess, tag = Path(sys.argv[1]), sys.argv[2]
+    out = ROOT / "profiles" / tag
+    out.mkdir(parents=True, exist_ok=True)
+    stats = sess / "prof" / "run_kernel_stats.csv"
+    rows = list(csv.DictReader(open(stats))) if stats.exists() else []
+    if stats.exists():
+        shutil.copy(stats, out / "kernel_stats.csv")
+    fetch = per_dispatch(sess / "pmc_FETCH_SIZE", "FETCH_SIZE")
+    write = per_dispatch(sess / "pmc_WRITE_SIZE", "WRITE_SIZE")
+    lines = [f"# rocprofv3 summary ({tag})", "",
+             f"Source: `{sess}` (rocprofv3 --kernel-trace --stats; PMC FETCH_SIZE and WRITE_SIZE in separate passes).",
+             "", "| kernel | calls | avg us | min us | max us |", "|---|---|---|---|---|"]
+    for r in rows:
+        lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
+                     f"{float(r['MinNs']) / 1e3:.2f} | {float(r['MaxNs']) / 1e3:.2f} |")
+    lines += ["", "| kernel | dispatches | FETCH_SIZE KiB/launch (raw) | HBM read bytes/launch (x2, gfx950) | "
+              "WRITE_SIZE KiB/launch |", "|---|---|---|---|---|"]
+    traffic = {}
+    for name, v in fetch.items():
+        # drop the first dispatches (warm-up) when there are enough
+        vv = v[2:] if len(v) > 4 else v
+        f_kib = sum(vv) / len(vv)
+        w = write.get(name, [])
+        ww = w[2:] if len(w) > 4 else w
+        w_kib = sum(ww) / len(ww) if ww else float("nan")
+        rd = 2 * f_kib * 1024
+        lines.append(f"| `{name[:90]}` | {len(v)} | {f_kib:.0f} | {rd:.4g} | {w_kib:.0f} |")
+        if "crc32_uniform4k_kernel" in name:
+            traffic = {"kernel": name, "fetch_size_kib_per_launch": f_kib, "write_size_kib_per_launch": w_kib,
+                       "hbm_bytes_per_launch": rd + (w_kib * 1024 if w_kib == w_kib else 0.0),
+                       "hbm_read_bytes_per_launch": rd, "algorithmic_bytes_per_launch": 65536 * 4096,
+                       "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount, MI355X_MICROARCH.md HBM)",
+                       "source": f"profiles/{tag}"}
+    (out / "summary.md").write_text("\n".join(lines) + "\n")
+    if traffic:
+        (ROOT / "profiles" / "traffic_uniform4k.json").write_text(json.dumps(traffic, indent=1) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
