@@ -73,6 +73,62 @@ int subspace_crc32_batch(subspace_crc_ctx* ctx, const void* dev_base, uint64_t a
                          const uint64_t* dev_offsets, const uint64_t* dev_lengths, uint64_t count, uint32_t init,
                          uint32_t flags, uint32_t* dev_out, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * Message slots: the reference's full 3-span checksum (common/channel.h:527-542),
+ * computed and stored (publisher) or verified (subscriber) for a batch of slots.
+ *
+ * A slot's 64-B MessagePrefix (common/channel.h:88-112) and its checksum extension live
+ * at `prefix`; its payload is the `message_size` bytes at `payload`. For each slot:
+ *   span 0 = prefix[4, 48)                      (slot_id .. metadata_size, 44 B)
+ *   span 1 = prefix[48 + checksum_size, +metadata_size)   (user metadata)
+ *   span 2 = payload[0, message_size)
+ *   crc    = ~SubspaceCRC32 chained over the spans from 0xFFFFFFFF (client/checksum.h:29-37)
+ * SUBSPACE_CRC_SLOT_CALCULATE (client/publisher.cc:664-675): sets kMessageHasChecksum (4)
+ *   in prefix->flags (before the CRC, as SetHasChecksum() does), then stores crc as a
+ *   native-endian uint32 at prefix+48 (the first 4 B of the checksum area).
+ * SUBSPACE_CRC_SLOT_VERIFY (client/client.cc:1346-1356, client/checksum.h:39-47): a slot
+ *   whose prefix has kMessageHasChecksum is compared on the first 4 B of its checksum
+ *   area; a slot without the flag is not checked.
+ * Prefixes must be 8-B aligned (MessagePrefix holds int64 fields); payloads may have any
+ * alignment. Prefix and payload bytes outside the spans (the padding word at offset 0,
+ * checksum bytes 4.., padding after the metadata) are neither covered nor modified.
+ * --------------------------------------------------------------------------------- */
+#define SUBSPACE_CRC_SLOT_CALCULATE 0u
+#define SUBSPACE_CRC_SLOT_VERIFY 1u
+
+/* per-slot status written to dev_status (when not NULL) */
+#define SUBSPACE_CRC_SLOT_OK 0u        /* checksum stored (CALCULATE) or matched (VERIFY) */
+#define SUBSPACE_CRC_SLOT_MISMATCH 1u  /* VERIFY: "Checksum verification failed" (client/client.cc:1447) */
+#define SUBSPACE_CRC_SLOT_UNCHECKED 2u /* VERIFY: prefix has no kMessageHasChecksum flag */
+
+/* One slot: device addresses of its MessagePrefix and payload, and the payload size
+ * (slot->message_size at publish, the delivered size at read). 24 B, device array. */
+typedef struct subspace_crc_slot {
+  uint64_t prefix;
+  uint64_t payload;
+  uint64_t message_size;
+} subspace_crc_slot;
+
+/* Slot list (any placement, e.g. split buffers). max_message_size bounds every
+ * message_size (the channel's slot size); it sizes the workspace only -- a larger
+ * message is still handled, through a slower tile search.
+ * dev_status: optional uint32[count]. dev_error_count: optional uint32, set to the number
+ * of SUBSPACE_CRC_SLOT_MISMATCH slots of this call. */
+int subspace_crc32_slots(subspace_crc_ctx* ctx, const subspace_crc_slot* dev_slots, uint64_t count,
+                         uint64_t max_message_size, int32_t checksum_size, int32_t metadata_size, uint32_t mode,
+                         uint32_t* dev_status, uint32_t* dev_error_count, void* stream);
+
+/* Contiguous channel layout (client/client_channel.h:122-172): slot i's prefix is at
+ * dev_buffer + i*slot_stride (slot_stride = PrefixSize + Aligned<64>(SlotSize)), its
+ * payload at prefix + ComputePrefixSize(checksum_size, metadata_size)
+ * (= Aligned<64>(48 + checksum_size + metadata_size), common/channel.h:914-919).
+ * Payload sizes: dev_message_sizes[i] (uint64) when not NULL, else `message_size` for
+ * every slot. */
+int subspace_crc32_slots_strided(subspace_crc_ctx* ctx, void* dev_buffer, uint64_t slot_stride, uint64_t count,
+                                 uint64_t message_size, const uint64_t* dev_message_sizes, int32_t checksum_size,
+                                 int32_t metadata_size, uint32_t mode, uint32_t* dev_status,
+                                 uint32_t* dev_error_count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

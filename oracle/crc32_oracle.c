@@ -96,6 +96,50 @@ void oracle_message_spans(const uint8_t* prefix, const uint8_t* payload, size_t 
   lengths_out[2] = message_size;
 }
 
+/* Publisher side of one slot (client/publisher.cc:664-675): SetHasChecksum() on the
+ * prefix flags (int64 at offset 32, kMessageHasChecksum = 4, common/channel.h:65), then
+ * CalculateCRC32Checksum over GetMessageChecksumData's spans into the checksum area. */
+void oracle_publish_slot(uint8_t* prefix, const uint8_t* payload, size_t message_size, int32_t checksum_size,
+                         int32_t metadata_size) {
+  int64_t flags;
+  memcpy(&flags, prefix + 32, 8);
+  flags |= 4;
+  memcpy(prefix + 32, &flags, 8);
+  const uint8_t* spans[3];
+  size_t lens[3];
+  oracle_message_spans(prefix, payload, message_size, checksum_size, metadata_size, spans, lens);
+  oracle_calculate_checksum(spans, lens, 3, prefix + 48);
+}
+
+/* Subscriber side (client/client.cc:1346-1356): 2 = no kMessageHasChecksum flag (not
+ * checked), else 0 = VerifyCRC32Checksum passed, 1 = "Checksum verification failed". */
+int oracle_verify_slot(const uint8_t* prefix, const uint8_t* payload, size_t message_size, int32_t checksum_size,
+                       int32_t metadata_size) {
+  int64_t flags;
+  memcpy(&flags, prefix + 32, 8);
+  if (!(flags & 4)) return 2;
+  const uint8_t* spans[3];
+  size_t lens[3];
+  oracle_message_spans(prefix, payload, message_size, checksum_size, metadata_size, spans, lens);
+  return oracle_verify_checksum(spans, lens, 3, prefix + 48) ? 0 : 1;
+}
+
+/* Slot batches over one host buffer: slot i's prefix at base + prefix_off[i], payload at
+ * base + payload_off[i], sizes[i] payload bytes. */
+void oracle_publish_slots(uint8_t* base, const uint64_t* prefix_off, const uint64_t* payload_off,
+                          const uint64_t* sizes, size_t n, int32_t checksum_size, int32_t metadata_size) {
+  for (size_t i = 0; i < n; i++)
+    oracle_publish_slot(base + prefix_off[i], base + payload_off[i], (size_t)sizes[i], checksum_size, metadata_size);
+}
+
+void oracle_verify_slots(const uint8_t* base, const uint64_t* prefix_off, const uint64_t* payload_off,
+                         const uint64_t* sizes, size_t n, int32_t checksum_size, int32_t metadata_size,
+                         uint32_t* status) {
+  for (size_t i = 0; i < n; i++)
+    status[i] = (uint32_t)oracle_verify_slot(base + prefix_off[i], base + payload_off[i], (size_t)sizes[i],
+                                             checksum_size, metadata_size);
+}
+
 /* ------------------------------------------------------------------ batch */
 typedef struct {
   const uint8_t* base;

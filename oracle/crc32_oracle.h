@@ -18,6 +18,15 @@ int oracle_verify_checksum(const uint8_t* const* spans, const size_t* lengths, s
 void oracle_message_spans(const uint8_t* prefix, const uint8_t* payload, size_t message_size,
                           int32_t checksum_size, int32_t metadata_size, const uint8_t** spans_out,
                           size_t* lengths_out);
+void oracle_publish_slot(uint8_t* prefix, const uint8_t* payload, size_t message_size, int32_t checksum_size,
+                         int32_t metadata_size);
+int oracle_verify_slot(const uint8_t* prefix, const uint8_t* payload, size_t message_size, int32_t checksum_size,
+                       int32_t metadata_size);
+void oracle_publish_slots(uint8_t* base, const uint64_t* prefix_off, const uint64_t* payload_off,
+                          const uint64_t* sizes, size_t n, int32_t checksum_size, int32_t metadata_size);
+void oracle_verify_slots(const uint8_t* base, const uint64_t* prefix_off, const uint64_t* payload_off,
+                         const uint64_t* sizes, size_t n, int32_t checksum_size, int32_t metadata_size,
+                         uint32_t* status);
 void oracle_crc32_batch(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, size_t n,
                         uint32_t init, uint32_t* out, int nthreads);
 

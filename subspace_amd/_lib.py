@@ -24,6 +24,8 @@ EXPORTED_SYMBOLS = (
     "subspace_crc_ctx_reserve",
     "subspace_crc32_batch_uniform",
     "subspace_crc32_batch",
+    "subspace_crc32_slots",
+    "subspace_crc32_slots_strided",
 )
 
 _lib = None
@@ -59,6 +61,11 @@ def load() -> ctypes.CDLL:
     lib.subspace_crc32_batch_uniform.argtypes = [vp, vp, u64, u64, u64, u32, u32, vp, vp]
     lib.subspace_crc32_batch.restype = i32
     lib.subspace_crc32_batch.argtypes = [vp, vp, u64, vp, vp, u64, u32, u32, vp, vp]
+    lib.subspace_crc32_slots.restype = i32
+    lib.subspace_crc32_slots.argtypes = [vp, vp, u64, u64, ctypes.c_int32, ctypes.c_int32, u32, vp, vp, vp]
+    lib.subspace_crc32_slots_strided.restype = i32
+    lib.subspace_crc32_slots_strided.argtypes = [vp, vp, u64, u64, u64, vp, ctypes.c_int32, ctypes.c_int32, u32,
+                                                 vp, vp, vp]
     lib.subspace_crc_testutil_fill_uniform.restype = i32
     lib.subspace_crc_testutil_fill_uniform.argtypes = [vp, u64, u64, u64, u64, u64, u64, vp]
     lib.subspace_crc_testutil_fill_ragged.restype = i32

@@ -20,11 +20,15 @@ template <int WG>
 __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
 
 struct TileDesc;
-__global__ void crc32_ragged_count_kernel(const u64*, u64, u32, u32, u64*, u32*);
-__global__ void crc32_ragged_desc_kernel(const u64*, const u64*, const u64*, const u32*, u64, u64, TileDesc*, u32*);
+__global__ void crc32_ragged_count_kernel(const u64*, u32, u64, u32, u32, u64*, u32*);
+__global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, const u32*, u64, u64, TileDesc*,
+                                         u32*);
 template <int WG>
-__global__ void crc32_ragged_kernel(const uint8_t*, const u64*, const u64*, const u64*, u64, const TileDesc*,
-                                    const u32*, const u32*, const u32*, const u32*, u32, u32*);
+__global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
+                                    const TileDesc*, const u32*, const u32*, const u32*, const u32*, u32, u32*);
+__global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, int, int, u32, const u32*,
+                                         const u32*, const u32*, u32*, u32*);
+__global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*);
 hipError_t ragged_scan(void* temp, size_t& temp_bytes, const u64* in, u64* out, u64 n, hipStream_t stream);
 __global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* offsets, u64* lengths);
 
@@ -62,6 +66,7 @@ struct subspace_crc_ctx {
   int num_cus = 256;
   u32* d_tab = nullptr;  // 4 x 256 slice tables
   u32* d_ops = nullptr;  // kNumOps nibble operators
+  u32* d_pow2 = nullptr;  // Z_{2^k}, k = 0..63, nibble operators (slot checksums)
   // zinv[r] = Z_r^{-1}(init), r = 0..127, cached per init value
   std::unordered_map<u32, u32*> zinv;
   Tables host_tab;
@@ -81,6 +86,9 @@ struct subspace_crc_ctx {
   u64* d_uoff = nullptr;  // offsets/lengths materialised for non-4K uniform batches
   u64* d_ulen = nullptr;
   u64 u_capacity = 0;
+  u32* d_crc0 = nullptr;  // slot batches: payload CRCs from init 0
+  u64* d_soff = nullptr;  // slot batches: payload offsets of the contiguous layout
+  u64 s_capacity = 0;
 };
 
 namespace {
@@ -140,6 +148,64 @@ int grid_for(subspace_crc_ctx* c, u64 work_units, int waves_per_block) {
   return (int)(blocks ? blocks : 1);
 }
 
+// Ragged path: per-message tile counts -> scan -> tile descriptors -> main kernel.
+// Offsets/lengths are read with element strides (1 = plain arrays, 3 = slot records).
+// `cap` sizes the descriptor workspace; a batch with more tiles takes the search path.
+int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* offsets, u32 ostride, const u64* lengths,
+               u32 lstride, u64 count, u32 init, u32 final_xor, u32* out, hipStream_t st) {
+  const u32* zinv;
+  int rc = get_zinv(c, init, &zinv);
+  if (rc) return rc;
+  rc = ensure_ragged_ws(c, count, cap);
+  if (rc) return rc;
+  const u64 n1 = count + 1;
+  crc32_ragged_count_kernel<<<(unsigned)((n1 + 255) / 256), 256, 0, st>>>(lengths, lstride, count, init, final_xor,
+                                                                           c->d_ntiles, out);
+  HIP_TRY(hipGetLastError());
+  size_t tmp = c->scan_tmp_bytes;
+  HIP_TRY(ragged_scan(c->d_scan_tmp, tmp, c->d_ntiles, c->d_tbase, n1, st));
+  crc32_ragged_desc_kernel<<<(unsigned)((cap + 255) / 256), 256, 0, st>>>(
+      offsets, ostride, lengths, lstride, c->d_tbase, zinv, count, cap, reinterpret_cast<TileDesc*>(c->d_desc),
+      c->d_overflow);
+  HIP_TRY(hipGetLastError());
+  const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU
+  crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, lds_bytes(kRaggedWG / 64), st>>>(
+      base, offsets, ostride, lengths, lstride, c->d_tbase, count, reinterpret_cast<const TileDesc*>(c->d_desc),
+      c->d_overflow, c->d_tab, c->d_ops, zinv, final_xor, out);
+  HIP_TRY(hipGetLastError());
+  return SUBSPACE_CRC_OK;
+}
+
+int ensure_slot_ws(subspace_crc_ctx* c, u64 count) {
+  if (count <= c->s_capacity) return SUBSPACE_CRC_OK;
+  (void)hipFree(c->d_crc0);
+  (void)hipFree(c->d_soff);
+  c->d_crc0 = nullptr;
+  c->d_soff = nullptr;
+  c->s_capacity = 0;
+  HIP_TRY(hipMalloc(&c->d_crc0, count * sizeof(u32)));
+  HIP_TRY(hipMalloc(&c->d_soff, count * sizeof(u64)));
+  c->s_capacity = count;
+  return SUBSPACE_CRC_OK;
+}
+
+int check_slot_args(int32_t checksum_size, int32_t metadata_size, uint32_t mode) {
+  if (mode != SUBSPACE_CRC_SLOT_CALCULATE && mode != SUBSPACE_CRC_SLOT_VERIFY)
+    return fail(SUBSPACE_CRC_EINVAL, "unknown slot mode %u", mode);
+  if (checksum_size < 4) return fail(SUBSPACE_CRC_EINVAL, "checksum_size %d < 4", checksum_size);
+  if (metadata_size < 0) return fail(SUBSPACE_CRC_EINVAL, "metadata_size %d < 0", metadata_size);
+  return SUBSPACE_CRC_OK;
+}
+
+int slot_finish(subspace_crc_ctx* c, const u64* slots, uint8_t* buf, u64 stride, const u64* sizes, u64 usize,
+                u64 count, int32_t cs, int32_t ms, u32 mode, u32* status, u32* err, hipStream_t st) {
+  if (err) HIP_TRY(hipMemsetAsync(err, 0, sizeof(u32), st));
+  crc32_slot_finish_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(
+      slots, buf, stride, sizes, usize, count, cs, ms, mode, c->d_crc0, c->d_tab, c->d_pow2, status, err);
+  HIP_TRY(hipGetLastError());
+  return SUBSPACE_CRC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -168,15 +234,22 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
   c->host_tab = make_tables();
   c->zinv1 = inverse(z_one(c->host_tab));
 
-  std::vector<u32> tab(1024), ops((size_t)kNumOps * 128, 0u);
+  std::vector<u32> tab(1024), ops((size_t)kNumOps * 128, 0u), pow2(64 * 128, 0u);
   for (int k = 0; k < 4; k++)
     for (int b = 0; b < 256; b++) tab[k * 256 + b] = c->host_tab.t[k][b];
   for (int k = 0; k < 6; k++) nibble_tables(z_bytes(c->host_tab, 128ull << k), &ops[(size_t)(kOpZ128 + k) * 128]);
   for (int k = 0; k < kNumTileOps; k++)
     nibble_tables(z_bytes(c->host_tab, 8192ull << k), &ops[(size_t)(kOpZTile + k) * 128]);
 
+  {
+    Mat32 z = z_one(c->host_tab);
+    for (int k = 0; k < 64; k++, z = mul(z, z)) nibble_tables(z, &pow2[(size_t)k * 128]);
+  }
+
   hipError_t e = hipMalloc(&c->d_tab, tab.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_ops, ops.size() * 4);
+  if (e == hipSuccess) e = hipMalloc(&c->d_pow2, pow2.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(c->d_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_ops, ops.data(), ops.size() * 4, hipMemcpyHostToDevice);
 #define SET_LDS(WGV)                                                                                   \
@@ -200,7 +273,10 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   if (!c) return;
   (void)hipFree(c->d_tab);
   (void)hipFree(c->d_ops);
-  for (auto& kv : c->zinv) hipFree(kv.second);
+  (void)hipFree(c->d_pow2);
+  (void)hipFree(c->d_crc0);
+  (void)hipFree(c->d_soff);
+  for (auto& kv : c->zinv) (void)hipFree(kv.second);
   (void)hipFree(c->d_ntiles);
   (void)hipFree(c->d_tbase);
   (void)hipFree(c->d_scan_tmp);
@@ -234,31 +310,11 @@ int subspace_crc32_batch(subspace_crc_ctx* c, const void* dev_base, uint64_t are
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
   const u32 final_xor = (flags & SUBSPACE_CRC_FINALIZE) ? 0xFFFFFFFFu : 0u;
-  const u32* zinv;
-  int rc = get_zinv(c, init, &zinv);
-  if (rc) return rc;
   // Tile capacity: exact for non-overlapping messages inside the arena; if the device
   // finds more tiles (overlapping messages) the kernel falls back to per-tile search.
   const u64 cap = arena_bytes / 8192 + count + 1;
-  rc = ensure_ragged_ws(c, count, cap);
-  if (rc) return rc;
-
-  const u64 n1 = count + 1;
-  crc32_ragged_count_kernel<<<(unsigned)((n1 + 255) / 256), 256, 0, st>>>(dev_lengths, count, init, final_xor,
-                                                                           c->d_ntiles, dev_out);
-  HIP_TRY(hipGetLastError());
-  size_t tmp = c->scan_tmp_bytes;
-  HIP_TRY(ragged_scan(c->d_scan_tmp, tmp, c->d_ntiles, c->d_tbase, n1, st));
-  const u64 desc_threads = cap;
-  crc32_ragged_desc_kernel<<<(unsigned)((desc_threads + 255) / 256), 256, 0, st>>>(
-      dev_offsets, dev_lengths, c->d_tbase, zinv, count, cap, reinterpret_cast<TileDesc*>(c->d_desc), c->d_overflow);
-  HIP_TRY(hipGetLastError());
-  const int blocks = c->num_cus;  // persistent: one 12-wave workgroup per CU
-  crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, lds_bytes(kRaggedWG / 64), st>>>(
-      static_cast<const uint8_t*>(dev_base), dev_offsets, dev_lengths, c->d_tbase, count,
-      reinterpret_cast<const TileDesc*>(c->d_desc), c->d_overflow, c->d_tab, c->d_ops, zinv, final_xor, dev_out);
-  HIP_TRY(hipGetLastError());
-  return SUBSPACE_CRC_OK;
+  return ragged_run(c, static_cast<const uint8_t*>(dev_base), cap, dev_offsets, 1, dev_lengths, 1, count, init,
+                    final_xor, dev_out, st);
 }
 
 int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint64_t stride, uint64_t length,
@@ -310,6 +366,74 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
   HIP_TRY(hipGetLastError());
   const u64 arena = stride * (count - 1) + length;
   return subspace_crc32_batch(c, dev_base, arena, c->d_uoff, c->d_ulen, count, init, flags, dev_out, stream);
+}
+
+int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots, uint64_t count,
+                         uint64_t max_message_size, int32_t checksum_size, int32_t metadata_size, uint32_t mode,
+                         uint32_t* dev_status, uint32_t* dev_error_count, void* stream) {
+  g_err[0] = 0;
+  if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  int rc = check_slot_args(checksum_size, metadata_size, mode);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (count == 0) {
+    if (dev_error_count) HIP_TRY(hipMemsetAsync(dev_error_count, 0, sizeof(u32), st));
+    return SUBSPACE_CRC_OK;
+  }
+  if (!dev_slots) return fail(SUBSPACE_CRC_EINVAL, "null device pointer");
+  if (count >= (1ull << 32)) return fail(SUBSPACE_CRC_EINVAL, "count %llu exceeds 2^32-1", (unsigned long long)count);
+  HIP_TRY(hipSetDevice(c->device));
+  rc = ensure_slot_ws(c, count);
+  if (rc) return rc;
+  // payload CRCs from init 0 at absolute addresses (base 0; fields 1 and 2 of each record)
+  const u64* rec = reinterpret_cast<const u64*>(dev_slots);
+  const u64 cap = count * ((max_message_size + 8191) / 8192) + 1;
+  rc = ragged_run(c, nullptr, cap, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st);
+  if (rc) return rc;
+  return slot_finish(c, rec, nullptr, 0, nullptr, 0, count, checksum_size, metadata_size, mode, dev_status,
+                     dev_error_count, st);
+}
+
+int subspace_crc32_slots_strided(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stride, uint64_t count,
+                                 uint64_t message_size, const uint64_t* dev_message_sizes, int32_t checksum_size,
+                                 int32_t metadata_size, uint32_t mode, uint32_t* dev_status,
+                                 uint32_t* dev_error_count, void* stream) {
+  g_err[0] = 0;
+  if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  int rc = check_slot_args(checksum_size, metadata_size, mode);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (count == 0) {
+    if (dev_error_count) HIP_TRY(hipMemsetAsync(dev_error_count, 0, sizeof(u32), st));
+    return SUBSPACE_CRC_OK;
+  }
+  if (!dev_buffer) return fail(SUBSPACE_CRC_EINVAL, "null device pointer");
+  if (((uintptr_t)dev_buffer % 8) || (slot_stride % 8))
+    return fail(SUBSPACE_CRC_EINVAL, "prefixes must be 8-B aligned (buffer %p, stride %llu)", dev_buffer,
+                (unsigned long long)slot_stride);
+  if (count >= (1ull << 32)) return fail(SUBSPACE_CRC_EINVAL, "count %llu exceeds 2^32-1", (unsigned long long)count);
+  // ComputePrefixSize (common/channel.h:914-919)
+  const u64 prefix_size = ((u64)(48 + checksum_size + metadata_size) + 63) & ~63ull;
+  if (!dev_message_sizes && slot_stride < prefix_size + message_size && count > 1)
+    return fail(SUBSPACE_CRC_EINVAL, "slot_stride %llu < prefix %llu + message %llu",
+                (unsigned long long)slot_stride, (unsigned long long)prefix_size, (unsigned long long)message_size);
+  HIP_TRY(hipSetDevice(c->device));
+  rc = ensure_slot_ws(c, count);
+  if (rc) return rc;
+  auto* buf = static_cast<uint8_t*>(dev_buffer);
+  if (dev_message_sizes) {
+    slot_payload_offsets_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(slot_stride, prefix_size, count,
+                                                                                c->d_soff);
+    HIP_TRY(hipGetLastError());
+    const u64 cap = (slot_stride * count) / 8192 + count + 1;
+    rc = ragged_run(c, buf, cap, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st);
+  } else {
+    rc = subspace_crc32_batch_uniform(c, buf + prefix_size, slot_stride, message_size, count, 0u, 0u, c->d_crc0,
+                                      stream);
+  }
+  if (rc) return rc;
+  return slot_finish(c, nullptr, buf, slot_stride, dev_message_sizes, message_size, count, checksum_size,
+                     metadata_size, mode, dev_status, dev_error_count, st);
 }
 
 // Tuning hook for experiments (not part of the public header): uniform-kernel workgroup

@@ -37,6 +37,11 @@ constexpr int kNumTileOps = 21;
 typedef __attribute__((address_space(3))) u32 lds_u32_t;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
 
+// v_readfirstlane as an unsigned dword (the builtin returns int: widening it directly to
+// 64 bits would sign-extend the low half of a byte offset >= 2 GiB)
+__device__ __forceinline__ u32 rfl(u32 v) { return (u32)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ u64 rfl64(u32 lo, u32 hi) { return ((u64)rfl(hi) << 32) | (u64)rfl(lo); }
+
 __device__ __forceinline__ u32 lds_ld(u32 addr) { return *reinterpret_cast<const lds_u32_t*>((uintptr_t)addr); }
 __device__ __forceinline__ void lds_st(u32 addr, u32 v) { *reinterpret_cast<lds_u32_t*>((uintptr_t)addr) = v; }
 __device__ __forceinline__ u32x4 lds_ld4(u32 addr) { return *reinterpret_cast<const lds_u32x4_t*>((uintptr_t)addr); }

@@ -44,15 +44,17 @@ __host__ __device__ inline u64 tiles_for_length(u64 len) { return (len + 8191) >
 
 // Per message: tile count; zero-length messages get their (constant) result here,
 // multi-tile messages get their output word zeroed for the tiles' atomicXor.
-__global__ void crc32_ragged_count_kernel(const u64* __restrict__ lengths, u64 count, u32 init, u32 final_xor,
-                                          u64* __restrict__ ntiles, u32* __restrict__ out) {
+// `lengths` (and `offsets` below) are read with an element stride (1 for plain arrays, 3 for
+// the lengths/payload fields of subspace_crc_slot records).
+__global__ void crc32_ragged_count_kernel(const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
+                                          u32 final_xor, u64* __restrict__ ntiles, u32* __restrict__ out) {
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (i > count) return;
   if (i == count) {
     ntiles[i] = 0;  // scan sentinel: tile_base[count] = total tiles
     return;
   }
-  const u64 len = lengths[i];
+  const u64 len = lengths[i * lstride];
   const u64 nt = tiles_for_length(len);
   ntiles[i] = nt;
   if (nt == 0) out[i] = init ^ final_xor;
@@ -70,13 +72,13 @@ __device__ inline u64 find_msg(const u64* __restrict__ tile_base, u64 count, u64
   return lo;
 }
 
-__device__ inline TileDesc make_desc(const u64* __restrict__ offsets, const u64* __restrict__ lengths,
-                                     const u64* __restrict__ tile_base, const u32* __restrict__ zinv, u64 m,
-                                     u64 tau) {
+__device__ inline TileDesc make_desc(const u64* __restrict__ offsets, u32 ostride, const u64* __restrict__ lengths,
+                                     u32 lstride, const u64* __restrict__ tile_base, const u32* __restrict__ zinv,
+                                     u64 m, u64 tau) {
   const u64 nt = tile_base[m + 1] - tile_base[m];
   const u64 j = tau - tile_base[m];
-  const u64 s = offsets[m];
-  const u64 e = s + lengths[m];
+  const u64 s = offsets[m * ostride];
+  const u64 e = s + lengths[m * lstride];
   TileDesc d;
   d.tile_end = e - ((nt - 1 - j) << 13);
   d.msg_start = s;
@@ -92,14 +94,15 @@ __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, const u64*
 }
 
 // Per tile (up to `capacity`): its descriptor. Sets *overflow if the batch has more tiles.
-__global__ void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, const u64* __restrict__ lengths,
+__global__ void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, u32 ostride,
+                                         const u64* __restrict__ lengths, u32 lstride,
                                          const u64* __restrict__ tile_base, const u32* __restrict__ zinv, u64 count,
                                          u64 capacity, TileDesc* __restrict__ desc, u32* __restrict__ overflow) {
   const u64 total = tile_base[count];
   const u64 tau = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (tau == 0) *overflow = total > capacity ? 1u : 0u;
   if (tau >= total || tau >= capacity) return;
-  desc[tau] = make_desc(offsets, lengths, tile_base, zinv, find_msg(tile_base, count, tau), tau);
+  desc[tau] = make_desc(offsets, ostride, lengths, lstride, tile_base, zinv, find_msg(tile_base, count, tau), tau);
 }
 
 // ------------------------------------------------------------------ main kernel
@@ -128,8 +131,8 @@ __device__ __forceinline__ u32 crc_line(const LineState& L, u32 crc, u32 m3, u32
 
 template <int WG, bool DESC>
 __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
-                                                          const u64* __restrict__ offsets,
-                                                          const u64* __restrict__ lengths,
+                                                          const u64* __restrict__ offsets, u32 ostride,
+                                                          const u64* __restrict__ lengths, u32 lstride,
                                                           const u64* __restrict__ tile_base, u64 count,
                                                           const TileDesc* __restrict__ desc,
                                                           const u32* __restrict__ overflow,
@@ -137,7 +140,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
                                                           const u32* __restrict__ zinv, u32 final_xor,
                                                           u32* __restrict__ out, u32 sbase) {
   const int lane = threadIdx.x & 63;
-  const u32 wid = (u32)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 wid = rfl(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
   const u32 xb = sbase + kLdsXpose + wid * kLdsXposePerWave;
@@ -161,18 +164,19 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
       d[0] = p[0];
       d[1] = p[1];
     } else {
-      const TileDesc t = make_desc(offsets, lengths, tile_base, zinv, find_msg(tile_base, count, tau), tau);
+      const TileDesc t =
+          make_desc(offsets, ostride, lengths, lstride, tile_base, zinv, find_msg(tile_base, count, tau), tau);
       d[0] = u32x4{(u32)t.tile_end, (u32)(t.tile_end >> 32), (u32)t.msg_start, (u32)(t.msg_start >> 32)};
       d[1] = u32x4{t.msg, t.after, t.seed, 0u};
     }
   };
   auto unpack = [&](const u32x4 (&d)[2]) {
     TileDesc t;
-    t.tile_end = ((u64)__builtin_amdgcn_readfirstlane(d[0][1]) << 32) | __builtin_amdgcn_readfirstlane(d[0][0]);
-    t.msg_start = ((u64)__builtin_amdgcn_readfirstlane(d[0][3]) << 32) | __builtin_amdgcn_readfirstlane(d[0][2]);
-    t.msg = __builtin_amdgcn_readfirstlane(d[1][0]);
-    t.after = __builtin_amdgcn_readfirstlane(d[1][1]);
-    t.seed = __builtin_amdgcn_readfirstlane(d[1][2]);
+    t.tile_end = rfl64(d[0][0], d[0][1]);
+    t.msg_start = rfl64(d[0][2], d[0][3]);
+    t.msg = rfl(d[1][0]);
+    t.after = rfl(d[1][1]);
+    t.seed = rfl(d[1][2]);
     t.pad = 0;
     return t;
   };
@@ -316,8 +320,8 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
 
 template <int WG>
 __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restrict__ base,
-                                                          const u64* __restrict__ offsets,
-                                                          const u64* __restrict__ lengths,
+                                                          const u64* __restrict__ offsets, u32 ostride,
+                                                          const u64* __restrict__ lengths, u32 lstride,
                                                           const u64* __restrict__ tile_base, u64 count,
                                                           const TileDesc* __restrict__ desc,
                                                           const u32* __restrict__ overflow,
@@ -329,14 +333,14 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
   // Precomputed descriptors unless the batch had more tiles than the workspace holds
   // (overlapping messages); then every tile is located by binary search.
   if (*overflow == 0u)
-    ragged_body<WG, true>(base, offsets, lengths, tile_base, count, desc, overflow, gtab, gops, zinv, final_xor, out,
+    ragged_body<WG, true>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, overflow, gtab, gops, zinv, final_xor, out,
                           sbase);
   else
-    ragged_body<WG, false>(base, offsets, lengths, tile_base, count, desc, overflow, gtab, gops, zinv, final_xor, out,
+    ragged_body<WG, false>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, overflow, gtab, gops, zinv, final_xor, out,
                            sbase);
 }
 
-template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, const u64*, const u64*, u64,
+template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
                                                   const TileDesc*, const u32*, const u32*, const u32*, const u32*,
                                                   u32, u32*);
 

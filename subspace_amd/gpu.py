@@ -14,6 +14,11 @@ from . import _lib
 
 FINALIZE = 0x1  # SUBSPACE_CRC_FINALIZE: store ~crc (the checksum CalculateCRC32Checksum writes)
 
+# message-slot checksums (include/subspace_crc.h)
+SLOT_CALCULATE = 0  # publisher: set kMessageHasChecksum, store the 3-span checksum in the prefix
+SLOT_VERIFY = 1     # subscriber: check the stored checksum of slots that carry the flag
+SLOT_OK, SLOT_MISMATCH, SLOT_UNCHECKED = 0, 1, 2
+
 
 class CrcError(RuntimeError):
     pass
@@ -83,6 +88,35 @@ class CrcContext:
             self._h, _ptr(buf), arena, _ptr(offsets), _ptr(lengths), n, init & 0xFFFFFFFF,
             FINALIZE if finalize else 0, _ptr(out), _stream_ptr(stream)), "subspace_crc32_batch")
 
+
+    def crc32_slots(self, slots, *, max_message_size: int, checksum_size: int = 4, metadata_size: int = 0,
+                    mode: int = SLOT_CALCULATE, status=None, error_count=None, stream=None) -> None:
+        """3-span checksums of a slot list. ``slots`` is an int64 device tensor of shape (n, 3):
+        (prefix address, payload address, message_size) per slot -- subspace_crc_slot records."""
+        if slots.dim() != 2 or slots.shape[1] != 3 or not slots.is_contiguous():
+            raise ValueError("slots must be a contiguous (n, 3) int64 tensor")
+        n = int(slots.shape[0])
+        if status is not None and int(status.numel()) < n:
+            raise ValueError("status is shorter than the slot list")
+        _check(self._lib.subspace_crc32_slots(
+            self._h, _ptr(slots), n, max_message_size, checksum_size, metadata_size, mode,
+            _ptr(status) if status is not None else None, _ptr(error_count) if error_count is not None else None,
+            _stream_ptr(stream)), "subspace_crc32_slots")
+
+    def crc32_slots_strided(self, buf, slot_stride: int, count: int, *, message_size: int = 0, sizes=None,
+                            checksum_size: int = 4, metadata_size: int = 0, mode: int = SLOT_CALCULATE,
+                            status=None, error_count=None, base_offset: int = 0, stream=None) -> None:
+        """3-span checksums of ``count`` slots laid out contiguously from buf[base_offset:]
+        (prefix at i*slot_stride, payload after ComputePrefixSize bytes)."""
+        if status is not None and int(status.numel()) < count:
+            raise ValueError("status is shorter than the slot count")
+        if sizes is not None and int(sizes.numel()) < count:
+            raise ValueError("sizes is shorter than the slot count")
+        _check(self._lib.subspace_crc32_slots_strided(
+            self._h, _ptr(buf) + base_offset, slot_stride, count, message_size,
+            _ptr(sizes) if sizes is not None else None, checksum_size, metadata_size, mode,
+            _ptr(status) if status is not None else None, _ptr(error_count) if error_count is not None else None,
+            _stream_ptr(stream)), "subspace_crc32_slots_strided")
 
 # ---------------------------------------------------------------- synthetic inputs (device)
 def fill_uniform(buf, stride: int, length: int, count: int, *, seed: int, first_id: int = 0, id_stride: int = 1,

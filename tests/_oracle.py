@@ -36,6 +36,24 @@ class Oracle:
         lib.oracle_synth_crc_batch.argtypes = [u64, vp, vp, sz, u32, vp, ctypes.c_int]
         lib.oracle_ragged_length.restype = u64
         lib.oracle_ragged_length.argtypes = [u64, u64]
+        lib.oracle_publish_slots.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int32, ctypes.c_int32]
+        lib.oracle_verify_slots.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int32, ctypes.c_int32, vp]
+
+    def publish_slots(self, host: np.ndarray, prefix_off, payload_off, sizes, checksum_size: int,
+                      metadata_size: int) -> None:
+        """Publisher checksum (flag + 3-span CRC into the prefix) for every slot, in place."""
+        assert host.dtype == np.uint8 and host.flags.c_contiguous
+        po, yo, sz = (np.ascontiguousarray(a, dtype=np.uint64) for a in (prefix_off, payload_off, sizes))
+        self.lib.oracle_publish_slots(host.ctypes.data, po.ctypes.data, yo.ctypes.data, sz.ctypes.data, len(po),
+                                      checksum_size, metadata_size)
+
+    def verify_slots(self, host: np.ndarray, prefix_off, payload_off, sizes, checksum_size: int,
+                     metadata_size: int) -> np.ndarray:
+        po, yo, sz = (np.ascontiguousarray(a, dtype=np.uint64) for a in (prefix_off, payload_off, sizes))
+        st = np.zeros(len(po), dtype=np.uint32)
+        self.lib.oracle_verify_slots(host.ctypes.data, po.ctypes.data, yo.ctypes.data, sz.ctypes.data, len(po),
+                                     checksum_size, metadata_size, st.ctypes.data)
+        return st
 
     def table(self) -> list[int]:
         t = self.lib.oracle_table()

@@ -1,0 +1,175 @@
+"""GPU parity of the message-slot checksums (subspace_crc32_slots / _slots_strided).
+
+A channel buffer is built on the host (prefix fields as a publisher fills them, random
+metadata and padding, random payloads), copied to the device, published (CALCULATE) by
+the HIP path and by the oracle's publisher restatement on the host copy; the two buffers
+must be byte-identical (only the flag and the checksum word change). VERIFY statuses
+after targeted corruptions must equal the oracle's subscriber restatement.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from subspace_amd import gpu, slots  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def build_channel(count, slot_size, cs, ms, sizes, seed):
+    ps = slots.compute_prefix_size(cs, ms)
+    stride = slots.slot_stride(slot_size, cs, ms)
+    rng = np.random.default_rng(seed)
+    host = rng.integers(0, 256, stride * count, dtype=np.uint8)
+    host.reshape(count, stride)[:, :ps] = slots.make_prefixes(count, sizes, checksum_size=cs, metadata_size=ms,
+                                                              seed=seed + 1)
+    return host, ps, stride
+
+
+def offsets(count, stride, ps):
+    po = np.arange(count, dtype=np.uint64) * np.uint64(stride)
+    return po, po + np.uint64(ps)
+
+
+def publish_strided(ctx, host, stride, count, cs, ms, sizes=None, message_size=0):
+    dev = torch.from_numpy(host).to(DEV)
+    status = torch.full((count,), 7, dtype=torch.int32, device=DEV)
+    d_sizes = None if sizes is None else torch.from_numpy(np.asarray(sizes, dtype=np.int64)).to(DEV)
+    ctx.crc32_slots_strided(dev, stride, count, message_size=message_size, sizes=d_sizes, checksum_size=cs,
+                            metadata_size=ms, mode=gpu.SLOT_CALCULATE, status=status)
+    torch.cuda.synchronize()
+    return dev, status.cpu().numpy()
+
+
+@pytest.mark.parametrize("cs,ms", [(4, 0), (4, 16), (20, 32), (8, 5)])
+def test_publish_uniform_4k(gpu_ctx, oracle, cs, ms):
+    count = 1500
+    sizes = np.full(count, 4096, dtype=np.uint64)
+    host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=cs * 100 + ms)
+    dev, status = publish_strided(gpu_ctx, host, stride, count, cs, ms, message_size=4096)
+    po, yo = offsets(count, stride, ps)
+    oracle.publish_slots(host, po, yo, sizes, cs, ms)
+    assert (status == 0).all()
+    got = dev.cpu().numpy()
+    bad = np.nonzero(got != host)[0]
+    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]} (stride {stride})"
+
+
+@pytest.mark.parametrize("slot_size,cs,ms", [(256, 4, 16), (5000, 20, 32), (70000, 4, 0)])
+def test_publish_ragged_sizes(gpu_ctx, oracle, slot_size, cs, ms):
+    count = 700
+    rng = np.random.default_rng(slot_size)
+    sizes = rng.integers(0, slot_size + 1, count).astype(np.uint64)
+    sizes[:3] = [0, 1, slot_size]
+    host, ps, stride = build_channel(count, slot_size, cs, ms, sizes, seed=slot_size + cs)
+    dev, status = publish_strided(gpu_ctx, host, stride, count, cs, ms, sizes=sizes)
+    po, yo = offsets(count, stride, ps)
+    oracle.publish_slots(host, po, yo, sizes, cs, ms)
+    assert (status == 0).all()
+    assert np.array_equal(dev.cpu().numpy(), host)
+
+
+def test_publish_slot_list_split_buffers(gpu_ctx, oracle):
+    """subspace_crc32_slots: prefixes in one allocation, payloads in another at unaligned
+    addresses, slots in shuffled order (split buffers, client_channel.h:126-129)."""
+    count, cs, ms = 900, 4, 24
+    ps = slots.compute_prefix_size(cs, ms)
+    rng = np.random.default_rng(5)
+    sizes = rng.integers(0, 20000, count).astype(np.uint64)
+    pre_host = slots.make_prefixes(count, sizes, checksum_size=cs, metadata_size=ms, seed=6).reshape(-1).copy()
+    gaps = rng.integers(0, 40, count).astype(np.uint64)
+    pay_off = np.concatenate([[0], np.cumsum(sizes + gaps)[:-1]]).astype(np.uint64) + np.uint64(3)
+    pay_host = rng.integers(0, 256, int(pay_off[-1] + sizes[-1] + 64), dtype=np.uint8)
+    d_pre = torch.from_numpy(pre_host).to(DEV)
+    d_pay = torch.from_numpy(pay_host).to(DEV)
+    order = rng.permutation(count)
+    rec = slots.slot_records(d_pre.data_ptr() + order.astype(np.uint64) * np.uint64(ps),
+                             d_pay.data_ptr() + pay_off[order], sizes[order])
+    d_rec = torch.from_numpy(rec.view(np.int64)).to(DEV)
+    status = torch.full((count,), 7, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_slots(d_rec, max_message_size=20000, checksum_size=cs, metadata_size=ms,
+                        mode=gpu.SLOT_CALCULATE, status=status)
+    torch.cuda.synchronize()
+    # oracle over one host arena holding both buffers
+    arena = np.concatenate([pre_host, pay_host])
+    oracle.publish_slots(arena, np.arange(count, dtype=np.uint64) * np.uint64(ps),
+                         pay_off + np.uint64(len(pre_host)), sizes, cs, ms)
+    assert (status.cpu().numpy() == 0).all()
+    assert np.array_equal(d_pre.cpu().numpy(), arena[:len(pre_host)])
+    assert np.array_equal(d_pay.cpu().numpy(), pay_host)  # payloads untouched
+
+
+def test_verify_statuses(gpu_ctx, oracle):
+    count, slot_size, cs, ms = 2000, 4096, 4, 16
+    sizes = np.full(count, 4096, dtype=np.uint64)
+    sizes[1::7] = np.arange(len(sizes[1::7])) % 4097
+    host, ps, stride = build_channel(count, slot_size, cs, ms, sizes, seed=77)
+    po, yo = offsets(count, stride, ps)
+    oracle.publish_slots(host, po, yo, sizes, cs, ms)
+    rng = np.random.default_rng(78)
+    kinds = rng.integers(0, 8, count)
+    for i, k in enumerate(kinds):
+        b = int(po[i])
+        n = int(sizes[i])
+        if k == 1 and n:
+            host[b + ps + rng.integers(0, n)] ^= np.uint8(1 << rng.integers(0, 8))  # payload bit flip
+        elif k == 2:
+            host[b + 48 + cs + rng.integers(0, ms)] ^= 0x10  # metadata
+        elif k == 3:
+            host[b + 4 + rng.integers(0, 44)] ^= 0x01  # span 0 (any field)
+        elif k == 4:
+            host[b + 48 + rng.integers(0, 4)] ^= 0x80  # stored checksum
+        elif k == 5:
+            host[b:b + 4] ^= 0xFF  # padding word: not covered
+            host[b + 48 + cs + ms:b + ps] ^= 0xAA  # prefix padding: not covered
+        elif k == 6:
+            host[b + 32] &= 0xFB  # no kMessageHasChecksum: not checked
+    want = oracle.verify_slots(host, po, yo, sizes, cs, ms)
+    assert set(np.unique(want)) == {0, 1, 2}
+    dev = torch.from_numpy(host).to(DEV)
+    d_sizes = torch.from_numpy(sizes.view(np.int64)).to(DEV)
+    status = torch.full((count,), 7, dtype=torch.int32, device=DEV)
+    err = torch.full((1,), 12345, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_slots_strided(dev, stride, count, sizes=d_sizes, checksum_size=cs, metadata_size=ms,
+                                mode=gpu.SLOT_VERIFY, status=status, error_count=err)
+    torch.cuda.synchronize()
+    got = status.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)
+    assert int(err.item()) == int((want == 1).sum())
+    assert np.array_equal(dev.cpu().numpy(), host)  # verify never writes the channel
+
+
+def test_verify_roundtrip_uniform_fast_path(gpu_ctx):
+    """CALCULATE then VERIFY on the device: every slot passes; one flipped bit fails exactly one."""
+    count, cs, ms = 65536, 4, 0
+    sizes = np.full(count, 4096, dtype=np.uint64)
+    host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=9)
+    dev = torch.from_numpy(host).to(DEV)
+    status = torch.zeros(count, dtype=torch.int32, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_slots_strided(dev, stride, count, message_size=4096, mode=gpu.SLOT_CALCULATE)
+    gpu_ctx.crc32_slots_strided(dev, stride, count, message_size=4096, mode=gpu.SLOT_VERIFY, status=status,
+                                error_count=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0 and int(status.abs().sum().item()) == 0
+    dev[12345 * stride + ps + 777] ^= 4
+    gpu_ctx.crc32_slots_strided(dev, stride, count, message_size=4096, mode=gpu.SLOT_VERIFY, status=status,
+                                error_count=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 1
+    assert np.nonzero(status.cpu().numpy())[0].tolist() == [12345]
+
+
+def test_empty_and_errors(gpu_ctx):
+    err = torch.full((1,), 9, dtype=torch.int32, device=DEV)
+    buf = torch.zeros(4160, dtype=torch.uint8, device=DEV)
+    gpu_ctx.crc32_slots_strided(buf, 4160, 0, message_size=4096, mode=gpu.SLOT_VERIFY, error_count=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    with pytest.raises(gpu.CrcError):
+        gpu_ctx.crc32_slots_strided(buf, 4160, 1, message_size=4096, mode=5)
+    with pytest.raises(gpu.CrcError):
+        gpu_ctx.crc32_slots_strided(buf, 4160, 1, message_size=4096, checksum_size=2)
+    with pytest.raises(gpu.CrcError):
+        gpu_ctx.crc32_slots_strided(buf, 4164, 2, message_size=4096)  # prefixes not 8-B aligned

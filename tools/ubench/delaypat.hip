@@ -75,13 +75,20 @@ int main() {
   u32* out; CK(hipMalloc(&out, 64ull << 20));
   gen<<<4096, 256>>>(buf, n16);
   CK(hipDeviceSynchronize());
-  auto rep = [&](const char* nm, float ms) { printf("%-36s %7.3f ms %6.2f TB/s\n", nm, ms, bytes / (ms * 1e-3) / 1e12); fflush(stdout); };
-#define R(WG, D, S) rep("wg" #WG " depth" #D " sleep" #S, time_it([&] { delaypat<WG, D, S><<<256, WG>>>(buf, ntiles, out); }, 5))
+  u64 cur_bytes = bytes, cur_tiles = ntiles;
+  auto rep = [&](const char* nm, float ms) { printf("%-28s %5llu MiB %8.1f us %6.2f TB/s\n", nm, cur_bytes >> 20, ms * 1e3, cur_bytes / (ms * 1e-3) / 1e12); fflush(stdout); };
+  // each launch reads the next cur_bytes window of the 4 GiB buffer (rotation defeats the 256 MB MALL)
+  u64 rot = 0;
+  auto win = [&]() { const u64 nwin = bytes / cur_bytes; return buf + ((rot++ % nwin) * (cur_bytes / 16)); };
+#define R(WG, D, S) rep("wg" #WG " depth" #D " sleep" #S, time_it([&] { delaypat<WG, D, S><<<256, WG>>>(win(), cur_tiles, out); }, 32))
   // sleep 24 x ~64 cycles ~= 1500 cycles ~ the CRC's per-tile compute latency
   R(512, 1, 0); R(512, 1, 24); R(512, 2, 24); R(512, 3, 24);
   R(768, 1, 24); R(768, 2, 24);
   R(1024, 1, 24); R(1024, 2, 24);
   R(256, 2, 24); R(256, 3, 24);
   R(512, 1, 48); R(512, 2, 48); R(1024, 1, 48); R(1024, 2, 48);
+  // the bench's batch size (256 MiB): fixed per-launch cost shows here
+  cur_bytes = 256ull << 20; cur_tiles = cur_bytes / 8192;
+  R(512, 1, 0); R(512, 1, 24); R(512, 2, 24); R(768, 1, 24); R(1024, 1, 24); R(1024, 2, 24); R(256, 3, 24);
   return 0;
 }
