@@ -16,7 +16,7 @@
 
 namespace subspace_amd {
 
-template <int WG>
+template <int WG, int DEPTH>
 __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
 
 struct TileDesc;
@@ -25,7 +25,9 @@ __global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const
                                          u32*);
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
-                                    const TileDesc*, const u32*, const u32*, const u32*, const u32*, u32, u32*);
+                                    const TileDesc*, const u32*, const u32*, const u32*, const u32*, u32, u32*, u32*);
+__global__ void crc32_ragged_final_kernel(const u64*, u64, const u32*, const u32*, u32*);
+hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u32* out, u64 n, hipStream_t stream);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, int, int, u32, const u32*,
                                          const u32*, const u32*, u32*, u32*);
 __global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*);
@@ -78,11 +80,16 @@ struct subspace_crc_ctx {
   size_t scan_tmp_bytes = 0;
   u64 ws_messages = 0;
   uint8_t* d_desc = nullptr;
+  u32* d_tilecrc = nullptr;  // per-tile values (desc_capacity)
+  u32* d_px = nullptr;       // their inclusive XOR-scan
+  void* d_xscan_tmp = nullptr;
+  size_t xscan_tmp_bytes = 0;
   u64 desc_capacity = 0;
   u32* d_overflow = nullptr;
   int uniform_wg = 512;    // workgroup size of the uniform kernel (256/512/640/768/1024)
   int uniform_blocks = 0;  // 0 = one workgroup per CU
-  int uniform_order = 0;   // tile order: 0 sweep, 1 per-workgroup region
+  int uniform_order = 0;   // tile order: 0 XCD-spread sweep, 1 per-workgroup region, 2 plain sweep
+  int uniform_depth = 2;   // tiles in flight per wave while one is processed (1 or 2)
   u64* d_uoff = nullptr;  // offsets/lengths materialised for non-4K uniform batches
   u64* d_ulen = nullptr;
   u64 u_capacity = 0;
@@ -132,9 +139,20 @@ int ensure_ragged_ws(subspace_crc_ctx* c, u64 messages, u64 tiles) {
   }
   if (tiles > c->desc_capacity) {
     (void)hipFree(c->d_desc);
+    (void)hipFree(c->d_tilecrc);
+    (void)hipFree(c->d_px);
+    (void)hipFree(c->d_xscan_tmp);
     c->d_desc = nullptr;
+    c->d_tilecrc = c->d_px = nullptr;
+    c->d_xscan_tmp = nullptr;
     c->desc_capacity = 0;
     HIP_TRY(hipMalloc(&c->d_desc, tiles * kTileDescBytes));
+    HIP_TRY(hipMalloc(&c->d_tilecrc, tiles * sizeof(u32)));
+    HIP_TRY(hipMalloc(&c->d_px, tiles * sizeof(u32)));
+    size_t tmp = 0;
+    HIP_TRY(xor_scan(nullptr, tmp, c->d_tilecrc, c->d_px, tiles, nullptr));
+    HIP_TRY(hipMalloc(&c->d_xscan_tmp, tmp));
+    c->xscan_tmp_bytes = tmp;
     c->desc_capacity = tiles;
   }
   if (!c->d_overflow) HIP_TRY(hipMalloc(&c->d_overflow, 16));
@@ -171,7 +189,14 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU
   crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, lds_bytes(kRaggedWG / 64), st>>>(
       base, offsets, ostride, lengths, lstride, c->d_tbase, count, reinterpret_cast<const TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_tab, c->d_ops, zinv, final_xor, out);
+      c->d_overflow, c->d_tab, c->d_ops, zinv, final_xor, out, c->d_tilecrc);
+  HIP_TRY(hipGetLastError());
+  // message CRC = XOR of its tiles' values = difference of two XOR-scan entries (entries
+  // past the batch's real tile count are scanned but never read)
+  size_t xtmp = c->xscan_tmp_bytes;
+  HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, c->d_px, cap, st));
+  crc32_ragged_final_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(c->d_tbase, count, c->d_px,
+                                                                              c->d_overflow, out);
   HIP_TRY(hipGetLastError());
   return SUBSPACE_CRC_OK;
 }
@@ -252,11 +277,12 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
   if (e == hipSuccess) e = hipMemcpy(c->d_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_ops, ops.data(), ops.size() * 4, hipMemcpyHostToDevice);
-#define SET_LDS(WGV)                                                                                   \
-  if (e == hipSuccess)                                                                                 \
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                            (int)lds_bytes(WGV / 64));
-  SET_LDS(256) SET_LDS(512) SET_LDS(640) SET_LDS(768) SET_LDS(1024)
+#define SET_LDS(WGV, D)                                                                                      \
+  if (e == hipSuccess)                                                                                       \
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV, D>,                                      \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(WGV / 64));
+  SET_LDS(256, 1) SET_LDS(256, 2) SET_LDS(512, 1) SET_LDS(512, 2)
+  SET_LDS(768, 1) SET_LDS(768, 2) SET_LDS(1024, 1) SET_LDS(1024, 2)
 #undef SET_LDS
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_ragged_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -281,6 +307,9 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_tbase);
   (void)hipFree(c->d_scan_tmp);
   (void)hipFree(c->d_desc);
+  (void)hipFree(c->d_tilecrc);
+  (void)hipFree(c->d_px);
+  (void)hipFree(c->d_xscan_tmp);
   (void)hipFree(c->d_overflow);
   (void)hipFree(c->d_uoff);
   (void)hipFree(c->d_ulen);
@@ -337,15 +366,15 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     if (c->uniform_blocks > 0 && (u64)c->uniform_blocks < (u64)blocks) blocks = c->uniform_blocks;
     const auto* b = static_cast<const uint8_t*>(dev_base);
     const int ord = c->uniform_order;
-#define LAUNCH(WGV)                                                                                    \
-  crc32_uniform4k_kernel<WGV><<<blocks, WGV, lds_bytes(WGV / 64), st>>>(b, stride, count, c->d_tab, c->d_ops, init, \
-                                                                        final_xor, dev_out, ord)
+#define LAUNCH(WGV, D)                                                                                 \
+  crc32_uniform4k_kernel<WGV, D><<<blocks, WGV, lds_bytes(WGV / 64), st>>>(b, stride, count, c->d_tab, c->d_ops, \
+                                                                           init, final_xor, dev_out, ord)
+    const bool d2 = c->uniform_depth == 2;
     switch (wg) {
-      case 256: LAUNCH(256); break;
-      case 640: LAUNCH(640); break;
-      case 768: LAUNCH(768); break;
-      case 1024: LAUNCH(1024); break;
-      default: LAUNCH(512); break;
+      case 256: if (d2) LAUNCH(256, 2); else LAUNCH(256, 1); break;
+      case 768: if (d2) LAUNCH(768, 2); else LAUNCH(768, 1); break;
+      case 1024: if (d2) LAUNCH(1024, 2); else LAUNCH(1024, 1); break;
+      default: if (d2) LAUNCH(512, 2); else LAUNCH(512, 1); break;
     }
 #undef LAUNCH
     HIP_TRY(hipGetLastError());
@@ -438,13 +467,15 @@ int subspace_crc32_slots_strided(subspace_crc_ctx* c, void* dev_buffer, uint64_t
 
 // Tuning hook for experiments (not part of the public header): uniform-kernel workgroup
 // size (512/768/1024) and an optional cap on the number of workgroups.
-int subspace_crc_testutil_tune(subspace_crc_ctx* c, int uniform_wg, int uniform_blocks, int uniform_order) {
+int subspace_crc_testutil_tune(subspace_crc_ctx* c, int uniform_wg, int uniform_blocks, int uniform_order,
+                               int uniform_depth) {
   if (!c) return SUBSPACE_CRC_EINVAL;
-  if (uniform_wg != 256 && uniform_wg != 512 && uniform_wg != 640 && uniform_wg != 768 && uniform_wg != 1024)
-    return SUBSPACE_CRC_EINVAL;
+  if (uniform_wg != 256 && uniform_wg != 512 && uniform_wg != 768 && uniform_wg != 1024) return SUBSPACE_CRC_EINVAL;
+  if (uniform_order < 0 || uniform_order > 2 || uniform_depth < 1 || uniform_depth > 2) return SUBSPACE_CRC_EINVAL;
   c->uniform_wg = uniform_wg;
   c->uniform_blocks = uniform_blocks;
   c->uniform_order = uniform_order;
+  c->uniform_depth = uniform_depth;
   return SUBSPACE_CRC_OK;
 }
 

@@ -42,6 +42,15 @@ typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
 __device__ __forceinline__ u32 rfl(u32 v) { return (u32)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ u64 rfl64(u32 lo, u32 hi) { return ((u64)rfl(hi) << 32) | (u64)rfl(lo); }
 
+// Buffer-resource word 3 for raw (unformatted, unswizzled) gfx950 buffer loads.
+constexpr int kBufferRsrcFlags = 0x00020000;
+
+// Position of wave `wid` of workgroup `b` (of G) in a sweep front: consecutive pairs of
+// front slots go to consecutive workgroups, i.e. round-robin over the 8 XCDs.
+__device__ __forceinline__ u64 front_slot(u32 b, u32 G, u32 wid) {
+  return ((u64)b + (u64)G * (wid >> 1)) * 2 + (wid & 1u);
+}
+
 __device__ __forceinline__ u32 lds_ld(u32 addr) { return *reinterpret_cast<const lds_u32_t*>((uintptr_t)addr); }
 __device__ __forceinline__ void lds_st(u32 addr, u32 v) { *reinterpret_cast<lds_u32_t*>((uintptr_t)addr) = v; }
 __device__ __forceinline__ u32x4 lds_ld4(u32 addr) { return *reinterpret_cast<const lds_u32x4_t*>((uintptr_t)addr); }

@@ -17,8 +17,13 @@
 //    tiles after) are precomputed by crc32_ragged_desc_kernel.
 //  * Every 4 tiles the 256 line CRCs are transposed through LDS (16 lanes per tile),
 //    tree-combined (Z_128..Z_4096), multiplied by Z_{8192*T} (T = tiles after this one
-//    in the message, binary decomposition over nibble operators) and written: a plain
-//    store for single-tile messages, atomicXor into a pre-zeroed word otherwise.
+//    in the message, binary decomposition over nibble operators) and stored per tile:
+//    tilecrc[tau]. A message's CRC is the XOR of its tiles' values, i.e. the difference of
+//    two entries of the inclusive XOR-scan of tilecrc (crc32_ragged_final_kernel). No
+//    atomics: huge messages (config D: 8192 tiles each, all in flight at once) would
+//    otherwise serialise every tile on one output word.
+//    (Batches whose tiles overflow the workspace -- overlapping messages -- fall back to
+//    atomicXor into pre-zeroed words.)
 //  * End-aligned lines are 16-B misaligned when e is: each lane then loads the 9
 //    aligned 16-B blocks covering its line and realigns with v_alignbyte_b32 (the
 //    dword shift e&15 >> 2 is wave-uniform, so it is a 4-way uniform switch).
@@ -138,14 +143,15 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
                                                           const u32* __restrict__ overflow,
                                                           const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                           const u32* __restrict__ zinv, u32 final_xor,
-                                                          u32* __restrict__ out, u32 sbase) {
+                                                          u32* __restrict__ out, u32* __restrict__ tilecrc,
+                                                          u32 sbase) {
   const int lane = threadIdx.x & 63;
   const u32 wid = rfl(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
   const u32 xb = sbase + kLdsXpose + wid * kLdsXposePerWave;
   const u64 total = tile_base[count];
-  const u64 w = (u64)blockIdx.x * (WG / 64) + wid;
+  const u64 w = front_slot(blockIdx.x, gridDim.x, wid);  // sweep front slot (crc_device.h)
   const u64 nw = (u64)gridDim.x * (WG / 64);
   const u64 nk = w < total ? (total - w + nw - 1) / nw : 0;  // tiles tau = k*nw + w, k < nk
   if (total == 0) return;  // every message empty: all waves of all blocks leave before any load
@@ -281,8 +287,13 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
       if (q == 0 && valid) {
         const bool first = (gfirst >> T) & 1u;
         const u32 contrib = first ? (c ^ final_xor) : c;
-        if (first && after == 0) out[msg] = contrib;  // single-tile message
-        else atomicXor(&out[msg], contrib);
+        if (DESC) {
+          tilecrc[((k & ~(u64)3) + (u64)T) * nw + w] = contrib;  // tile tau of group slot T
+        } else if (first && after == 0) {
+          out[msg] = contrib;  // single-tile message
+        } else {
+          atomicXor(&out[msg], contrib);
+        }
       }
       wave_lds_sync();
     }
@@ -327,26 +338,47 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
                                                           const u32* __restrict__ overflow,
                                                           const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                           const u32* __restrict__ zinv, u32 final_xor,
-                                                          u32* __restrict__ out) {
+                                                          u32* __restrict__ out, u32* __restrict__ tilecrc) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
   // Precomputed descriptors unless the batch had more tiles than the workspace holds
   // (overlapping messages); then every tile is located by binary search.
   if (*overflow == 0u)
-    ragged_body<WG, true>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, overflow, gtab, gops, zinv, final_xor, out,
-                          sbase);
+    ragged_body<WG, true>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, overflow, gtab, gops, zinv,
+                          final_xor, out, tilecrc, sbase);
   else
-    ragged_body<WG, false>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, overflow, gtab, gops, zinv, final_xor, out,
-                           sbase);
+    ragged_body<WG, false>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, overflow, gtab, gops,
+                           zinv, final_xor, out, tilecrc, sbase);
 }
 
 template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
                                                   const TileDesc*, const u32*, const u32*, const u32*, const u32*,
-                                                  u32, u32*);
+                                                  u32, u32*, u32*);
 
-// hipcub scan wrapper (exclusive prefix sum of per-message tile counts).
+// Per message with tiles: out[m] = XOR of its tiles' values = px[last] ^ px[first - 1],
+// px = inclusive XOR-scan of tilecrc. Skipped when the batch overflowed the workspace
+// (those results were produced with atomics).
+__global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, u64 count, const u32* __restrict__ px,
+                                          const u32* __restrict__ overflow, u32* __restrict__ out) {
+  const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= count || *overflow) return;
+  const u64 t0 = tile_base[m], t1 = tile_base[m + 1];
+  if (t1 == t0) return;  // empty message: written by the count kernel
+  out[m] = px[t1 - 1] ^ (t0 ? px[t0 - 1] : 0u);
+}
+
+// hipcub scan wrappers: exclusive prefix sum of per-message tile counts; inclusive XOR
+// scan of per-tile values.
 hipError_t ragged_scan(void* temp, size_t& temp_bytes, const u64* in, u64* out, u64 n, hipStream_t stream) {
   return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, stream);
+}
+
+struct XorOp {
+  __host__ __device__ u32 operator()(u32 a, u32 b) const { return a ^ b; }
+};
+
+hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u32* out, u64 n, hipStream_t stream) {
+  return hipcub::DeviceScan::InclusiveScan(temp, temp_bytes, in, out, XorOp(), (int)n, stream);
 }
 
 }  // namespace subspace_amd

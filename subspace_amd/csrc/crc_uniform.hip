@@ -18,7 +18,7 @@
 
 namespace subspace_amd {
 
-template <int WG>
+template <int WG, int DEPTH>
 __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __restrict__ base, u64 stride, u64 count,
                                                              const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                              u32 init, u32 final_xor, u32* __restrict__ out,
@@ -35,13 +35,22 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   const u32 xb = sbase + kLdsXpose + (u32)wid * kLdsXposePerWave;
   const int l = lane & 31, h = lane >> 5;
   const u64 ntiles = (count + 1) >> 1;
-  // Tile order. order 0 ("sweep"): tau = k*nw + w, all waves advance one compact front.
-  // order 1 ("region"): workgroup b owns the contiguous tiles [b*per, (b+1)*per), its waves
+  // Tile order. Sweep (orders 0 and 2): tau = k*nw + w, all waves advance one compact
+  // front. The front position w of a wave: order 0 gives consecutive 16 KiB pairs of tiles
+  // to consecutive workgroups, w = (b + G*(wid/2))*2 + wid%2 -- so every XCD (block b runs
+  // on XCD b%8) streams from everywhere in the front (tools/ubench/streamread.hip:
+  // lines_remap sub2, 6.6 vs 6.0 TB/s for one 256 MiB launch); order 2 gives a workgroup
+  // its wpb consecutive tiles, w = b*wpb + wid.
+  // Order 1 ("region"): workgroup b owns the contiguous tiles [b*per, (b+1)*per), its waves
   // interleave inside it: tau = b*per + k*wpb + wid.
   constexpr u64 wpb = WG / 64;
   const u64 nw = (u64)gridDim.x * wpb;
   u64 t0, tstep, tend;
   if (order == 0) {
+    t0 = front_slot(blockIdx.x, gridDim.x, (u32)wid);
+    tstep = nw;
+    tend = ntiles;
+  } else if (order == 2) {
     t0 = (u64)blockIdx.x * wpb + (u64)wid;
     tstep = nw;
     tend = ntiles;
@@ -53,36 +62,50 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     tend = b0 + per < ntiles ? b0 + per : ntiles;
   }
   // waves beyond the work still help fill LDS, then leave (no later block barrier)
-  const u64 nk = t0 < tend ? (tend - t0 + tstep - 1) / tstep : 0;  // this wave's tiles: tau = t0 + k*tstep
+  // this wave's tiles: tau = t0 + k*tstep, k < nk. 32-bit tile counters keep the loop
+  // control scalar (a 64-bit compare needs VALU temporaries, which hipcc may place in a
+  // buffer register still being loaded, forcing a vmcnt drain at the loop head).
+  const u32 nk = t0 < tend ? (u32)((tend - t0 + tstep - 1) / tstep) : 0u;
   const u32 s_init = (l == 0) ? init : 0u;
 
-  // Lane's line of tile k. The missing odd message of the last tile (odd count) re-reads
-  // the even message instead, so every lane loads unconditionally (no divergent branch
-  // around the loads, which would force vmcnt(0) waits); its CRC is never stored.
-  auto line_ptr = [&](u64 k) {
-    u64 msg = 2 * (t0 + k * tstep) + (u64)h;
-    msg = msg < count ? msg : msg - 1;
-    return reinterpret_cast<const u32x4*>(base + msg * stride + (u64)l * 128);
+  // Tile k's lines are read with buffer loads: a scalar resource (base = the tile's first
+  // message, range = the bytes the tile may touch) and one per-lane offset that never
+  // changes (h*stride + l*128). All address arithmetic is scalar, so no VALU temporary can
+  // land in a buffer register with a load in flight (which costs a vmcnt drain), and every
+  // lane issues every load (no divergent branch around loads either). Reads outside the
+  // range return zeros without touching memory: the missing odd message of a batch's last
+  // tile, and prefetches past a wave's last tile (range 0).
+  const u32 voff = (u32)h * (u32)stride + (u32)l * 128u;  // host guarantees stride < 2^31
+  auto tile_rsrc = [&](u32 k) {
+    const u64 m0 = 2 * (t0 + (u64)k * tstep);
+    const bool live = k < nk;
+    const u32 nrec = !live ? 0u : (m0 + 1 != count ? (u32)stride + 4096u : 4096u);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(live ? base + m0 * stride : base), (short)0,
+                                             (int)nrec, kBufferRsrcFlags);
+  };
+  auto load_tile = [&](u32x4 (&d)[8], u32 k) {
+    const auto r = tile_rsrc(k);
+#pragma unroll
+    for (int i = 0; i < 8; i++) d[i] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 16 * i, 0);
+    // keep the loads at this point, in order (hipcc otherwise sinks them into the compute)
+    __builtin_amdgcn_sched_barrier(0);
   };
 
   // Table loads first, then tile 0's loads, then the LDS stores: tile 0's latency hides
   // behind the fill and the barrier.
   LdsFill<WG, kOpZ128 + 5> fill;  // step tables + Z_128 .. Z_2048
   fill.load(gtab, gops);
-  u32x4 v[8];
-  {
-    // waves without work (nk == 0) load tile "0" of wave 0 -- harmless, keeps the load unconditional
-    const u32x4* q = nk > 0 ? line_ptr(0) : reinterpret_cast<const u32x4*>(base + (u64)l * 128 * (h == 0));
+  // DEPTH + 1 line buffers: tile k is processed while tiles k+1 .. k+DEPTH are in flight
+  u32x4 buf[DEPTH + 1][8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = q[i];
-  }
+  for (int d = 0; d < DEPTH; d++) load_tile(buf[d], (u32)d);  // (range 0 for waves without work)
   fill.store(sbase);
   __syncthreads();
   if (nk == 0) return;
   u32 part0 = 0, part1 = 0, part2 = 0, part3 = 0;
 
   // Line CRC of one tile, then (every 4th tile, or the wave's last) the combine tree.
-  auto process = [&](const u32x4 (&d)[8], u64 k) {
+  auto process = [&](const u32x4 (&d)[8], u32 k) {
     u32 crc = s_init;
 #pragma unroll
     for (int i = 0; i < 8; i++)
@@ -116,33 +139,38 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
       wave_lds_sync();
     }
   };
-  // Unconditional prefetch (past the wave's last tile it re-reads that tile): a load inside
-  // a branch makes hipcc drain it with vmcnt(0) in the middle of the compute.
-  auto prefetch = [&](u32x4 (&d)[8], u64 k) {
-    const u32x4* q = line_ptr(k < nk ? k : nk - 1);
-#pragma unroll
-    for (int i = 0; i < 8; i++) d[i] = q[i];
-    // keep the loads at this point (hipcc otherwise sinks them into the compute)
-    __builtin_amdgcn_sched_barrier(0);
-  };
 
-  // Ping-pong buffers, loop unrolled by two: no register copies between iterations, and
-  // the next tile's loads are always issued before this tile's data is waited for.
-  u32x4 (&A)[8] = v;
-  u32x4 B[8];
-  for (u64 k = 0; k < nk; k += 2) {
-    prefetch(B, k + 1);
-    process(A, k);
-    if (k + 1 >= nk) break;
-    prefetch(A, k + 2);
-    process(B, k + 1);
+  // Rotating buffers, loop unrolled DEPTH + 1 times: no register copies between
+  // iterations, and tile k+DEPTH's loads are issued before tile k's data is waited for
+  // (vmcnt(8*DEPTH)): with DEPTH 2 a wave keeps a tile in flight even while it computes.
+  // The body has no early exit: a break between phases would give the loop head a
+  // predecessor with fewer loads in flight, and hipcc's waitcnt merge would then drain
+  // more than tile k at the head. The last 0..DEPTH tiles (already loaded) follow it.
+  u32 k = 0;
+  for (; k + DEPTH < nk; k += DEPTH + 1) {
+#pragma unroll
+    for (int s = 0; s <= DEPTH; s++) {
+      load_tile(buf[(s + DEPTH) % (DEPTH + 1)], k + s + DEPTH);
+      process(buf[s], k + s);
+    }
   }
+#pragma unroll
+  for (int s = 0; s < DEPTH; s++)
+    if (k + s < nk) process(buf[s], k + s);
 }
 
-template __global__ void crc32_uniform4k_kernel<768>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
-template __global__ void crc32_uniform4k_kernel<512>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
-template __global__ void crc32_uniform4k_kernel<640>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
-template __global__ void crc32_uniform4k_kernel<256>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
-template __global__ void crc32_uniform4k_kernel<1024>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
+
+#define SUBSPACE_UNIFORM_INST(WG, D)                                                                         \
+  template __global__ void crc32_uniform4k_kernel<WG, D>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, \
+                                                         u32*, int);
+SUBSPACE_UNIFORM_INST(256, 1)
+SUBSPACE_UNIFORM_INST(256, 2)
+SUBSPACE_UNIFORM_INST(512, 1)
+SUBSPACE_UNIFORM_INST(512, 2)
+SUBSPACE_UNIFORM_INST(768, 1)
+SUBSPACE_UNIFORM_INST(768, 2)
+SUBSPACE_UNIFORM_INST(1024, 1)
+SUBSPACE_UNIFORM_INST(1024, 2)
+#undef SUBSPACE_UNIFORM_INST
 
 }  // namespace subspace_amd

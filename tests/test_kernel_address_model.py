@@ -107,3 +107,29 @@ def test_uniform_kernel_lines_stay_in_messages(count, stride):
                 assert 0 <= msg < count
         if nk == 0:
             continue  # idle waves read lines of message 0 (base + l*128 for h == 0, else base)
+
+
+def front_slot(b, G, wid):
+    """crc_device.h front_slot: consecutive pairs of sweep-front slots go to consecutive
+    workgroups (round-robin over XCDs)."""
+    return (b + G * (wid >> 1)) * 2 + (wid & 1)
+
+
+@pytest.mark.parametrize("wg", [256, 512, 640, 768, 1024])
+@pytest.mark.parametrize("grid", [1, 2, 3, 255, 256])
+def test_front_slot_is_a_bijection(wg, grid):
+    wpb = wg // 64
+    slots = [front_slot(b, grid, wid) for b in range(grid) for wid in range(wpb)]
+    assert sorted(slots) == list(range(grid * wpb))
+
+
+def test_front_slot_tiles_covered_exactly_once():
+    grid, wpb, total = 256, 8, 70001
+    nw = grid * wpb
+    seen = []
+    for b in range(grid):
+        for wid in range(wpb):
+            w = front_slot(b, grid, wid)
+            nk = (total - w + nw - 1) // nw if w < total else 0
+            seen += [k * nw + w for k in range(nk)]
+    assert sorted(seen) == list(range(total))
