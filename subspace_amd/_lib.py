@@ -13,6 +13,8 @@ from pathlib import Path
 
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = _HERE / "libsubspace_crc.so"
+if os.environ.get("SUBSPACE_CRC_PROBE_LIB"):  # investigation builds (tools/ubench/build_probes.sh)
+    LIB_PATH = Path(os.environ["SUBSPACE_CRC_PROBE_LIB"])
 
 # Every symbol include/subspace_crc.h declares (tests check they are all exported).
 EXPORTED_SYMBOLS = (
@@ -71,7 +73,7 @@ def load() -> ctypes.CDLL:
     lib.subspace_crc_testutil_fill_ragged.restype = i32
     lib.subspace_crc_testutil_fill_ragged.argtypes = [vp, vp, vp, u64, u64, u64, u64, vp]
     lib.subspace_crc_testutil_tune.restype = i32
-    lib.subspace_crc_testutil_tune.argtypes = [vp, i32, i32, i32, i32]
+    lib.subspace_crc_testutil_tune.argtypes = [vp, i32, i32, i32]
     _lib = lib
     return lib
 

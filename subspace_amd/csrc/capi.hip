@@ -16,8 +16,8 @@
 
 namespace subspace_amd {
 
-template <int WG, int DEPTH>
-__global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
+template <int WG>
+__global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, u32*, int);
 
 struct TileDesc;
 __global__ void crc32_ragged_count_kernel(const u64*, u32, u64, u32, u32, u64*, u32*);
@@ -89,7 +89,7 @@ struct subspace_crc_ctx {
   int uniform_wg = 512;    // workgroup size of the uniform kernel (256/512/640/768/1024)
   int uniform_blocks = 0;  // 0 = one workgroup per CU
   int uniform_order = 0;   // tile order: 0 XCD-spread sweep, 1 per-workgroup region, 2 plain sweep
-  int uniform_depth = 2;   // tiles in flight per wave while one is processed (1 or 2)
+  u32* d_sink = nullptr;   // scratch words for result stores without a result
   u64* d_uoff = nullptr;  // offsets/lengths materialised for non-4K uniform batches
   u64* d_ulen = nullptr;
   u64 u_capacity = 0;
@@ -262,6 +262,7 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
   std::vector<u32> tab(1024), ops((size_t)kNumOps * 128, 0u), pow2(64 * 128, 0u);
   for (int k = 0; k < 4; k++)
     for (int b = 0; b < 256; b++) tab[k * 256 + b] = c->host_tab.t[k][b];
+  nibble_tables(z_bytes(c->host_tab, 64), &ops[(size_t)kOpZ64 * 128]);
   for (int k = 0; k < 6; k++) nibble_tables(z_bytes(c->host_tab, 128ull << k), &ops[(size_t)(kOpZ128 + k) * 128]);
   for (int k = 0; k < kNumTileOps; k++)
     nibble_tables(z_bytes(c->host_tab, 8192ull << k), &ops[(size_t)(kOpZTile + k) * 128]);
@@ -274,15 +275,15 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
   hipError_t e = hipMalloc(&c->d_tab, tab.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_ops, ops.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_pow2, pow2.size() * 4);
+  if (e == hipSuccess) e = hipMalloc(&c->d_sink, 64 * sizeof(u32));
   if (e == hipSuccess) e = hipMemcpy(c->d_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_ops, ops.data(), ops.size() * 4, hipMemcpyHostToDevice);
-#define SET_LDS(WGV, D)                                                                                      \
+#define SET_LDS(WGV)                                                                                         \
   if (e == hipSuccess)                                                                                       \
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV, D>,                                      \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(WGV / 64));
-  SET_LDS(256, 1) SET_LDS(256, 2) SET_LDS(512, 1) SET_LDS(512, 2)
-  SET_LDS(768, 1) SET_LDS(768, 2) SET_LDS(1024, 1) SET_LDS(1024, 2)
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                            (int)lds_bytes(WGV / 64));
+  SET_LDS(256) SET_LDS(512) SET_LDS(768) SET_LDS(1024)
 #undef SET_LDS
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_ragged_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -300,6 +301,7 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_tab);
   (void)hipFree(c->d_ops);
   (void)hipFree(c->d_pow2);
+  (void)hipFree(c->d_sink);
   (void)hipFree(c->d_crc0);
   (void)hipFree(c->d_soff);
   for (auto& kv : c->zinv) (void)hipFree(kv.second);
@@ -366,15 +368,14 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     if (c->uniform_blocks > 0 && (u64)c->uniform_blocks < (u64)blocks) blocks = c->uniform_blocks;
     const auto* b = static_cast<const uint8_t*>(dev_base);
     const int ord = c->uniform_order;
-#define LAUNCH(WGV, D)                                                                                 \
-  crc32_uniform4k_kernel<WGV, D><<<blocks, WGV, lds_bytes(WGV / 64), st>>>(b, stride, count, c->d_tab, c->d_ops, \
-                                                                           init, final_xor, dev_out, ord)
-    const bool d2 = c->uniform_depth == 2;
+#define LAUNCH(WGV)                                                                                    \
+  crc32_uniform4k_kernel<WGV><<<blocks, WGV, lds_bytes(WGV / 64), st>>>(b, stride, count, c->d_tab, c->d_ops, init, \
+                                                                        final_xor, dev_out, c->d_sink, ord)
     switch (wg) {
-      case 256: if (d2) LAUNCH(256, 2); else LAUNCH(256, 1); break;
-      case 768: if (d2) LAUNCH(768, 2); else LAUNCH(768, 1); break;
-      case 1024: if (d2) LAUNCH(1024, 2); else LAUNCH(1024, 1); break;
-      default: if (d2) LAUNCH(512, 2); else LAUNCH(512, 1); break;
+      case 256: LAUNCH(256); break;
+      case 768: LAUNCH(768); break;
+      case 1024: LAUNCH(1024); break;
+      default: LAUNCH(512); break;
     }
 #undef LAUNCH
     HIP_TRY(hipGetLastError());
@@ -467,15 +468,13 @@ int subspace_crc32_slots_strided(subspace_crc_ctx* c, void* dev_buffer, uint64_t
 
 // Tuning hook for experiments (not part of the public header): uniform-kernel workgroup
 // size (512/768/1024) and an optional cap on the number of workgroups.
-int subspace_crc_testutil_tune(subspace_crc_ctx* c, int uniform_wg, int uniform_blocks, int uniform_order,
-                               int uniform_depth) {
+int subspace_crc_testutil_tune(subspace_crc_ctx* c, int uniform_wg, int uniform_blocks, int uniform_order) {
   if (!c) return SUBSPACE_CRC_EINVAL;
   if (uniform_wg != 256 && uniform_wg != 512 && uniform_wg != 768 && uniform_wg != 1024) return SUBSPACE_CRC_EINVAL;
-  if (uniform_order < 0 || uniform_order > 2 || uniform_depth < 1 || uniform_depth > 2) return SUBSPACE_CRC_EINVAL;
+  if (uniform_order < 0 || uniform_order > 2) return SUBSPACE_CRC_EINVAL;
   c->uniform_wg = uniform_wg;
   c->uniform_blocks = uniform_blocks;
   c->uniform_order = uniform_order;
-  c->uniform_depth = uniform_depth;
   return SUBSPACE_CRC_OK;
 }
 

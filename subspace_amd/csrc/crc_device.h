@@ -30,8 +30,9 @@ constexpr u32 kLdsXposePerWave = 1024u;
 constexpr size_t lds_bytes(int waves) { return kLdsXpose + (size_t)waves * kLdsXposePerWave; }
 
 // operator slots
-constexpr int kOpZ128 = 0;    // slots 0..5: Z_{128 * 2^k}, k = 0..5 (128 B .. 4 KiB)
-constexpr int kOpZTile = 6;   // slots 6..26: Z_{8192 * 2^k}, k = 0..20 (8 KiB .. 8 GiB)
+constexpr int kOpZ64 = 0;     // slot 0: Z_64 (joins the two 64-B halves of a line)
+constexpr int kOpZ128 = 1;    // slots 1..6: Z_{128 * 2^k}, k = 0..5 (128 B .. 4 KiB)
+constexpr int kOpZTile = 7;   // slots 7..27: Z_{8192 * 2^k}, k = 0..20 (8 KiB .. 8 GiB)
 constexpr int kNumTileOps = 21;
 
 typedef __attribute__((address_space(3))) u32 lds_u32_t;

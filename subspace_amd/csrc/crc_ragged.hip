@@ -186,26 +186,31 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
     t.pad = 0;
     return t;
   };
-  // Issue the loads of this lane's line for tile descriptor d. Positions are signed: a
-  // message's first tile can start before the arena start. Every lane issues all 9 loads
-  // unconditionally (a load in a divergent branch would make hipcc drain with vmcnt(0));
-  // blocks holding no byte of the message are redirected to the block of the message's
-  // first byte and zeroed at use.
-  auto load_line = [&](const TileDesc& d, LineState& L) {
-    const i64 line_start = (i64)d.tile_end - 8192 + (i64)lane * 128;
-    const i64 a0 = line_start & ~(i64)15;
-    const i64 s = (i64)d.msg_start;
-    const i64 safe = s & ~(i64)15;
-    const bool mis = (d.tile_end & 15) != 0;
+  // Issue the loads of this lane's line for tile descriptor d, as buffer loads against a
+  // scalar resource spanning exactly the tile's blocks that hold message bytes:
+  //   [max(aligned tile start, aligned message start), tile end rounded up to 16).
+  // Blocks outside it (before the message, or an aligned line's 9th block) read as zeros
+  // without touching memory, so every lane issues all 9 loads (no divergent branch around
+  // loads) and nothing outside the message's own blocks is ever read. A per-lane offset
+  // below the range start wraps to a huge value: out of range as well. `live` false (a
+  // prefetch past the wave's last tile) gives an empty range.
+  auto load_line = [&](const TileDesc& d, LineState& L, bool live) {
+    const i64 t0a = ((i64)d.tile_end - 8192) & ~(i64)15;
+    const i64 sa = (i64)d.msg_start & ~(i64)15;
+    const i64 rb = t0a > sa ? t0a : sa;
+    const i64 rend = ((i64)d.tile_end + 15) & ~(i64)15;
+    const u32 nrec = live ? (u32)(rend - rb) : 0u;
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + rb), (short)0, (int)nrec,
+                                                     kBufferRsrcFlags);
+    const u32 vo = (u32)lane * 128u - (u32)(rb - t0a);
 #pragma unroll
-    for (int b = 0; b < 9; b++) {
-      const i64 blk = a0 + 16 * b;
-      // block 8 exists only for misaligned lines (an aligned line's 9th block lies past it,
-      // past the message end for the message's last line)
-      const bool need = (b < 8 || mis) && blk + 16 > s;
-      const i64 src = need ? blk : safe;
-      L.d[b] = *reinterpret_cast<const u32x4*>(base + src);
-    }
+    for (int b = 0; b < 8; b++) L.d[b] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16u * b, 0, 0);
+    // The 9th block of an aligned tile's last line starts exactly at the range end; its
+    // offset goes in the VGPR (not folded into the instruction offset), so the range check
+    // sees it whichever offsets the hardware includes.
+    u32 vo8;
+    asm volatile("v_add_u32 %0, 0x80, %1" : "=v"(vo8) : "v"(vo));
+    L.d[8] = __builtin_amdgcn_raw_buffer_load_b128(r, vo8, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -308,24 +313,28 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
   fetch_desc(1, dB);
   TileDesc dcur = unpack(dA);
   LineState A, B;
-  load_line(dcur, A);
+  load_line(dcur, A, nk != 0);
   fill.store(sbase);
   __syncthreads();
   if (nk == 0) return;
 
-  // Ping-pong line buffers, loop unrolled by two; descriptors two tiles ahead.
-  for (u64 k = 0; k < nk; k += 2) {
-    const TileDesc d1 = unpack(dB);   // tile k+1 (clamped)
-    fetch_desc(k + 2, dA);            // tile k+2
-    load_line(d1, B);
+  // Ping-pong line buffers, loop unrolled by two, descriptors two tiles ahead. The body
+  // has no early exit (a break between the halves would give the loop head a predecessor
+  // with fewer loads in flight, and hipcc's waitcnt merge would drain the prefetch there);
+  // an odd last tile, already loaded, follows the loop.
+  u64 k = 0;
+  for (; k + 1 < nk; k += 2) {
+    const TileDesc d1 = unpack(dB);   // tile k+1
+    fetch_desc(k + 2, dA);            // tile k+2 (clamped)
+    load_line(d1, B, true);
     process(A, dcur, k);
-    if (k + 1 >= nk) break;
-    const TileDesc d2 = unpack(dA);   // tile k+2
-    fetch_desc(k + 3, dB);            // tile k+3
-    load_line(d2, A);
+    const TileDesc d2 = unpack(dA);   // tile k+2 (clamped)
+    fetch_desc(k + 3, dB);            // tile k+3 (clamped)
+    load_line(d2, A, k + 2 < nk);
     process(B, d1, k + 1);
     dcur = d2;
   }
+  if (k < nk) process(A, dcur, k);
 }
 
 

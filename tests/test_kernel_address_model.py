@@ -1,52 +1,60 @@
-"""CPU model of the ragged kernel's load addresses (subspace_amd/csrc/crc_ragged.hip,
-make_desc + load_line): every 16-B block any lane loads must overlap its own message,
-so no load can leave the caller's buffer. Runs without a GPU."""
+"""CPU models of the kernels' load addresses and tile indexing (subspace_amd/csrc/
+crc_ragged.hip make_desc + load_line, crc_uniform.hip tile_rsrc / load_tile, and the sweep
+front mapping): every byte any load can read lies inside the caller's messages, every
+message byte is read, every tile is visited exactly once. Runs without a GPU."""
 import numpy as np
 import pytest
+
+M32 = 1 << 32
 
 
 def tiles_for_length(n):
     return (n + 8191) >> 13
 
 
-def loaded_blocks(s, e):
-    """(lane, block, src) for every load the kernel issues for message [s, e)."""
+def ragged_loads(s, e):
+    """For message [s, e): (tile j, lane, block, address or None) for every load of
+    load_line -- buffer loads against the range [rb, rend), offsets are 32-bit (wrapping);
+    an offset >= the range size reads zeros without a memory access (None)."""
     n = e - s
     nt = tiles_for_length(n)
     for j in range(nt):
         tile_end = e - ((nt - 1 - j) << 13)
-        mis = (tile_end & 15) != 0
-        safe = s & ~15
+        t0a = (tile_end - 8192) & ~15
+        sa = s & ~15
+        rb = max(t0a, sa)
+        rend = (tile_end + 15) & ~15
+        nrec = rend - rb
         for lane in range(64):
-            line_start = tile_end - 8192 + lane * 128
-            a0 = line_start & ~15
+            vo = (lane * 128 - (rb - t0a)) % M32
             for b in range(9):
-                blk = a0 + 16 * b
-                need = (b < 8 or mis) and blk + 16 > s
-                yield lane, b, (blk if need else safe), need
+                off = (vo + 16 * b) % M32
+                yield j, lane, b, (rb + off if off < nrec else None)
 
 
 @pytest.mark.parametrize("seed", range(6))
-def test_every_load_overlaps_its_message(seed):
+def test_every_ragged_load_stays_in_its_message_blocks(seed):
     rng = np.random.default_rng(seed)
-    for _ in range(300):
+    for _ in range(200):
         s = int(rng.integers(0, 5000))
-        n = int(rng.choice([rng.integers(1, 300), rng.integers(1, 40000), 8192 * int(rng.integers(1, 4)) + int(rng.integers(-20, 20))]))
+        n = int(rng.choice([rng.integers(1, 300), rng.integers(1, 40000),
+                            8192 * int(rng.integers(1, 4)) + int(rng.integers(-20, 20))]))
         n = max(n, 1)
         e = s + n
-        for lane, b, src, need in loaded_blocks(s, e):
-            assert src + 16 > s and src < e, (s, e, lane, b, src)
-            assert src >= 0
+        for j, lane, b, addr in ragged_loads(s, e):
+            if addr is None:
+                continue
+            # a 16-B block that holds at least one message byte
+            assert addr + 16 > s and addr < e, (s, e, j, lane, b, addr)
 
 
-def test_needed_blocks_cover_message():
-    # the blocks marked `need` cover every message byte exactly once per line window
-    for s, n in [(0, 1), (3, 100), (17, 8192), (5, 8193), (0, 4096), (1, 65536 + 7)]:
+def test_ragged_loads_cover_every_message_byte():
+    for s, n in [(0, 1), (3, 100), (17, 8192), (5, 8193), (0, 4096), (1, 65536 + 7), (15, 24577)]:
         e = s + n
         covered = set()
-        for lane, b, src, need in loaded_blocks(s, e):
-            if need:
-                covered.update(range(max(src, s), min(src + 16, e)))
+        for j, lane, b, addr in ragged_loads(s, e):
+            if addr is not None:
+                covered.update(range(max(addr, s), min(addr + 16, e)))
         assert covered == set(range(s, e))
 
 
@@ -86,27 +94,36 @@ def test_tiles_are_covered_exactly_once():
     assert sorted(seen) == list(range(total))
 
 
-@pytest.mark.parametrize("count,stride", [(1, 4096), (2, 4096), (3, 4160), (1000, 4096), (4097, 8192), (65537, 4096)])
-def test_uniform_kernel_lines_stay_in_messages(count, stride):
-    """Replays crc32_uniform4k_kernel's line_ptr / prefetch clamping (order 0, 256 x 8 waves)."""
+@pytest.mark.parametrize("count,stride", [(1, 4096), (2, 4096), (3, 4160), (1000, 4096), (4097, 8192),
+                                          (20001, 4096)])
+@pytest.mark.parametrize("depth", [1, 2])
+def test_uniform_kernel_loads_stay_in_messages(count, stride, depth):
+    """Replays crc32_uniform4k_kernel's load_tile ranges (order 0, 256 x 8 waves): every
+    in-range load lies inside message 2*tau + h, and every message of every tile is read."""
     ntiles = (count + 1) // 2
     nblocks, wpb = 256, 8
     nw = nblocks * wpb
-    for w in range(nw):
-        t0, tstep = w, nw
-        nk = (ntiles - t0 + tstep - 1) // tstep if t0 < ntiles else 0
-        ks = [0] if nk else []
-        k = 0
-        while k < nk:  # prefetch(B, k+1); process(A, k); prefetch(A, k+2); process(B, k+1)
-            ks += [min(k + 1, nk - 1), min(k + 2, nk - 1)]
-            k += 2
-        for kk in ks:
-            for h in (0, 1):
-                msg = 2 * (t0 + kk * tstep) + h
-                msg = msg if msg < count else msg - 1
-                assert 0 <= msg < count
-        if nk == 0:
-            continue  # idle waves read lines of message 0 (base + l*128 for h == 0, else base)
+    read = set()
+    for b in range(nblocks):
+        for wid in range(wpb):
+            t0 = front_slot(b, nblocks, wid)
+            nk = (ntiles - t0 + nw - 1) // nw if t0 < ntiles else 0
+            # loads issued: prologue tiles 0..depth-1, then k+depth for every processed tile k
+            ks = list(range(depth)) + [k + depth for k in range(nk)]
+            for k in ks:
+                live = k < nk
+                m0 = 2 * (t0 + k * nw)
+                nrec = 0 if not live else (stride + 4096 if m0 + 1 != count else 4096)
+                for h in (0, 1):
+                    for l in range(32):
+                        for i in range(8):
+                            off = h * stride + l * 128 + 16 * i
+                            if off >= nrec:
+                                continue
+                            msg = m0 + h
+                            assert msg < count and off - h * stride + 16 <= 4096
+                            read.add(msg)
+    assert read == set(range(count))
 
 
 def front_slot(b, G, wid):
@@ -115,7 +132,7 @@ def front_slot(b, G, wid):
     return (b + G * (wid >> 1)) * 2 + (wid & 1)
 
 
-@pytest.mark.parametrize("wg", [256, 512, 640, 768, 1024])
+@pytest.mark.parametrize("wg", [256, 512, 768, 1024])
 @pytest.mark.parametrize("grid", [1, 2, 3, 255, 256])
 def test_front_slot_is_a_bijection(wg, grid):
     wpb = wg // 64

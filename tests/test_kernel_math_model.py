@@ -148,3 +148,13 @@ def test_ragged_decomposition(s, L):
     buf = rng.integers(0, 256, s + L + 64, dtype=np.uint8).tobytes()
     for init in (M32, 0xA5A5A5A5):
         assert ragged_model(buf, s, L, init) == ref(init, buf[s:s + L]), (s, L, hex(init))
+
+
+def test_uniform_line_as_two_64b_chains():
+    """ILP = 2 in crc32_uniform4k_kernel: a line's CRC from two independent 64-B chains,
+    Z_64(crc(s, first half)) ^ crc(0, second half) == crc(s, line)."""
+    z64 = zbytes(64)
+    rng = np.random.default_rng(64)
+    for init in (M32, 0, 0x0BADCAFE):
+        line = rng.integers(0, 256, 128, dtype=np.uint8).tobytes()
+        assert apply(z64, crc_raw(init, line[:64])) ^ crc_raw(0, line[64:]) == crc_raw(init, line)

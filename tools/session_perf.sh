@@ -15,7 +15,7 @@ run() {  # name, timeout, command...
 }
 run pytest 900 python -m pytest tests/ -x -q -m gpu -p no:cacheprovider --timeout 600 -rf
 run configs 600 python tools/bench_configs.py --configs C,Cu,D,E
-run sweep 400 python tools/sweep_uniform.py 65536,1048576 512,768,1024 5 0,2 1,2
+run sweep 500 python tools/sweep_uniform.py 65536,1048576 256,512,768,1024 5 0,2
 run modes 300 python tools/launch_modes.py
 run bench 300 python bench.py --no-cpu-baseline --no-e2e
 echo done >> $OUT/status.txt

@@ -18,7 +18,6 @@ def main():
     wgs = [int(x) for x in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["512", "768", "1024"])]
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
     orders = [int(x) for x in (sys.argv[4].split(",") if len(sys.argv) > 4 else ["0"])]
-    depths = [int(x) for x in (sys.argv[5].split(",") if len(sys.argv) > 5 else ["2"])]
     ctx = gpu.CrcContext(0)
     lib = _lib.load()
     dev = torch.device("cuda", 0)
@@ -33,16 +32,16 @@ def main():
         iters = max(8, int(2e9 // (count * 4096)))
         ref = None
         for r in range(rounds):
-            for wg, order, depth in [(a, b, c) for a in wgs for b in orders for c in depths]:
-                if lib.subspace_crc_testutil_tune(ctx._h, wg, 0, order, depth) != 0:
-                    raise SystemExit(f"bad variant wg={wg} order={order} depth={depth}")
+            for wg, order in [(a, b) for a in wgs for b in orders]:
+                if lib.subspace_crc_testutil_tune(ctx._h, wg, 0, order) != 0:
+                    raise SystemExit(f"bad variant wg={wg} order={order}")
                 if r == 0:  # every variant must produce the same CRCs
                     ctx.crc32_uniform(bufs[0], 4096, 4096, count, out)
                     got = out.clone()
                     if ref is None:
                         ref = got
                     elif not torch.equal(ref, got):
-                        raise SystemExit(f"variant wg={wg} order={order} depth={depth} differs")
+                        raise SystemExit(f"variant wg={wg} order={order} differs")
                 for i in range(3):
                     ctx.crc32_uniform(bufs[i % nb], 4096, 4096, count, out)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -52,12 +51,12 @@ def main():
                 b.record()
                 torch.cuda.synchronize()
                 ms = a.elapsed_time(b) / iters
-                res.setdefault((count, wg, order, depth), []).append(ms)
+                res.setdefault((count, wg, order), []).append(ms)
         del bufs
         torch.cuda.empty_cache()
-    for (count, wg, order, depth), v in sorted(res.items()):
+    for (count, wg, order), v in sorted(res.items()):
         med, best = float(np.median(v)), float(np.min(v))
-        print(json.dumps({"count": count, "wg": wg, "order": order, "depth": depth, "median_ms": round(med, 4), "best_ms": round(best, 4),
+        print(json.dumps({"count": count, "wg": wg, "order": order, "median_ms": round(med, 4), "best_ms": round(best, 4),
                           "TBps_median": round(count * 4096 / med / 1e9, 3),
                           "TBps_best": round(count * 4096 / best / 1e9, 3)}), flush=True)
 

@@ -71,6 +71,37 @@ __global__ __launch_bounds__(WG) void lines_remap(const u32x4* __restrict__ p, u
   out[blockIdx.x * WG + threadIdx.x] = acc;
 }
 
+// lines_remap sub2 + the CRC kernels' result stores: every 4 tiles a wave stores the 8
+// results of its last 4 tiles (2 adjacent words per tile) from 8 lanes (ST=1), as 4 u64
+// pairs (ST=2), or not at all (ST=0: one store per wave at the end).
+template <int WG, int ST>
+__global__ __launch_bounds__(WG) void lines_store(const u32x4* __restrict__ p, u64 nchunks, u32* out, u32* res) {
+  const int lane = threadIdx.x & 63;
+  const u64 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u64 w = ((u64)blockIdx.x + (u64)gridDim.x * (wid / 2)) * 2 + wid % 2;
+  const u64 nw = (u64)gridDim.x * (WG / 64);
+  u32 acc = 0;
+  u64 k = 0;
+  for (u64 c = w; c < nchunks; c += nw, k++) {
+    const u32x4* q = p + c * 512 + lane * 8;
+    u32x4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = q[i];
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+    if (ST && (k & 3) == 3) {
+      const int M = lane >> 3;
+      const u64 tile = c - (3 - (u64)(M >> 1)) * nw;  // tile of result slot M
+      if (ST == 1) {
+        if ((lane & 7) == 0) res[2 * tile + (M & 1)] = acc;
+      } else {
+        if ((lane & 15) == 0) *reinterpret_cast<unsigned long long*>(res + 2 * tile) = acc * 3ull;
+      }
+    }
+  }
+  out[blockIdx.x * WG + threadIdx.x] = acc;
+}
+
 // Lines, but the 8 loads of a lane go out as 16-B pieces interleaved across lanes within
 // 2 KiB: instruction i reads piece (i) of lines lane/... -- kept simple: lane reads its line
 // as 2 x 64 B halves placed 4 KiB apart (two half-tiles), i.e. 32-B granularity per lane.
@@ -116,6 +147,7 @@ int main() {
   const u64 bytes = 4ull << 30, n16 = bytes / 16;
   u32x4* buf; CK(hipMalloc(&buf, bytes));
   u32* out; CK(hipMalloc(&out, 64ull << 20));
+  u32* res; CK(hipMalloc(&res, (bytes / 4096) * 4 + 64));
   gen<<<4096, 256>>>(buf, n16);
   CK(hipDeviceSynchronize());
   for (u64 win : {256ull << 20, 1ull << 30, 4ull << 30}) {
@@ -128,6 +160,10 @@ int main() {
     };
 #define RUN(K, WG, G) rep(#K " wg" #WG " grid" #G, time_it([&] { K<WG><<<G, WG>>>(W(), chunks, out); }, 32))
 #define RUN2(WG, SUB, G) rep("lines_remap wg" #WG " sub" #SUB, time_it([&] { lines_remap<WG, SUB><<<G, WG>>>(W(), chunks, out); }, 32))
+#define RUN3(ST) rep("lines_store st" #ST, time_it([&] { lines_store<512, ST><<<256, 512>>>(W(), chunks, out, res); }, 32))
+    RUN3(0);
+    RUN3(1);
+    RUN3(2);
     RUN(lines, 512, 256);
     RUN(lines, 256, 1024);
     RUN(lines, 128, 2048);
