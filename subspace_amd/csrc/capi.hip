@@ -17,7 +17,7 @@
 namespace subspace_amd {
 
 template <int WG>
-__global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, u32*, int);
+__global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
 
 struct TileDesc;
 __global__ void crc32_ragged_count_kernel(const u64*, u32, u64, u32, u32, u64*, u32*);
@@ -89,7 +89,6 @@ struct subspace_crc_ctx {
   int uniform_wg = 512;    // workgroup size of the uniform kernel (256/512/640/768/1024)
   int uniform_blocks = 0;  // 0 = one workgroup per CU
   int uniform_order = 0;   // tile order: 0 XCD-spread sweep, 1 per-workgroup region, 2 plain sweep
-  u32* d_sink = nullptr;   // scratch words for result stores without a result
   u64* d_uoff = nullptr;  // offsets/lengths materialised for non-4K uniform batches
   u64* d_ulen = nullptr;
   u64 u_capacity = 0;
@@ -275,14 +274,13 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
   hipError_t e = hipMalloc(&c->d_tab, tab.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_ops, ops.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_pow2, pow2.size() * 4);
-  if (e == hipSuccess) e = hipMalloc(&c->d_sink, 64 * sizeof(u32));
   if (e == hipSuccess) e = hipMemcpy(c->d_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_ops, ops.data(), ops.size() * 4, hipMemcpyHostToDevice);
 #define SET_LDS(WGV)                                                                                         \
   if (e == hipSuccess)                                                                                       \
     e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                            (int)lds_bytes(WGV / 64));
+                            (int)uniform_lds_bytes(WGV / 64));
   SET_LDS(256) SET_LDS(512) SET_LDS(768) SET_LDS(1024)
 #undef SET_LDS
   if (e == hipSuccess)
@@ -301,7 +299,6 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_tab);
   (void)hipFree(c->d_ops);
   (void)hipFree(c->d_pow2);
-  (void)hipFree(c->d_sink);
   (void)hipFree(c->d_crc0);
   (void)hipFree(c->d_soff);
   for (auto& kv : c->zinv) (void)hipFree(kv.second);
@@ -369,8 +366,8 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     const auto* b = static_cast<const uint8_t*>(dev_base);
     const int ord = c->uniform_order;
 #define LAUNCH(WGV)                                                                                    \
-  crc32_uniform4k_kernel<WGV><<<blocks, WGV, lds_bytes(WGV / 64), st>>>(b, stride, count, c->d_tab, c->d_ops, init, \
-                                                                        final_xor, dev_out, c->d_sink, ord)
+  crc32_uniform4k_kernel<WGV><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(b, stride, count, c->d_tab,         \
+                                                                                c->d_ops, init, final_xor, dev_out, ord)
     switch (wg) {
       case 256: LAUNCH(256); break;
       case 768: LAUNCH(768); break;

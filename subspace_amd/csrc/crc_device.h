@@ -29,6 +29,16 @@ constexpr u32 kLdsXpose = kLdsOps + kNumOps * 512u;
 constexpr u32 kLdsXposePerWave = 1024u;
 constexpr size_t lds_bytes(int waves) { return kLdsXpose + (size_t)waves * kLdsXposePerWave; }
 
+// Uniform-kernel layout: tables, its 6 operator slots (Z_64, Z_128 .. Z_2048), a 1 KiB
+// transpose buffer per wave, then a per-wave ring of results awaiting their store.
+constexpr int kUniformOps = 6;
+constexpr u32 kUniXpose = kLdsOps + kUniformOps * 512u;
+// results per wave ring (a power of two): as many as fit 155 KiB of LDS
+constexpr int uniform_ring(int waves) { return waves >= 16 ? 128 : waves >= 12 ? 256 : 512; }
+constexpr size_t uniform_lds_bytes(int waves) {
+  return kUniXpose + (size_t)waves * (kLdsXposePerWave + 4u * (size_t)uniform_ring(waves));
+}
+
 // operator slots
 constexpr int kOpZ64 = 0;     // slot 0: Z_64 (joins the two 64-B halves of a line)
 constexpr int kOpZ128 = 1;    // slots 1..6: Z_{128 * 2^k}, k = 0..5 (128 B .. 4 KiB)

@@ -14,11 +14,11 @@
 //    consecutive lines of message j>>3, combined in-lane (Z_128, Z_256) and across 8
 //    lanes (Z_512, Z_1024, Z_2048) with nibble-table GF(2) operators:
 //      crc(msg) = XOR_i Z_{128*(31-i)}(line_i)     (crc_raw linearity)
-//  * The tile loop is unrolled by the 4-tile group, so the result store sits at one fixed
-//    point of the body and is issued by every lane every time (lanes without a result
-//    write a scratch word). vmcnt counts stores too: with the store unconditional the
-//    waitcnt pass knows it is there and waits for the next tile's loads with
-//    vmcnt(9) instead of vmcnt(8) -- which would also wait for the store's write-back.
+//  * Results go to a per-wave LDS ring and are stored to HBM only when the ring is full
+//    (every 256 tiles at 8 waves per CU) and at the end. vmcnt counts stores with the
+//    loads, in order, so a store in the stream makes the wait for the next tile's loads
+//    wait for the store's write-back too: a store every 4 tiles cost ~10 % of a
+//    streaming kernel's rate (tools/ubench/streamread.hip lines_store: 6.0 vs 6.6 TB/s).
 #include "crc_device.h"
 
 namespace subspace_amd {
@@ -27,7 +27,7 @@ template <int WG>
 __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __restrict__ base, u64 stride, u64 count,
                                                              const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                              u32 init, u32 final_xor, u32* __restrict__ out,
-                                                             u32* __restrict__ sink, int order) {
+                                                             int order) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
 
@@ -37,7 +37,10 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
-  const u32 xb = sbase + kLdsXpose + (u32)wid * kLdsXposePerWave;
+  constexpr int kWaves = WG / 64;
+  constexpr int kRing = uniform_ring(kWaves);  // results per wave ring
+  const u32 xb = sbase + kUniXpose + (u32)wid * kLdsXposePerWave;
+  const u32 ring = sbase + kUniXpose + kWaves * kLdsXposePerWave + (u32)wid * (4u * kRing);
   const int l = lane & 31, h = lane >> 5;
   const u64 ntiles = (count + 1) >> 1;
   // Tile order. Sweep (orders 0 and 2): tau = k*nw + w, all waves advance one compact
@@ -98,9 +101,9 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     return crc;
   };
 
-  // Results of the group of tiles kb .. kb+3 (nv of them real): transpose, tree, one store
-  // instruction from every lane.
-  auto group_store = [&](u32 p0, u32 p1, u32 p2, u32 p3, u32 kb, u32 nv) {
+  // Results of the group of tiles kb .. kb+3 (nv of them real): transpose, tree, into the
+  // ring slots 2*(kb - kf + t) + h (kf = first tile of the ring's window).
+  auto group_result = [&](u32 p0, u32 p1, u32 p2, u32 p3, u32 kb, u32 nv, u32 kf) {
     // transpose: message slot M = 2t + h, line l -> xb + M*128 + l*4
     lds_st(xb + (0 + h) * 128 + l * 4, p0);
     lds_st(xb + (2 + h) * 128 + l * 4, p1);
@@ -115,28 +118,34 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     c = opmul(sbase, kOpZ128 + 2, c) ^ __shfl_down(c, 1);  // 1 KiB, valid at even q8
     c = opmul(sbase, kOpZ128 + 3, c) ^ __shfl_down(c, 2);  // 2 KiB, valid at q8 % 4 == 0
     c = opmul(sbase, kOpZ128 + 4, c) ^ __shfl_down(c, 4);  // 4 KiB, valid at q8 == 0
-    const u64 msg = 2 * (t0 + (u64)(kb + (u32)(M >> 1)) * tstep) + (u64)(M & 1);
-    const bool real = q8 == 0 && (u32)(M >> 1) < nv && msg < count;
-    u32* dst = real ? out + msg : sink + lane;
-    *dst = c ^ final_xor;
+    if (q8 == 0 && (u32)(M >> 1) < nv) lds_st(ring + 4u * (2u * (kb - kf) + (u32)M), c ^ final_xor);
+    wave_lds_sync();
+  };
+  // Store the ring's results of tiles kf .. kf+nt-1 (messages 2*tau, 2*tau+1 of each).
+  auto flush = [&](u32 kf, u32 nt) {
+#pragma unroll
+    for (int i = 0; i < kRing / 64; i++) {
+      const u32 slot = (u32)(i * 64 + lane);
+      const u32 t = slot >> 1;
+      const u64 msg = 2 * (t0 + (u64)(kf + t) * tstep) + (u64)(slot & 1u);
+      if (t < nt && msg < count) out[msg] = lds_ld(ring + 4u * slot);
+    }
     wave_lds_sync();
   };
 
-  // Table loads first, then tile 0's loads and a scratch store (so the loop is entered
-  // with the same "loads, then one store" pattern as its back edge), then the LDS stores:
-  // tile 0's latency hides behind the fill and the barrier.
-  LdsFill<WG, kOpZ128 + 5> fill;  // step tables + Z_64, Z_128 .. Z_2048
+  // Table loads first, then tile 0's loads, then the LDS stores: tile 0's latency hides
+  // behind the fill and the barrier.
+  LdsFill<WG, kUniformOps> fill;  // step tables + Z_64, Z_128 .. Z_2048
   fill.load(gtab, gops);
   u32x4 A[8], B[8];
   load_tile(A, 0);
-  sink[lane] = 0u;
   fill.store(sbase);
   __syncthreads();
   if (nk == 0) return;
 
   // Whole groups: ping-pong buffers, the next tile's loads always issued before this
-  // tile's data is waited for, the group's store at the end of the body.
-  u32 k = 0;
+  // tile's data is waited for; the ring is stored when full.
+  u32 k = 0, kf = 0;
   for (; k + 3 < nk; k += 4) {
     load_tile(B, k + 1);
     const u32 p0 = line_crc(A);
@@ -146,7 +155,11 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     const u32 p2 = line_crc(A);
     load_tile(A, k + 4);
     const u32 p3 = line_crc(B);
-    group_store(p0, p1, p2, p3, k, 4u);
+    group_result(p0, p1, p2, p3, k, 4u, kf);
+    if (k + 4 - kf == (u32)(kRing / 2)) {
+      flush(kf, kRing / 2);
+      kf = k + 4;
+    }
   }
   // The last 1..3 tiles (tile k already in A); loads past the end re-read the last tile.
   if (k < nk) {
@@ -155,17 +168,18 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     load_tile(A, k + 2);
     const u32 p1 = line_crc(B);
     const u32 p2 = line_crc(A);
-    group_store(p0, p1, p2, 0u, k, nk - k);
+    group_result(p0, p1, p2, 0u, k, nk - k, kf);
   }
+  if (nk > kf) flush(kf, nk - kf);
 }
 
 template __global__ void crc32_uniform4k_kernel<256>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                     u32*, int);
+                                                     int);
 template __global__ void crc32_uniform4k_kernel<512>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                     u32*, int);
+                                                     int);
 template __global__ void crc32_uniform4k_kernel<768>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                     u32*, int);
+                                                     int);
 template __global__ void crc32_uniform4k_kernel<1024>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                      u32*, int);
+                                                      int);
 
 }  // namespace subspace_amd

@@ -102,6 +102,37 @@ __global__ __launch_bounds__(WG) void lines_store(const u32x4* __restrict__ p, u
   out[blockIdx.x * WG + threadIdx.x] = acc;
 }
 
+// lines_remap sub2 shape with the CRC kernel's workgroup footprint: LDS (dynamic, 152 KiB
+// at launch) and optionally FILL (128 KiB of LDS writes + barrier before the loop) and a
+// CHAIN of dependent LDS round trips every 4 tiles (the combine tree's latency).
+template <int WG, bool FILL, int CHAIN>
+__global__ __launch_bounds__(WG) void lines_lds(const u32x4* __restrict__ p, u64 nchunks, u32* out) {
+  extern __shared__ __attribute__((aligned(16))) u32 smem[];
+  const int lane = threadIdx.x & 63;
+  const u64 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u64 w = ((u64)blockIdx.x + (u64)gridDim.x * (wid / 2)) * 2 + wid % 2;
+  const u64 nw = (u64)gridDim.x * (WG / 64);
+  if (FILL) {
+    for (int i = threadIdx.x; i < 32768; i += WG) smem[i] = (u32)i * 2654435761u;
+    __syncthreads();
+  }
+  u32 acc = 0;
+  u64 k = 0;
+  for (u64 c = w; c < nchunks; c += nw, k++) {
+    const u32x4* q = p + c * 512 + lane * 8;
+    u32x4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = q[i];
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+    if (CHAIN && (k & 3) == 3) {
+#pragma unroll
+      for (int j = 0; j < CHAIN; j++) acc ^= smem[(acc ^ lane) & 32767];
+    }
+  }
+  out[blockIdx.x * WG + threadIdx.x] = acc;
+}
+
 // Lines, but the 8 loads of a lane go out as 16-B pieces interleaved across lanes within
 // 2 KiB: instruction i reads piece (i) of lines lane/... -- kept simple: lane reads its line
 // as 2 x 64 B halves placed 4 KiB apart (two half-tiles), i.e. 32-B granularity per lane.
@@ -148,6 +179,11 @@ int main() {
   u32x4* buf; CK(hipMalloc(&buf, bytes));
   u32* out; CK(hipMalloc(&out, 64ull << 20));
   u32* res; CK(hipMalloc(&res, (bytes / 4096) * 4 + 64));
+  CK(hipFuncSetAttribute((const void*)lines_lds<512, false, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024));
+  CK(hipFuncSetAttribute((const void*)lines_lds<512, true, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024));
+  CK(hipFuncSetAttribute((const void*)lines_lds<512, true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024));
+  CK(hipFuncSetAttribute((const void*)lines_lds<512, true, 32>, hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024));
+  CK(hipFuncSetAttribute((const void*)lines_lds<512, true, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024));
   gen<<<4096, 256>>>(buf, n16);
   CK(hipDeviceSynchronize());
   for (u64 win : {256ull << 20, 1ull << 30, 4ull << 30}) {
@@ -161,21 +197,18 @@ int main() {
 #define RUN(K, WG, G) rep(#K " wg" #WG " grid" #G, time_it([&] { K<WG><<<G, WG>>>(W(), chunks, out); }, 32))
 #define RUN2(WG, SUB, G) rep("lines_remap wg" #WG " sub" #SUB, time_it([&] { lines_remap<WG, SUB><<<G, WG>>>(W(), chunks, out); }, 32))
 #define RUN3(ST) rep("lines_store st" #ST, time_it([&] { lines_store<512, ST><<<256, 512>>>(W(), chunks, out, res); }, 32))
+#define RUN4(F, C) rep("lines_lds fill" #F " chain" #C, time_it([&] { lines_lds<512, F, C><<<256, 512, 152 * 1024>>>(W(), chunks, out); }, 32))
+    RUN4(false, 0);
+    RUN4(true, 0);
+    RUN4(true, 8);
+    RUN4(true, 32);
+    RUN4(true, 128);
     RUN3(0);
     RUN3(1);
     RUN3(2);
     RUN(lines, 512, 256);
     RUN(lines, 256, 1024);
-    RUN(lines, 128, 2048);
-    RUN(lines, 1024, 256);
-    RUN2(512, 4, 256);
     RUN2(512, 2, 256);
-    RUN2(512, 1, 256);
-    RUN2(1024, 4, 256);
-    RUN2(1024, 2, 256);
-    RUN2(1024, 1, 256);
-    RUN(lines, 256, 512);
-    RUN(coalesced, 256, 1024);
   }
   return 0;
 }
