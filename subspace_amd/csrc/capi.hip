@@ -69,6 +69,7 @@ struct subspace_crc_ctx {
   u32* d_tab = nullptr;  // 4 x 256 slice tables
   u32* d_ops = nullptr;  // kNumOps nibble operators
   u32* d_pow2 = nullptr;  // Z_{2^k}, k = 0..63, nibble operators (slot checksums)
+  u32* d_laneops = nullptr;  // uniform kernel: Z_{128*s}, s = 0..31, as [nibble][value][s]
   // zinv[r] = Z_r^{-1}(init), r = 0..127, cached per init value
   std::unordered_map<u32, u32*> zinv;
   Tables host_tab;
@@ -258,7 +259,7 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
   c->host_tab = make_tables();
   c->zinv1 = inverse(z_one(c->host_tab));
 
-  std::vector<u32> tab(1024), ops((size_t)kNumOps * 128, 0u), pow2(64 * 128, 0u);
+  std::vector<u32> tab(1024), ops((size_t)kNumOps * 128, 0u), pow2(64 * 128, 0u), laneops(kLaneOpWords, 0u);
   for (int k = 0; k < 4; k++)
     for (int b = 0; b < 256; b++) tab[k * 256 + b] = c->host_tab.t[k][b];
   nibble_tables(z_bytes(c->host_tab, 64), &ops[(size_t)kOpZ64 * 128]);
@@ -271,7 +272,16 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
     for (int k = 0; k < 64; k++, z = mul(z, z)) nibble_tables(z, &pow2[(size_t)k * 128]);
   }
 
+  for (int sl = 0; sl < 32; sl++) {
+    u32 nt[128];
+    nibble_tables(z_bytes(c->host_tab, 128ull * sl), nt);
+    for (int k = 0; k < 8; k++)
+      for (int n = 0; n < 16; n++) laneops[((size_t)k * 16 + n) * 32 + sl] = nt[k * 16 + n];
+  }
+
   hipError_t e = hipMalloc(&c->d_tab, tab.size() * 4);
+  if (e == hipSuccess) e = hipMalloc(&c->d_laneops, laneops.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(c->d_laneops, laneops.data(), laneops.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&c->d_ops, ops.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_pow2, pow2.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(c->d_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice);
@@ -299,6 +309,7 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_tab);
   (void)hipFree(c->d_ops);
   (void)hipFree(c->d_pow2);
+  (void)hipFree(c->d_laneops);
   (void)hipFree(c->d_crc0);
   (void)hipFree(c->d_soff);
   for (auto& kv : c->zinv) (void)hipFree(kv.second);
@@ -367,7 +378,7 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     const int ord = c->uniform_order;
 #define LAUNCH(WGV)                                                                                    \
   crc32_uniform4k_kernel<WGV><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(b, stride, count, c->d_tab,         \
-                                                                                c->d_ops, init, final_xor, dev_out, ord)
+                                                                                c->d_laneops, init, final_xor, dev_out, ord)
     switch (wg) {
       case 256: LAUNCH(256); break;
       case 768: LAUNCH(768); break;

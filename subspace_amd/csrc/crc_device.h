@@ -29,15 +29,12 @@ constexpr u32 kLdsXpose = kLdsOps + kNumOps * 512u;
 constexpr u32 kLdsXposePerWave = 1024u;
 constexpr size_t lds_bytes(int waves) { return kLdsXpose + (size_t)waves * kLdsXposePerWave; }
 
-// Uniform-kernel layout: tables, its 6 operator slots (Z_64, Z_128 .. Z_2048), a 1 KiB
-// transpose buffer per wave, then a per-wave ring of results awaiting their store.
-constexpr int kUniformOps = 6;
-constexpr u32 kUniXpose = kLdsOps + kUniformOps * 512u;
-// results per wave ring (a power of two): as many as fit 155 KiB of LDS
-constexpr int uniform_ring(int waves) { return waves >= 16 ? 128 : waves >= 12 ? 256 : 512; }
-constexpr size_t uniform_lds_bytes(int waves) {
-  return kUniXpose + (size_t)waves * (kLdsXposePerWave + 4u * (size_t)uniform_ring(waves));
-}
+// Uniform-kernel layout: tables, the per-lane line-shift operators (kLaneOpWords, see
+// crc32_uniform4k_kernel), then a per-wave ring of results awaiting their store.
+constexpr int kLaneOpWords = 8 * 16 * 32;  // [nibble k][value n][lane slot s]: 16 KiB
+constexpr u32 kUniRing = kLdsOps + kLaneOpWords * 4u;
+constexpr int kUniRingResults = 256;  // results per wave ring (128 tiles)
+constexpr size_t uniform_lds_bytes(int waves) { return kUniRing + (size_t)waves * 4u * kUniRingResults; }
 
 // operator slots
 constexpr int kOpZ64 = 0;     // slot 0: Z_64 (joins the two 64-B halves of a line)

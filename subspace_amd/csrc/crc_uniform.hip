@@ -9,16 +9,18 @@
 //    always has the next tile's 8 loads in flight while it computes the current one.
 //  * Per line: 32 slice-by-4 steps from 32-way replicated LDS tables (4 conflict-free
 //    ds_read_b32 + 4 v_perm + 4 v_xor per word).
-//  * Every 4 tiles the wave holds line CRCs of 8 messages (crc_raw(0, line), or with
-//    the batch init for line 0). They are transposed through LDS so lane j holds 4
-//    consecutive lines of message j>>3, combined in-lane (Z_128, Z_256) and across 8
-//    lanes (Z_512, Z_1024, Z_2048) with nibble-table GF(2) operators:
-//      crc(msg) = XOR_i Z_{128*(31-i)}(line_i)     (crc_raw linearity)
+//  * Combine, per tile: lane l of half h holds line l's CRC; the message CRC is
+//      crc(msg) = XOR_l Z_{128*(31-l)}(line_l)      (crc_raw linearity)
+//    Each lane applies its own operator Z_{128*(31-l)} from nibble tables laid out
+//    [nibble k][value n][lane slot], so the 32 lanes of a half read 32 different banks
+//    (conflict-free, 8 ds_read_b32, one LDS round trip), and the XOR over the half is a
+//    DPP reduction (row_shr 1/2/4/8 + row_bcast15: VALU only). Lanes 31 and 63 end with
+//    the two messages' CRCs.
 //  * Results go to a per-wave LDS ring and are stored to HBM only when the ring is full
-//    (every 256 tiles at 8 waves per CU) and at the end. vmcnt counts stores with the
-//    loads, in order, so a store in the stream makes the wait for the next tile's loads
-//    wait for the store's write-back too: a store every 4 tiles cost ~10 % of a
-//    streaming kernel's rate (tools/ubench/streamread.hip lines_store: 6.0 vs 6.6 TB/s).
+//    (every 128 tiles) and at the end. vmcnt counts stores with the loads, in order, so
+//    a store in the stream makes the wait for the next tile's loads wait for the store's
+//    write-back too: a store every 4 tiles cost ~10 % of a streaming kernel's rate
+//    (tools/ubench/streamread.hip lines_store: 6.0 vs 6.6 TB/s).
 #include "crc_device.h"
 
 namespace subspace_amd {
@@ -37,10 +39,9 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
-  constexpr int kWaves = WG / 64;
-  constexpr int kRing = uniform_ring(kWaves);  // results per wave ring
-  const u32 xb = sbase + kUniXpose + (u32)wid * kLdsXposePerWave;
-  const u32 ring = sbase + kUniXpose + kWaves * kLdsXposePerWave + (u32)wid * (4u * kRing);
+  constexpr int kRing = kUniRingResults;
+  const u32 ring = sbase + kUniRing + (u32)wid * (4u * kRing);
+  const u32 lop = sbase + kLdsOps + 4u * (u32)(31 - (lane & 31));  // this lane's operator slot
   const int l = lane & 31, h = lane >> 5;
   const u64 ntiles = (count + 1) >> 1;
   // Tile order. Sweep (orders 0 and 2): tau = k*nw + w, all waves advance one compact
@@ -101,25 +102,17 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     return crc;
   };
 
-  // Results of the group of tiles kb .. kb+3 (nv of them real): transpose, tree, into the
-  // ring slots 2*(kb - kf + t) + h (kf = first tile of the ring's window).
-  auto group_result = [&](u32 p0, u32 p1, u32 p2, u32 p3, u32 kb, u32 nv, u32 kf) {
-    // transpose: message slot M = 2t + h, line l -> xb + M*128 + l*4
-    lds_st(xb + (0 + h) * 128 + l * 4, p0);
-    lds_st(xb + (2 + h) * 128 + l * 4, p1);
-    lds_st(xb + (4 + h) * 128 + l * 4, p2);
-    lds_st(xb + (6 + h) * 128 + l * 4, p3);
-    wave_lds_sync();
-    const int M = lane >> 3, q8 = lane & 7;
-    const u32x4 s = lds_ld4(xb + M * 128 + q8 * 16);  // lines 4*q8 .. 4*q8+3 of slot M
-    const u32 a = opmul(sbase, kOpZ128 + 0, s[0]) ^ s[1];
-    const u32 b = opmul(sbase, kOpZ128 + 0, s[2]) ^ s[3];
-    u32 c = opmul(sbase, kOpZ128 + 1, a) ^ b;              // 4 lines (512 B)
-    c = opmul(sbase, kOpZ128 + 2, c) ^ __shfl_down(c, 1);  // 1 KiB, valid at even q8
-    c = opmul(sbase, kOpZ128 + 3, c) ^ __shfl_down(c, 2);  // 2 KiB, valid at q8 % 4 == 0
-    c = opmul(sbase, kOpZ128 + 4, c) ^ __shfl_down(c, 4);  // 4 KiB, valid at q8 == 0
-    if (q8 == 0 && (u32)(M >> 1) < nv) lds_st(ring + 4u * (2u * (kb - kf) + (u32)M), c ^ final_xor);
-    wave_lds_sync();
+  // Message CRCs of tile k into ring slots 2*(k - kf) + h (kf = first tile of the window).
+  auto tile_result = [&](u32 crc, u32 k, u32 kf) {
+    u32 v = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) v ^= lds_ld(lop + 2048u * j + (((crc >> (4 * j)) & 15u) << 7));
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    if (l == 31) lds_st(ring + 4u * (2u * (k - kf) + (u32)h), v ^ final_xor);
   };
   // Store the ring's results of tiles kf .. kf+nt-1 (messages 2*tau, 2*tau+1 of each).
   auto flush = [&](u32 kf, u32 nt) {
@@ -135,7 +128,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
 
   // Table loads first, then tile 0's loads, then the LDS stores: tile 0's latency hides
   // behind the fill and the barrier.
-  LdsFill<WG, kUniformOps> fill;  // step tables + Z_64, Z_128 .. Z_2048
+  LdsFill<WG, kLaneOpWords / 128> fill;  // step tables + per-lane operators
   fill.load(gtab, gops);
   u32x4 A[8], B[8];
   load_tile(A, 0);
@@ -143,33 +136,23 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   __syncthreads();
   if (nk == 0) return;
 
-  // Whole groups: ping-pong buffers, the next tile's loads always issued before this
-  // tile's data is waited for; the ring is stored when full.
+  // Ping-pong buffers, loop unrolled by two (no early exit: a break between the halves
+  // would give the loop head a predecessor with fewer loads in flight, and hipcc's waitcnt
+  // merge would drain the prefetch there); the ring is stored when full.
   u32 k = 0, kf = 0;
-  for (; k + 3 < nk; k += 4) {
+  for (; k + 1 < nk; k += 2) {
     load_tile(B, k + 1);
-    const u32 p0 = line_crc(A);
+    tile_result(line_crc(A), k, kf);
     load_tile(A, k + 2);
-    const u32 p1 = line_crc(B);
-    load_tile(B, k + 3);
-    const u32 p2 = line_crc(A);
-    load_tile(A, k + 4);
-    const u32 p3 = line_crc(B);
-    group_result(p0, p1, p2, p3, k, 4u, kf);
-    if (k + 4 - kf == (u32)(kRing / 2)) {
+    tile_result(line_crc(B), k + 1, kf);
+    if (k + 2 - kf == (u32)(kRing / 2)) {
+      wave_lds_sync();
       flush(kf, kRing / 2);
-      kf = k + 4;
+      kf = k + 2;
     }
   }
-  // The last 1..3 tiles (tile k already in A); loads past the end re-read the last tile.
-  if (k < nk) {
-    load_tile(B, k + 1);
-    const u32 p0 = line_crc(A);
-    load_tile(A, k + 2);
-    const u32 p1 = line_crc(B);
-    const u32 p2 = line_crc(A);
-    group_result(p0, p1, p2, 0u, k, nk - k, kf);
-  }
+  if (k < nk) tile_result(line_crc(A), k, kf);  // odd last tile, already loaded
+  wave_lds_sync();
   if (nk > kf) flush(kf, nk - kf);
 }
 

@@ -158,3 +158,33 @@ def test_uniform_line_as_two_64b_chains():
     for init in (M32, 0, 0x0BADCAFE):
         line = rng.integers(0, 256, 128, dtype=np.uint8).tobytes()
         assert apply(z64, crc_raw(init, line[:64])) ^ crc_raw(0, line[64:]) == crc_raw(init, line)
+
+
+def dpp_half_xor(vals):
+    """crc32_uniform4k_kernel's reduction: XOR with row_shr 1, 2, 4, 8 (lanes whose source
+    falls outside the 16-lane row keep their value), then row_bcast:15 into rows 1 and 3.
+    Returns the 64 lane values."""
+    v = list(vals)
+    for n in (1, 2, 4, 8):
+        v = [v[i] ^ (v[i - n] if (i % 16) >= n else 0) for i in range(64)]
+    bc = [0] * 64
+    for r in (1, 3):
+        for i in range(16 * r, 16 * r + 16):
+            bc[i] = v[16 * r - 1]
+    return [v[i] ^ bc[i] for i in range(64)]
+
+
+def test_uniform_per_lane_operators_and_dpp_reduction():
+    """Per tile: lane l of half h applies Z_{128*(31-l)} to its line CRC; the DPP
+    reduction leaves message 2*tau + h's CRC in lane 32*h + 31."""
+    ops = [zbytes(128 * s) for s in range(32)]
+    rng = np.random.default_rng(31)
+    for init in (M32, 0x1234ABCD):
+        msgs = [rng.integers(0, 256, 4096, dtype=np.uint8).tobytes() for _ in range(2)]
+        lanes = []
+        for h in range(2):
+            for l in range(32):
+                line = msgs[h][128 * l:128 * l + 128]
+                lanes.append(apply(ops[31 - l], crc_raw(init if l == 0 else 0, line)))
+        red = dpp_half_xor(lanes)
+        assert red[31] == ref(init, msgs[0]) and red[63] == ref(init, msgs[1])
