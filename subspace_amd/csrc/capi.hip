@@ -3,6 +3,7 @@
 // sizes, int status codes, thread-local error strings.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -67,7 +68,7 @@ struct subspace_crc_ctx {
   int device = 0;
   int num_cus = 256;
   u32* d_tab = nullptr;  // 4 x 256 slice tables
-  u32* d_ops = nullptr;  // kNumOps nibble operators
+  u32* d_rops = nullptr;  // ragged kernel: line-shift operators + Z_4096 + tile shifts (kRagOpWords)
   u32* d_pow2 = nullptr;  // Z_{2^k}, k = 0..63, nibble operators (slot checksums)
   u32* d_laneops = nullptr;  // uniform kernel: Z_{128*s}, s = 0..31, as [nibble][value][s]
   // zinv[r] = Z_r^{-1}(init), r = 0..127, cached per init value
@@ -187,9 +188,9 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
       c->d_overflow);
   HIP_TRY(hipGetLastError());
   const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU
-  crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, lds_bytes(kRaggedWG / 64), st>>>(
+  crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, ragged_lds_bytes(), st>>>(
       base, offsets, ostride, lengths, lstride, c->d_tbase, count, reinterpret_cast<const TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_tab, c->d_ops, zinv, final_xor, out, c->d_tilecrc);
+      c->d_overflow, c->d_tab, c->d_rops, zinv, final_xor, out, c->d_tilecrc);
   HIP_TRY(hipGetLastError());
   // message CRC = XOR of its tiles' values = difference of two XOR-scan entries (entries
   // past the batch's real tile count are scanned but never read)
@@ -259,13 +260,9 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
   c->host_tab = make_tables();
   c->zinv1 = inverse(z_one(c->host_tab));
 
-  std::vector<u32> tab(1024), ops((size_t)kNumOps * 128, 0u), pow2(64 * 128, 0u), laneops(kLaneOpWords, 0u);
+  std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kLaneOpWords, 0u), rops(kRagOpWords, 0u);
   for (int k = 0; k < 4; k++)
     for (int b = 0; b < 256; b++) tab[k * 256 + b] = c->host_tab.t[k][b];
-  nibble_tables(z_bytes(c->host_tab, 64), &ops[(size_t)kOpZ64 * 128]);
-  for (int k = 0; k < 6; k++) nibble_tables(z_bytes(c->host_tab, 128ull << k), &ops[(size_t)(kOpZ128 + k) * 128]);
-  for (int k = 0; k < kNumTileOps; k++)
-    nibble_tables(z_bytes(c->host_tab, 8192ull << k), &ops[(size_t)(kOpZTile + k) * 128]);
 
   {
     Mat32 z = z_one(c->host_tab);
@@ -278,15 +275,19 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
     for (int k = 0; k < 8; k++)
       for (int n = 0; n < 16; n++) laneops[((size_t)k * 16 + n) * 32 + sl] = nt[k * 16 + n];
   }
+  // ragged kernel: the line-shift operators, Z_4096, then Z_{8192 * 2^k} for k = 0..30
+  std::copy(laneops.begin(), laneops.end(), rops.begin());
+  nibble_tables(z_bytes(c->host_tab, 4096), &rops[kLaneOpWords]);
+  for (int k = 0; k < 31; k++) nibble_tables(z_bytes(c->host_tab, 8192ull << k), &rops[kLaneOpWords + 128 * (1 + k)]);
 
   hipError_t e = hipMalloc(&c->d_tab, tab.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_laneops, laneops.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(c->d_laneops, laneops.data(), laneops.size() * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc(&c->d_ops, ops.size() * 4);
+  if (e == hipSuccess) e = hipMalloc(&c->d_rops, rops.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_pow2, pow2.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(c->d_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(c->d_ops, ops.data(), ops.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->d_rops, rops.data(), rops.size() * 4, hipMemcpyHostToDevice);
 #define SET_LDS(WGV)                                                                                         \
   if (e == hipSuccess)                                                                                       \
     e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
@@ -295,7 +296,7 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
 #undef SET_LDS
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_ragged_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds_bytes(kRaggedWG / 64));
+                            (int)ragged_lds_bytes());
   if (e != hipSuccess) {
     subspace_crc_ctx_destroy(c);
     return hip_fail(e, "context setup");
@@ -307,7 +308,7 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
 void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   if (!c) return;
   (void)hipFree(c->d_tab);
-  (void)hipFree(c->d_ops);
+  (void)hipFree(c->d_rops);
   (void)hipFree(c->d_pow2);
   (void)hipFree(c->d_laneops);
   (void)hipFree(c->d_crc0);

@@ -7,10 +7,13 @@
 //                      (l & 31), i.e. LDS bank (l & 31), so the 4 data-dependent lookups
 //                      of a step are bank-conflict-free for any data (ds_read_b32 banks
 //                      lanes in two groups of 32, bank = dword address mod 32).
-//   [128 KiB, +16 KiB) 32 GF(2) operator slots, each 8 nibble tables x 16 dwords (512 B).
-//                      A 16-entry table spans 16 distinct banks, so nibble lookups are
+//   [128 KiB, +16 KiB) per-lane line-shift operators Z_{128*s}, s = 0..31, laid out
+//                      [nibble k][value n][slot s]: the 32 lanes of a half read 32
+//                      different banks (conflict-free for any data).
+//   [144 KiB, ...)     uniform kernel: per-wave result rings; ragged kernel: 22 GF(2)
+//                      operator slots, each 8 nibble tables x 16 dwords (512 B). A
+//                      16-entry table spans 16 distinct banks, so nibble lookups are
 //                      conflict-free without replication.
-//   [144 KiB, ...)     1 KiB per wave: transpose buffer for the combine tree.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -23,11 +26,7 @@ using i64 = int64_t;
 using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
 
 constexpr u32 kLdsTables = 0;
-constexpr u32 kLdsOps = 128u * 1024u;
-constexpr int kNumOps = 32;
-constexpr u32 kLdsXpose = kLdsOps + kNumOps * 512u;
-constexpr u32 kLdsXposePerWave = 1024u;
-constexpr size_t lds_bytes(int waves) { return kLdsXpose + (size_t)waves * kLdsXposePerWave; }
+constexpr u32 kLdsOps = 128u * 1024u;  // operator area; opmul slot s = 512 B at kLdsOps + 512*s
 
 // Uniform-kernel layout: tables, the per-lane line-shift operators (kLaneOpWords, see
 // crc32_uniform4k_kernel), then a per-wave ring of results awaiting their store.
@@ -36,11 +35,17 @@ constexpr u32 kUniRing = kLdsOps + kLaneOpWords * 4u;
 constexpr int kUniRingResults = 256;  // results per wave ring (128 tiles)
 constexpr size_t uniform_lds_bytes(int waves) { return kUniRing + (size_t)waves * 4u * kUniRingResults; }
 
-// operator slots
-constexpr int kOpZ64 = 0;     // slot 0: Z_64 (joins the two 64-B halves of a line)
-constexpr int kOpZ128 = 1;    // slots 1..6: Z_{128 * 2^k}, k = 0..5 (128 B .. 4 KiB)
-constexpr int kOpZTile = 7;   // slots 7..27: Z_{8192 * 2^k}, k = 0..20 (8 KiB .. 8 GiB)
+// Ragged-kernel layout: tables, the same line-shift operators, then opmul slots Z_4096 and
+// Z_{8192 * 2^k}, k = 0..20 (8 KiB .. 8 GiB). The device operator array continues with
+// Z_{8192 * 2^k}, k = 21..30, read from global memory (messages of 16 GiB and more).
 constexpr int kNumTileOps = 21;
+constexpr int kRagOpZ4096 = kLaneOpWords * 4 / 512;  // opmul slot 32
+constexpr int kRagOpZTile = kRagOpZ4096 + 1;
+constexpr int kRagLdsOpWords = kLaneOpWords + (1 + kNumTileOps) * 128;
+constexpr int kRagHighOps = kRagLdsOpWords;  // word offset of Z_{8192 * 2^21} in the device array
+constexpr int kRagOpWords = kRagLdsOpWords + (31 - kNumTileOps) * 128;
+constexpr size_t ragged_lds_bytes() { return kLdsOps + (size_t)kRagLdsOpWords * 4u; }
+static_assert(ragged_lds_bytes() <= 160u * 1024u, "ragged kernel LDS exceeds 160 KiB");
 
 typedef __attribute__((address_space(3))) u32 lds_u32_t;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;

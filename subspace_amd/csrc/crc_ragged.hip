@@ -15,20 +15,24 @@
 //  * Waves stream the global tile list in sweep order (tau = k*nw + w), one tile of
 //    loads in flight ahead. Per-tile descriptors (tile end, message start, message id,
 //    tiles after) are precomputed by crc32_ragged_desc_kernel.
-//  * Every 4 tiles the 256 line CRCs are transposed through LDS (16 lanes per tile),
-//    tree-combined (Z_128..Z_4096), multiplied by Z_{8192*T} (T = tiles after this one
-//    in the message, binary decomposition over nibble operators) and stored per tile:
-//    tilecrc[tau]. A message's CRC is the XOR of its tiles' values, i.e. the difference of
-//    two entries of the inclusive XOR-scan of tilecrc (crc32_ragged_final_kernel). No
-//    atomics: huge messages (config D: 8192 tiles each, all in flight at once) would
-//    otherwise serialise every tile on one output word.
+//  * Per tile, lane l of half h applies its own line-shift operator Z_{128*(31-l)} (the
+//    uniform kernel's conflict-free [nibble][value][lane] tables) and a DPP reduction
+//    leaves the two half-tile values in lanes 31 and 63. They are parked, one tile per
+//    lane, in registers (lane k&63 keeps tile k); every 64 tiles each lane finishes its own tile,
+//      tile value = Z_{8192*T}( Z_4096(half0) ^ half1 )     (T = tiles after it)
+//    with a per-lane binary decomposition of T over nibble operators -- one wave pass
+//    shifts 64 tiles -- and stores tilecrc[tau]. A message's CRC is the XOR of its tiles'
+//    values, i.e. the difference of two entries of the inclusive XOR-scan of tilecrc
+//    (crc32_ragged_final_kernel). No atomics: huge messages (config D: 8192 tiles each,
+//    all in flight at once) would otherwise serialise every tile on one output word.
 //    (Batches whose tiles overflow the workspace -- overlapping messages -- fall back to
 //    atomicXor into pre-zeroed words.)
-//  * End-aligned lines are 16-B misaligned when e is: each lane then loads the 9
-//    aligned 16-B blocks covering its line and realigns with v_alignbyte_b32 (the
-//    dword shift e&15 >> 2 is wave-uniform, so it is a 4-way uniform switch).
-//    Loads never touch a 16-B block that contains no message byte, so nothing outside
-//    the messages' own aligned blocks is read.
+//  * End-aligned lines are 16-B misaligned when e is. Each lane loads the 8 aligned 16-B
+//    blocks starting at or below its line; the line's last e&15 bytes sit in the next
+//    lane's first block, which arrives by a DPP wave shift, and for lane 63 in the tile's
+//    last (partial) block, one load shared by the whole wave. The words are realigned
+//    with v_alignbyte_b32 (the dword shift (e&15)>>2 is wave-uniform: a 4-way uniform
+//    switch). Loads never touch a 16-B block that holds no message byte.
 #include <hipcub/hipcub.hpp>
 
 #include "crc_device.h"
@@ -112,44 +116,51 @@ __global__ void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, u32 os
 
 // ------------------------------------------------------------------ main kernel
 struct LineState {
-  u32x4 d[9];  // aligned 16-B blocks covering the lane's line (9th only when misaligned)
+  u32x4 d[8];  // the 8 aligned 16-B blocks starting at or below the lane's line
+  u32x4 x;     // the tile's last aligned block (the same for every lane)
 };
 
 template <int Q>
-__device__ __forceinline__ u32 word_at(const LineState& L, int j, u32 m3) {
+__device__ __forceinline__ u32 word_at(const u32x4 (&d)[9], int j, u32 m3) {
   // word j of the realigned line: bytes [4(j+Q) + m3, +4) of the aligned window
   const int x = j + Q;
-  const u32 lo = L.d[x >> 2][x & 3];
-  const u32 hi = L.d[(x + 1) >> 2][(x + 1) & 3];
+  const u32 lo = d[x >> 2][x & 3];
+  const u32 hi = d[(x + 1) >> 2][(x + 1) & 3];
   return __builtin_amdgcn_alignbyte(hi, lo, m3);
 }
 
 template <int Q, bool MIS>
-__device__ __forceinline__ u32 crc_line(const LineState& L, u32 crc, u32 m3, u32 lc0, u32 lc1) {
+__device__ __forceinline__ u32 crc_line(const u32x4 (&d)[9], u32 crc, u32 m3, u32 lc0, u32 lc1) {
 #pragma unroll
   for (int j = 0; j < 32; j++) {
-    const u32 w = MIS ? word_at<Q>(L, j, m3) : L.d[j >> 2][j & 3];
+    const u32 w = MIS ? word_at<Q>(d, j, m3) : d[j >> 2][j & 3];
     crc = step4(crc ^ w, lc0, lc1);
   }
   return crc;
 }
 
+// Nibble operator read from global memory (the tile-shift operators for 2^21 tiles and
+// more, which only messages of 16 GiB and more need).
+__device__ __forceinline__ u32 opmul_global(const u32* __restrict__ op, u32 v) {
+  u32 r = op[v & 15u];
+#pragma unroll
+  for (int k = 1; k < 8; k++) r ^= op[16 * k + ((v >> (4 * k)) & 15u)];
+  return r;
+}
+
 template <int WG, bool DESC>
-__device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
-                                                          const u64* __restrict__ offsets, u32 ostride,
-                                                          const u64* __restrict__ lengths, u32 lstride,
-                                                          const u64* __restrict__ tile_base, u64 count,
-                                                          const TileDesc* __restrict__ desc,
-                                                          const u32* __restrict__ overflow,
-                                                          const u32* __restrict__ gtab, const u32* __restrict__ gops,
-                                                          const u32* __restrict__ zinv, u32 final_xor,
-                                                          u32* __restrict__ out, u32* __restrict__ tilecrc,
-                                                          u32 sbase) {
+__device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, const u64* __restrict__ offsets,
+                                            u32 ostride, const u64* __restrict__ lengths, u32 lstride,
+                                            const u64* __restrict__ tile_base, u64 count,
+                                            const TileDesc* __restrict__ desc, const u32* __restrict__ gtab,
+                                            const u32* __restrict__ gops, const u32* __restrict__ zinv,
+                                            u32 final_xor, u32* __restrict__ out, u32* __restrict__ tilecrc,
+                                            u32 sbase) {
   const int lane = threadIdx.x & 63;
   const u32 wid = rfl(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
-  const u32 xb = sbase + kLdsXpose + wid * kLdsXposePerWave;
+  const u32 lop = sbase + kLdsOps + 4u * (u32)(31 - (lane & 31));  // this lane's line-shift operator
   const u64 total = tile_base[count];
   const u64 w = front_slot(blockIdx.x, gridDim.x, wid);  // sweep front slot (crc_device.h)
   const u64 nw = (u64)gridDim.x * (WG / 64);
@@ -186,18 +197,21 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
     t.pad = 0;
     return t;
   };
-  // Issue the loads of this lane's line for tile descriptor d, as buffer loads against a
-  // scalar resource spanning exactly the tile's blocks that hold message bytes:
+  // Issue the loads of tile d, as buffer loads against a scalar resource spanning exactly
+  // the tile's blocks that hold message bytes:
   //   [max(aligned tile start, aligned message start), tile end rounded up to 16).
-  // Blocks outside it (before the message, or an aligned line's 9th block) read as zeros
-  // without touching memory, so every lane issues all 9 loads (no divergent branch around
-  // loads) and nothing outside the message's own blocks is ever read. A per-lane offset
-  // below the range start wraps to a huge value: out of range as well. `live` false (a
-  // prefetch past the wave's last tile) gives an empty range.
+  // Lane l loads the 8 blocks from a - 128*(64-l) (a = tile end rounded down to 16); blocks
+  // before the range start (before the message) read as zeros without touching memory (a
+  // per-lane offset below the start wraps to a huge value), so every lane issues every
+  // load (no divergent branch around loads). The 9th load is the same for all lanes: the
+  // tile's last block [a, a+16) when the end is misaligned (it is inside the range), else
+  // the dummy [a-16, a). `live` false (a prefetch past the wave's last tile) gives an
+  // empty range.
   auto load_line = [&](const TileDesc& d, LineState& L, bool live) {
     const i64 t0a = ((i64)d.tile_end - 8192) & ~(i64)15;
     const i64 sa = (i64)d.msg_start & ~(i64)15;
     const i64 rb = t0a > sa ? t0a : sa;
+    const i64 a = (i64)d.tile_end & ~(i64)15;
     const i64 rend = ((i64)d.tile_end + 15) & ~(i64)15;
     const u32 nrec = live ? (u32)(rend - rb) : 0u;
     const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + rb), (short)0, (int)nrec,
@@ -205,108 +219,112 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
     const u32 vo = (u32)lane * 128u - (u32)(rb - t0a);
 #pragma unroll
     for (int b = 0; b < 8; b++) L.d[b] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16u * b, 0, 0);
-    // The 9th block of an aligned tile's last line starts exactly at the range end; its
-    // offset goes in the VGPR (not folded into the instruction offset), so the range check
-    // sees it whichever offsets the hardware includes.
-    u32 vo8;
-    asm volatile("v_add_u32 %0, 0x80, %1" : "=v"(vo8) : "v"(vo));
-    L.d[8] = __builtin_amdgcn_raw_buffer_load_b128(r, vo8, 0, 0);
+    // the shared block's offset goes in the VGPR (not the scalar offset), so the range
+    // check sees it whichever offsets the hardware includes
+    const u32 xo = vzero + (u32)((rend > a ? a : a - 16) - rb);
+    L.x = __builtin_amdgcn_raw_buffer_load_b128(r, xo, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  u32 part[4] = {0, 0, 0, 0};
-  u32 gmsg[4] = {0, 0, 0, 0}, gafter[4] = {0, 0, 0, 0};
-  u32 gfirst = 0;  // bit t: tile t of the group is its message's first tile
+  // Half-tile values parked one tile per lane (slot k & 63), finished every 64 tiles.
+  u32 H0 = 0, H1 = 0, AF = 0, MG = 0;  // half 0, half 1, after | first << 31, message
 
-  auto process = [&](LineState& cur, const TileDesc& dcur, u64 k) {
+  auto process = [&](const LineState& cur, const TileDesc& dcur, u64 k) {
     const i64 tile_start = (i64)dcur.tile_end - 8192;
     const i64 line_start = tile_start + (i64)lane * 128;
     const i64 s = (i64)dcur.msg_start;
     const bool partial = tile_start < s;  // wave-uniform
     const bool active = line_start + 128 > s;
-    u32 crc;
+    const u32 mis = (u32)(dcur.tile_end & 15);
+    u32x4 d[9];
+#pragma unroll
+    for (int b = 0; b < 8; b++) d[b] = cur.d[b];
+    if (mis) {  // wave-uniform: lane l's 9th block is lane l+1's first, lane 63's the shared one
+#pragma unroll
+      for (int x = 0; x < 4; x++)
+        d[8][x] = (u32)__builtin_amdgcn_update_dpp((int)cur.x[x], (int)cur.d[0][x], 0x130, 0xF, 0xF, false);
+    } else {
+      d[8] = u32x4{0u, 0u, 0u, 0u};
+    }
     if (partial) {
-      // zero every byte below the message start (this also clears redirected blocks),
-      // seed the first line with zinv[r]
-      const i64 a0 = line_start & ~(i64)15;
+      // zero every byte of the 144-B window below the message start, seed the first line
+      // with zinv[r]
+      const i64 zb64 = s - (line_start & ~(i64)15);
+      const u32 zb = zb64 <= 0 ? 0u : (zb64 >= 144 ? 144u : (u32)zb64);
 #pragma unroll
       for (int b = 0; b < 9; b++) {
 #pragma unroll
         for (int x = 0; x < 4; x++) {
-          const i64 addr = a0 + 16 * b + 4 * x;
+          const u32 p = 16u * b + 4u * x;
           u32 keep = 0xFFFFFFFFu;
-          if (addr + 4 <= s) keep = 0;
-          else if (addr < s) keep = 0xFFFFFFFFu << (8 * (u32)(s - addr));
-          cur.d[b][x] &= keep;
+          if (p + 4u <= zb) keep = 0;
+          else if (p < zb) keep = 0xFFFFFFFFu << (8u * (zb - p));
+          d[b][x] &= keep;
         }
       }
     }
     // the line holding the message's first byte starts from zinv[r] (precomputed seed)
-    crc = (active && line_start <= s) ? dcur.seed : 0u;
-    const u32 mis = (u32)(dcur.tile_end & 15);
+    u32 crc = (active && line_start <= s) ? dcur.seed : 0u;
     const u32 m3 = mis & 3;
     switch (mis >> 2) {  // wave-uniform
-      case 0: crc = mis ? crc_line<0, true>(cur, crc, m3, lc0, lc1) : crc_line<0, false>(cur, crc, m3, lc0, lc1); break;
-      case 1: crc = crc_line<1, true>(cur, crc, m3, lc0, lc1); break;
-      case 2: crc = crc_line<2, true>(cur, crc, m3, lc0, lc1); break;
-      default: crc = crc_line<3, true>(cur, crc, m3, lc0, lc1); break;
+      case 0: crc = mis ? crc_line<0, true>(d, crc, m3, lc0, lc1) : crc_line<0, false>(d, crc, m3, lc0, lc1); break;
+      case 1: crc = crc_line<1, true>(d, crc, m3, lc0, lc1); break;
+      case 2: crc = crc_line<2, true>(d, crc, m3, lc0, lc1); break;
+      default: crc = crc_line<3, true>(d, crc, m3, lc0, lc1); break;
     }
     if (!active) crc = 0;
 
-    const int t = (int)(k & 3);
-    // static-index stores keep part[] / gmsg[] / gafter[] in registers
+    // line l of half h -> Z_{128*(31-l)}(line): 8 conflict-free nibble lookups; then XOR
+    // over each half with DPP (lane 31: lines 0..31, lane 63: lines 32..63)
+    u32 v = 0;
 #pragma unroll
-    for (int tt = 0; tt < 4; tt++)
-      if (tt == t) {
-        part[tt] = crc;
-        gmsg[tt] = dcur.msg;
-        gafter[tt] = dcur.after;
-      }
-    gfirst = (partial || tile_start == s) ? (gfirst | (1u << t)) : (gfirst & ~(1u << t));
+    for (int j = 0; j < 8; j++) v ^= lds_ld(lop + 2048u * j + (((crc >> (4 * j)) & 15u) << 7));
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    const int slot = (int)(k & 63);
+    const bool first = partial || tile_start == s;
+    const u32 h0 = (u32)__builtin_amdgcn_readlane((int)v, 31), h1 = (u32)__builtin_amdgcn_readlane((int)v, 63);
+    const bool mine = lane == slot;  // one compare, four selects of wave-uniform values
+    H0 = mine ? h0 : H0;
+    H1 = mine ? h1 : H1;
+    AF = mine ? (dcur.after | (first ? 0x80000000u : 0u)) : AF;
+    MG = mine ? dcur.msg : MG;
+  };
 
-    if (t == 3 || k + 1 == nk) {
-#pragma unroll
-      for (int tt = 0; tt < 4; tt++) lds_st(xb + tt * 256 + lane * 4, part[tt]);
-      wave_lds_sync();
-      const int T = lane >> 4, q = lane & 15;
-      const u32x4 sv = lds_ld4(xb + T * 256 + q * 16);  // lines 4q..4q+3 of group tile T
-      const u32 a = opmul(sbase, kOpZ128 + 0, sv[0]) ^ sv[1];
-      const u32 b = opmul(sbase, kOpZ128 + 0, sv[2]) ^ sv[3];
-      u32 c = opmul(sbase, kOpZ128 + 1, a) ^ b;               // 512 B
-      c = opmul(sbase, kOpZ128 + 2, c) ^ __shfl_down(c, 1);   // 1 KiB
-      c = opmul(sbase, kOpZ128 + 3, c) ^ __shfl_down(c, 2);   // 2 KiB
-      c = opmul(sbase, kOpZ128 + 4, c) ^ __shfl_down(c, 4);   // 4 KiB
-      c = opmul(sbase, kOpZ128 + 5, c) ^ __shfl_down(c, 8);   // 8 KiB: tile result at q == 0
-      const bool valid = (u64)T <= (u64)t;                     // group slot holds a tile
-      u32 after = 0, msg = 0;
-#pragma unroll
-      for (int tt = 0; tt < 4; tt++)
-        if (tt == T) { after = gafter[tt]; msg = gmsg[tt]; }
-      // shift to the message end: Z_{8192 * after}, binary decomposition (wave-uniform loop)
-      u32 rem = (q == 0 && valid) ? after : 0u;
-      for (int bit = 0; bit < kNumTileOps && __any(rem != 0u); bit++) {
-        const u32 cm = opmul(sbase, kOpZTile + bit, c);
-        c = (rem & 1u) ? cm : c;
-        rem >>= 1;
+  // Finish and store the parked tiles kf .. kf+nt-1 (lane i holds tile kf + i).
+  auto flush = [&](u64 kf, u32 nt) {
+    const bool valid = (u32)lane < nt;
+    u32 c = opmul(sbase, kRagOpZ4096, H0) ^ H1;  // the tile's 8 KiB from its two halves
+    u32 rem = valid ? (AF & 0x7FFFFFFFu) : 0u;   // shift to the message end: Z_{8192 * after}
+    int bit = 0;
+    for (; bit < kNumTileOps && __any(rem != 0u); bit++) {
+      const u32 cm = opmul(sbase, kRagOpZTile + bit, c);
+      c = (rem & 1u) ? cm : c;
+      rem >>= 1;
+    }
+    for (; bit < 31 && __any(rem != 0u); bit++) {  // messages of 16 GiB and more
+      const u32 cm = opmul_global(gops + kRagHighOps + 128 * (bit - kNumTileOps), c);
+      c = (rem & 1u) ? cm : c;
+      rem >>= 1;
+    }
+    if (AF >> 31) c ^= final_xor;
+    if (valid) {
+      if (DESC) {
+        tilecrc[(kf + (u64)lane) * nw + w] = c;
+      } else if ((AF >> 31) && (AF & 0x7FFFFFFFu) == 0u) {
+        out[MG] = c;  // single-tile message
+      } else {
+        atomicXor(&out[MG], c);
       }
-      if (q == 0 && valid) {
-        const bool first = (gfirst >> T) & 1u;
-        const u32 contrib = first ? (c ^ final_xor) : c;
-        if (DESC) {
-          tilecrc[((k & ~(u64)3) + (u64)T) * nw + w] = contrib;  // tile tau of group slot T
-        } else if (first && after == 0) {
-          out[msg] = contrib;  // single-tile message
-        } else {
-          atomicXor(&out[msg], contrib);
-        }
-      }
-      wave_lds_sync();
     }
   };
 
   // Prologue: table loads, then descriptors 0 and 1 and tile 0's line loads, then the LDS
   // stores and the barrier (tile 0's latency hides behind the fill).
-  LdsFill<WG, kOpZTile + kNumTileOps> fill;
+  LdsFill<WG, kRagLdsOpWords / 128> fill;
   fill.load(gtab, gops);
   u32x4 dA[2], dB[2];
   fetch_desc(0, dA);
@@ -321,7 +339,8 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
   // Ping-pong line buffers, loop unrolled by two, descriptors two tiles ahead. The body
   // has no early exit (a break between the halves would give the loop head a predecessor
   // with fewer loads in flight, and hipcc's waitcnt merge would drain the prefetch there);
-  // an odd last tile, already loaded, follows the loop.
+  // an odd last tile, already loaded, follows the loop. The parked tiles are finished
+  // whenever all 64 slots are full, and once more at the end.
   u64 k = 0;
   for (; k + 1 < nk; k += 2) {
     const TileDesc d1 = unpack(dB);   // tile k+1
@@ -333,10 +352,12 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base,
     load_line(d2, A, k + 2 < nk);
     process(B, d1, k + 1);
     dcur = d2;
+    if (((k + 2) & 63) == 0) flush(k + 2 - 64, 64u);
   }
   if (k < nk) process(A, dcur, k);
+  const u64 kf = nk & ~(u64)63;
+  if (nk > kf) flush(kf, (u32)(nk - kf));
 }
-
 
 template <int WG>
 __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restrict__ base,
@@ -353,11 +374,11 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
   // Precomputed descriptors unless the batch had more tiles than the workspace holds
   // (overlapping messages); then every tile is located by binary search.
   if (*overflow == 0u)
-    ragged_body<WG, true>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, overflow, gtab, gops, zinv,
+    ragged_body<WG, true>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, zinv,
                           final_xor, out, tilecrc, sbase);
   else
-    ragged_body<WG, false>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, overflow, gtab, gops,
-                           zinv, final_xor, out, tilecrc, sbase);
+    ragged_body<WG, false>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, zinv,
+                           final_xor, out, tilecrc, sbase);
 }
 
 template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,

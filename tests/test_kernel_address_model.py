@@ -1,5 +1,5 @@
 """CPU models of the kernels' load addresses and tile indexing (subspace_amd/csrc/
-crc_ragged.hip make_desc + load_line, crc_uniform.hip tile_rsrc / load_tile, and the sweep
+crc_ragged.hip make_desc + load_line + the 9th-block wave shift, crc_uniform.hip tile_rsrc / load_tile, and the sweep
 front mapping): every byte any load can read lies inside the caller's messages, every
 message byte is read, every tile is visited exactly once. Runs without a GPU."""
 import numpy as np
@@ -15,7 +15,9 @@ def tiles_for_length(n):
 def ragged_loads(s, e):
     """For message [s, e): (tile j, lane, block, address or None) for every load of
     load_line -- buffer loads against the range [rb, rend), offsets are 32-bit (wrapping);
-    an offset >= the range size reads zeros without a memory access (None)."""
+    an offset >= the range size reads zeros without a memory access (None). Blocks 0..7
+    are the lane's own; block 8 is the load shared by the wave (same address in every
+    lane): the tile's last block [a, a+16) if the end is misaligned, else [a-16, a)."""
     n = e - s
     nt = tiles_for_length(n)
     for j in range(nt):
@@ -23,13 +25,32 @@ def ragged_loads(s, e):
         t0a = (tile_end - 8192) & ~15
         sa = s & ~15
         rb = max(t0a, sa)
+        a = tile_end & ~15
         rend = (tile_end + 15) & ~15
         nrec = rend - rb
+        xo = ((a if rend > a else a - 16) - rb) % M32
         for lane in range(64):
             vo = (lane * 128 - (rb - t0a)) % M32
-            for b in range(9):
+            for b in range(8):
                 off = (vo + 16 * b) % M32
                 yield j, lane, b, (rb + off if off < nrec else None)
+            yield j, lane, 8, (rb + xo if xo < nrec else None)
+
+
+def ragged_line_window(s, e, j, lane):
+    """The 9 blocks process() realigns for (tile j, lane): its own 8, then lane+1's block
+    0 (DPP wave_shl:1) or, for lane 63, the shared block (zeros when the tile end is
+    16-B aligned) -- as addresses (None = zeros)."""
+    loads = {}
+    for jj, ln, b, addr in ragged_loads(s, e):
+        if jj == j:
+            loads[(ln, b)] = addr
+    own = [loads[(lane, b)] for b in range(8)]
+    nt = tiles_for_length(e - s)
+    if ((e - ((nt - 1 - j) << 13)) & 15) == 0:
+        return own + [None]  # aligned tile end: the 9th block is not used (zeros)
+    nxt = loads[(lane + 1, 0)] if lane < 63 else loads[(63, 8)]
+    return own + [nxt]
 
 
 @pytest.mark.parametrize("seed", range(6))
@@ -46,6 +67,30 @@ def test_every_ragged_load_stays_in_its_message_blocks(seed):
                 continue
             # a 16-B block that holds at least one message byte
             assert addr + 16 > s and addr < e, (s, e, j, lane, b, addr)
+
+
+@pytest.mark.parametrize("s,n", [(0, 1), (3, 100), (17, 8192), (5, 8193), (0, 4096), (1, 65536 + 7), (15, 24577),
+                                 (64, 16384 + 9), (7, 8192 * 3)])
+def test_ragged_line_windows_hold_each_line(s, n):
+    """Every lane's realigned 128-B line [E - 128(64-l), +128) is read from its 9-block
+    window: blocks at consecutive 16-B steps from the aligned start, the 9th through the
+    wave shift -- and every message byte of the line comes from a real load."""
+    e = s + n
+    nt = tiles_for_length(n)
+    for j in range(nt):
+        tile_end = e - ((nt - 1 - j) << 13)
+        a = tile_end & ~15
+        for lane in range(64):
+            win = ragged_line_window(s, e, j, lane)
+            base = a - 128 * (64 - lane)
+            line = range(tile_end - 128 * (64 - lane), tile_end - 128 * (63 - lane))
+            for b, addr in enumerate(win):
+                if addr is not None:
+                    assert addr == base + 16 * b, (s, n, j, lane, b)
+            for x in line:
+                if s <= x < e:
+                    b = (x - base) // 16
+                    assert 0 <= b < 9 and win[b] is not None, (s, n, j, lane, x)
 
 
 def test_ragged_loads_cover_every_message_byte():

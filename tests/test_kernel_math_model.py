@@ -1,6 +1,7 @@
 """CPU model of the kernels' CRC decomposition (the algebra, not the HIP code):
 the ragged kernel's end-aligned virtual lines, zero-masked first line seeded with
-zinv[r], per-tile tree, Z_{8192*T} shift and XOR combine; the uniform kernel's per-line
+zinv[r], per-lane line-shift operators + DPP half reduction, Z_4096 join, Z_{8192*T}
+shift and XOR combine; the uniform kernel's per-line
 CRCs and transposed tree. Each must equal the reference CRC (zlib) bit for bit."""
 import zlib
 
@@ -69,6 +70,8 @@ def inverse(m):
 ZINV1 = inverse(Z1)
 ZTREE = [zbytes(128 << k) for k in range(6)]
 ZTILE = [zbytes(8192 << k) for k in range(8)]
+LANE_OPS = [zbytes(128 * sl) for sl in range(32)]
+Z4096 = zbytes(4096)
 
 
 def ragged_model(buf: bytes, s: int, L: int, init: int) -> int:
@@ -98,11 +101,11 @@ def ragged_model(buf: bytes, s: int, L: int, init: int) -> int:
                     data[i] = 0
             seed = zinv[s - ls] if ls <= s else 0
             lines.append(crc_raw(seed, data))
-        # tree: level k combines pairs 2^k lines apart with Z_{128*2^k}
-        cur = lines
-        for k in range(6):
-            cur = [apply(ZTREE[k], cur[2 * i]) ^ cur[2 * i + 1] for i in range(len(cur) // 2)]
-        t = cur[0]
+        # per lane: Z_{128*(31 - l%32)} on its line; XOR over each half (DPP); the halves
+        # joined with Z_4096; then the shift to the message end, Z_{8192*T}
+        shifted = [apply(LANE_OPS[31 - (lane & 31)], lines[lane]) for lane in range(64)]
+        red = dpp_half_xor(shifted)
+        t = apply(Z4096, red[31]) ^ red[63]
         after = nt - 1 - j
         k = 0
         while after:
