@@ -45,8 +45,11 @@ ROTATE = 4  # 4 x 256 MiB > the 256 MiB Infinity Cache: every step reads HBM
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    # Defaults measure steady state: after an idle spell the first ~300 back-to-back launches
+    # of this kernel run up to 25 % slower while the GPU's power management settles
+    # (profiles/r01/sustained.md); 400 untimed launches take ~20 ms.
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="budget for the CPU baseline legs")

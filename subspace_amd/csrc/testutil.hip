@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "crc_device.h"
+
 namespace {
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -40,9 +42,49 @@ __global__ void synth_fill_kernel(uint8_t* __restrict__ base, const uint64_t* __
   }
 }
 
+// Streaming-read ceiling probe: the CRC kernels' load shape (lane <-> 128-B line, 8 x
+// 16-B loads per lane, 64 consecutive lines per wave instruction, XCD-spread sweep front,
+// one tile prefetched) with the CRC replaced by an XOR fold -- what HBM gives this access
+// pattern.
+using subspace_amd::u32x4;
+__global__ __launch_bounds__(512) void stream_read_kernel(const u32x4* __restrict__ p, uint64_t ntiles,
+                                                          unsigned* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t w = subspace_amd::front_slot(blockIdx.x, gridDim.x, subspace_amd::rfl(threadIdx.x >> 6));
+  const uint64_t nw = (uint64_t)gridDim.x * 8;
+  unsigned acc = 0;
+  uint64_t t = w;
+  u32x4 a[8], b[8];
+  const uint64_t last = ntiles - 1;
+#pragma unroll
+  for (int i = 0; i < 8; i++) a[i] = p[(t < ntiles ? t : last) * 512 + lane * 8 + i];
+  for (; t < ntiles; t += 2 * nw) {
+    const uint64_t t1 = t + nw < ntiles ? t + nw : last;
+#pragma unroll
+    for (int i = 0; i < 8; i++) b[i] = p[t1 * 512 + lane * 8 + i];
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc ^= a[i].x ^ a[i].y ^ a[i].z ^ a[i].w;
+    const uint64_t t2 = t + 2 * nw < ntiles ? t + 2 * nw : last;
+#pragma unroll
+    for (int i = 0; i < 8; i++) a[i] = p[t2 * 512 + lane * 8 + i];
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc ^= b[i].x ^ b[i].y ^ b[i].z ^ b[i].w;
+  }
+  out[blockIdx.x * 512 + threadIdx.x] = acc;
+}
+
 }  // namespace
 
 extern "C" {
+
+// bytes must be a multiple of 8 KiB; out holds 256 * 512 words.
+int subspace_crc_testutil_stream_read(const void* dev_base, uint64_t bytes, unsigned* dev_out, void* stream) {
+  if (!dev_base || !dev_out || bytes < 8192 || (bytes % 8192)) return -1;
+  stream_read_kernel<<<256, 512, 0, (hipStream_t)stream>>>(static_cast<const u32x4*>(dev_base), bytes / 8192,
+                                                           dev_out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 
 int subspace_crc_testutil_fill_uniform(void* dev_base, uint64_t stride, uint64_t length, uint64_t count,
                                        uint64_t first_id, uint64_t id_stride, uint64_t seed, void* stream) {

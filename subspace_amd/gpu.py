@@ -130,3 +130,12 @@ def fill_ragged(buf, offsets, lengths, *, seed: int, first_id: int = 0, id_strid
     _check(_lib.load().subspace_crc_testutil_fill_ragged(
         _ptr(buf), _ptr(offsets), _ptr(lengths), int(offsets.numel()), first_id, id_stride, seed,
         _stream_ptr(stream)), "fill_ragged")
+
+
+def stream_read(buf, out, stream=None) -> None:
+    """Streaming-read ceiling probe over buf (the CRC kernels' load shape, no CRC);
+    out: int32 device tensor of 256 * 512 words."""
+    if int(out.numel()) < 256 * 512:
+        raise ValueError("out needs 131072 words")
+    _check(_lib.load().subspace_crc_testutil_stream_read(
+        _ptr(buf), int(buf.numel() * buf.element_size()), _ptr(out), _stream_ptr(stream)), "stream_read")

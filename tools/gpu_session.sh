@@ -37,7 +37,7 @@ for s in $STEPS; do
       stop_if_fault $? bench ;;
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run \
-        --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 100 --warmup 10 --no-cpu-baseline \
+        --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline \
         --no-e2e > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
       stop_if_fault $? prof ;;
     pmc)
