@@ -22,8 +22,7 @@ __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, con
 
 struct TileDesc;
 __global__ void crc32_ragged_count_kernel(const u64*, u32, u64, u32, u32, u64*, u32*);
-__global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, const u32*, u64, u64, TileDesc*,
-                                         u32*);
+__global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, u64, u64, TileDesc*, u32*);
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
                                     const TileDesc*, const u32*, const u32*, const u32*, const u32*, u32, u32*, u32*);
@@ -60,7 +59,7 @@ int hip_fail(hipError_t e, const char* what) {
   } while (0)
 
 constexpr int kRaggedWG = 512;
-constexpr size_t kTileDescBytes = 32;
+constexpr size_t kTileDescBytes = 16;
 
 }  // namespace
 
@@ -184,7 +183,7 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   size_t tmp = c->scan_tmp_bytes;
   HIP_TRY(ragged_scan(c->d_scan_tmp, tmp, c->d_ntiles, c->d_tbase, n1, st));
   crc32_ragged_desc_kernel<<<(unsigned)((cap + 255) / 256), 256, 0, st>>>(
-      offsets, ostride, lengths, lstride, c->d_tbase, zinv, count, cap, reinterpret_cast<TileDesc*>(c->d_desc),
+      offsets, ostride, lengths, lstride, c->d_tbase, count, cap, reinterpret_cast<TileDesc*>(c->d_desc),
       c->d_overflow);
   HIP_TRY(hipGetLastError());
   const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU

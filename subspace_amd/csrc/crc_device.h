@@ -44,7 +44,8 @@ constexpr int kRagOpZTile = kRagOpZ4096 + 1;
 constexpr int kRagLdsOpWords = kLaneOpWords + (1 + kNumTileOps) * 128;
 constexpr int kRagHighOps = kRagLdsOpWords;  // word offset of Z_{8192 * 2^21} in the device array
 constexpr int kRagOpWords = kRagLdsOpWords + (31 - kNumTileOps) * 128;
-constexpr size_t ragged_lds_bytes() { return kLdsOps + (size_t)kRagLdsOpWords * 4u; }
+constexpr u32 kRagZinv = kLdsOps + (u32)kRagLdsOpWords * 4u;  // then zinv[0..127] of the batch's init
+constexpr size_t ragged_lds_bytes() { return kRagZinv + 128u * 4u; }
 static_assert(ragged_lds_bytes() <= 160u * 1024u, "ragged kernel LDS exceeds 160 KiB");
 
 typedef __attribute__((address_space(3))) u32 lds_u32_t;

@@ -13,8 +13,9 @@
 //    message's first tile is partial). Lane i <-> line i of the tile, exactly like the
 //    uniform kernel: 64 consecutive 128-B lines per wave load instruction.
 //  * Waves stream the global tile list in sweep order (tau = k*nw + w), one tile of
-//    loads in flight ahead. Per-tile descriptors (tile end, message start, message id,
-//    tiles after) are precomputed by crc32_ragged_desc_kernel.
+//    loads in flight ahead. Per-tile 16-B descriptors (tile end, tiles after, first-tile
+//    flag, message start offset in the first tile) are precomputed by
+//    crc32_ragged_desc_kernel.
 //  * Per tile, lane l of half h applies its own line-shift operator Z_{128*(31-l)} (the
 //    uniform kernel's conflict-free [nibble][value][lane] tables) and a DPP reduction
 //    leaves the two half-tile values in lanes 31 and 63. They are parked, one tile per
@@ -39,15 +40,14 @@
 
 namespace subspace_amd {
 
+// 16 B per tile: one vector load and four readfirstlanes per tile in the main kernel.
 struct TileDesc {
-  u64 tile_end;   // absolute offset (from base) one past the tile's last byte
-  u64 msg_start;  // offset of the message's first byte
-  u32 msg;        // message index
-  u32 after;      // tiles after this one in the message
-  u32 seed;       // first tile only: zinv[r], the start state of the line holding msg_start
-  u32 pad;
+  u64 tile_end;  // absolute offset (from base) one past the tile's last byte
+  u32 after;     // tiles after this one in the message | kFirstTile for its first tile
+  u32 lead;      // first tile: message start - tile start (0..8191), else 0
 };
-static_assert(sizeof(TileDesc) == 32, "TileDesc is 32 B");
+static_assert(sizeof(TileDesc) == 16, "TileDesc is 16 B");
+constexpr u32 kFirstTile = 0x80000000u;
 
 __host__ __device__ inline u64 tiles_for_length(u64 len) { return (len + 8191) >> 13; }
 
@@ -82,36 +82,31 @@ __device__ inline u64 find_msg(const u64* __restrict__ tile_base, u64 count, u64
 }
 
 __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, u32 ostride, const u64* __restrict__ lengths,
-                                     u32 lstride, const u64* __restrict__ tile_base, const u32* __restrict__ zinv,
-                                     u64 m, u64 tau) {
+                                     u32 lstride, const u64* __restrict__ tile_base, u64 m, u64 tau) {
   const u64 nt = tile_base[m + 1] - tile_base[m];
   const u64 j = tau - tile_base[m];
   const u64 s = offsets[m * ostride];
   const u64 e = s + lengths[m * lstride];
   TileDesc d;
   d.tile_end = e - ((nt - 1 - j) << 13);
-  d.msg_start = s;
-  d.msg = (u32)m;
-  d.after = (u32)(nt - 1 - j);
-  // the line holding byte s starts r = (s - tile_start) mod 128 bytes before it (lines are
-  // end-aligned, so tile_start == e - 8192*(nt-j) and r only depends on e - s mod 128)
-  const i64 tile_start = (i64)d.tile_end - 8192;
-  const u64 r = (u64)((i64)s - tile_start) & 127u;
-  d.seed = j == 0 ? zinv[r] : 0u;
-  d.pad = 0;
+  d.after = (u32)(nt - 1 - j) | (j == 0 ? kFirstTile : 0u);
+  // first tile: the message starts `lead` bytes into it; the line holding byte s is line
+  // lead >> 7 and starts r = lead & 127 bytes before s (lines are end-aligned), so its lane
+  // starts from zinv[r]
+  d.lead = j == 0 ? (u32)((i64)s - ((i64)d.tile_end - 8192)) : 0u;
   return d;
 }
 
 // Per tile (up to `capacity`): its descriptor. Sets *overflow if the batch has more tiles.
 __global__ void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, u32 ostride,
                                          const u64* __restrict__ lengths, u32 lstride,
-                                         const u64* __restrict__ tile_base, const u32* __restrict__ zinv, u64 count,
-                                         u64 capacity, TileDesc* __restrict__ desc, u32* __restrict__ overflow) {
+                                         const u64* __restrict__ tile_base, u64 count, u64 capacity,
+                                         TileDesc* __restrict__ desc, u32* __restrict__ overflow) {
   const u64 total = tile_base[count];
   const u64 tau = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (tau == 0) *overflow = total > capacity ? 1u : 0u;
   if (tau >= total || tau >= capacity) return;
-  desc[tau] = make_desc(offsets, ostride, lengths, lstride, tile_base, zinv, find_msg(tile_base, count, tau), tau);
+  desc[tau] = make_desc(offsets, ostride, lengths, lstride, tile_base, find_msg(tile_base, count, tau), tau);
 }
 
 // ------------------------------------------------------------------ main kernel
@@ -161,6 +156,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
   const u32 lop = sbase + kLdsOps + 4u * (u32)(31 - (lane & 31));  // this lane's line-shift operator
+  const u32 zsb = sbase + kRagZinv;  // zinv[r], r = 0..127 (first-line seeds of this batch's init)
   const u64 total = tile_base[count];
   const u64 w = front_slot(blockIdx.x, gridDim.x, wid);  // sweep front slot (crc_device.h)
   const u64 nw = (u64)gridDim.x * (WG / 64);
@@ -171,30 +167,27 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   u32 vzero;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
 
-  // Descriptor of tile k as raw dwords (a vector load). Past the wave's last tile it is
-  // clamped to that tile; a wave without tiles uses the batch's last tile, so every load
-  // the kernel issues stays inside a real message.
-  auto fetch_desc = [&](u64 k, u32x4 (&d)[2]) {
+  // Descriptor of tile k as raw dwords (a vector load; DESC false: built by search, with
+  // the message id for the atomic path). Past the wave's last tile it is clamped to that
+  // tile; a wave without tiles uses the batch's last tile, so every load the kernel issues
+  // stays inside a real message.
+  auto fetch_desc = [&](u64 k, u32x4& d, u32& dm) {
     const u64 tau = nk ? (k < nk ? k : nk - 1) * nw + w : total - 1;
     if (DESC) {
-      const u32x4* p = reinterpret_cast<const u32x4*>(desc + tau + vzero);
-      d[0] = p[0];
-      d[1] = p[1];
+      d = *reinterpret_cast<const u32x4*>(desc + tau + vzero);
+      dm = 0;
     } else {
-      const TileDesc t =
-          make_desc(offsets, ostride, lengths, lstride, tile_base, zinv, find_msg(tile_base, count, tau), tau);
-      d[0] = u32x4{(u32)t.tile_end, (u32)(t.tile_end >> 32), (u32)t.msg_start, (u32)(t.msg_start >> 32)};
-      d[1] = u32x4{t.msg, t.after, t.seed, 0u};
+      const u64 m = find_msg(tile_base, count, tau);
+      const TileDesc t = make_desc(offsets, ostride, lengths, lstride, tile_base, m, tau);
+      d = u32x4{(u32)t.tile_end, (u32)(t.tile_end >> 32), t.after, t.lead};
+      dm = (u32)m;
     }
   };
-  auto unpack = [&](const u32x4 (&d)[2]) {
+  auto unpack = [&](const u32x4& d) {
     TileDesc t;
-    t.tile_end = rfl64(d[0][0], d[0][1]);
-    t.msg_start = rfl64(d[0][2], d[0][3]);
-    t.msg = rfl(d[1][0]);
-    t.after = rfl(d[1][1]);
-    t.seed = rfl(d[1][2]);
-    t.pad = 0;
+    t.tile_end = rfl64(d[0], d[1]);
+    t.after = rfl(d[2]);
+    t.lead = rfl(d[3]);
     return t;
   };
   // Issue the loads of tile d, as buffer loads against a scalar resource spanning exactly
@@ -208,9 +201,9 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   // the dummy [a-16, a). `live` false (a prefetch past the wave's last tile) gives an
   // empty range.
   auto load_line = [&](const TileDesc& d, LineState& L, bool live) {
-    const i64 t0a = ((i64)d.tile_end - 8192) & ~(i64)15;
-    const i64 sa = (i64)d.msg_start & ~(i64)15;
-    const i64 rb = t0a > sa ? t0a : sa;
+    const i64 tile_start = (i64)d.tile_end - 8192;
+    const i64 t0a = tile_start & ~(i64)15;
+    const i64 rb = (d.after & kFirstTile) ? ((tile_start + (i64)d.lead) & ~(i64)15) : t0a;
     const i64 a = (i64)d.tile_end & ~(i64)15;
     const i64 rend = ((i64)d.tile_end + 15) & ~(i64)15;
     const u32 nrec = live ? (u32)(rend - rb) : 0u;
@@ -227,52 +220,53 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   };
 
   // Half-tile values parked one tile per lane (slot k & 63), finished every 64 tiles.
-  u32 H0 = 0, H1 = 0, AF = 0, MG = 0;  // half 0, half 1, after | first << 31, message
+  u32 H0 = 0, H1 = 0, AF = 0, MG = 0;  // half 0, half 1, after | kFirstTile, message (DESC false)
 
-  auto process = [&](const LineState& cur, const TileDesc& dcur, u64 k) {
-    const i64 tile_start = (i64)dcur.tile_end - 8192;
-    const i64 line_start = tile_start + (i64)lane * 128;
-    const i64 s = (i64)dcur.msg_start;
-    const bool partial = tile_start < s;  // wave-uniform
-    const bool active = line_start + 128 > s;
+  auto process = [&](const LineState& cur, const TileDesc& dcur, u32 dm, u64 k) {
+    const bool first = (dcur.after & kFirstTile) != 0;  // wave-uniform, like everything below
     const u32 mis = (u32)(dcur.tile_end & 15);
     u32x4 d[9];
 #pragma unroll
     for (int b = 0; b < 8; b++) d[b] = cur.d[b];
-    if (mis) {  // wave-uniform: lane l's 9th block is lane l+1's first, lane 63's the shared one
+    if (mis) {  // lane l's 9th block is lane l+1's first, lane 63's the shared one
 #pragma unroll
       for (int x = 0; x < 4; x++)
         d[8][x] = (u32)__builtin_amdgcn_update_dpp((int)cur.x[x], (int)cur.d[0][x], 0x130, 0xF, 0xF, false);
     } else {
       d[8] = u32x4{0u, 0u, 0u, 0u};
     }
-    if (partial) {
-      // zero every byte of the 144-B window below the message start, seed the first line
-      // with zinv[r]
-      const i64 zb64 = s - (line_start & ~(i64)15);
-      const u32 zb = zb64 <= 0 ? 0u : (zb64 >= 144 ? 144u : (u32)zb64);
+    u32 crc = 0;
+    if (first) {
+      // The message starts `lead` bytes into the tile: zero every byte of each lane's 144-B
+      // window below it (the window starts lead + mis - 128*lane bytes before the message),
+      // and start the lane holding the first byte from zinv[lead & 127]. Lanes wholly
+      // before the message then compute crc_raw(0, zeros) = 0.
+      const u32 lead = dcur.lead;
+      if (lead) {
+        const int zb0 = (int)(lead + mis) - 128 * lane;
+        const u32 zb = zb0 <= 0 ? 0u : (zb0 >= 144 ? 144u : (u32)zb0);
 #pragma unroll
-      for (int b = 0; b < 9; b++) {
+        for (int b = 0; b < 9; b++) {
 #pragma unroll
-        for (int x = 0; x < 4; x++) {
-          const u32 p = 16u * b + 4u * x;
-          u32 keep = 0xFFFFFFFFu;
-          if (p + 4u <= zb) keep = 0;
-          else if (p < zb) keep = 0xFFFFFFFFu << (8u * (zb - p));
-          d[b][x] &= keep;
+          for (int x = 0; x < 4; x++) {
+            const u32 p = 16u * b + 4u * x;
+            u32 keep = 0xFFFFFFFFu;
+            if (p + 4u <= zb) keep = 0;
+            else if (p < zb) keep = 0xFFFFFFFFu << (8u * (zb - p));
+            d[b][x] &= keep;
+          }
         }
       }
+      const u32 seed = lds_ld(zsb + 4u * (lead & 127u));
+      crc = (u32)lane == (lead >> 7) ? seed : 0u;
     }
-    // the line holding the message's first byte starts from zinv[r] (precomputed seed)
-    u32 crc = (active && line_start <= s) ? dcur.seed : 0u;
     const u32 m3 = mis & 3;
-    switch (mis >> 2) {  // wave-uniform
+    switch (mis >> 2) {
       case 0: crc = mis ? crc_line<0, true>(d, crc, m3, lc0, lc1) : crc_line<0, false>(d, crc, m3, lc0, lc1); break;
       case 1: crc = crc_line<1, true>(d, crc, m3, lc0, lc1); break;
       case 2: crc = crc_line<2, true>(d, crc, m3, lc0, lc1); break;
       default: crc = crc_line<3, true>(d, crc, m3, lc0, lc1); break;
     }
-    if (!active) crc = 0;
 
     // line l of half h -> Z_{128*(31-l)}(line): 8 conflict-free nibble lookups; then XOR
     // over each half with DPP (lane 31: lines 0..31, lane 63: lines 32..63)
@@ -284,21 +278,19 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-    const int slot = (int)(k & 63);
-    const bool first = partial || tile_start == s;
     const u32 h0 = (u32)__builtin_amdgcn_readlane((int)v, 31), h1 = (u32)__builtin_amdgcn_readlane((int)v, 63);
-    const bool mine = lane == slot;  // one compare, four selects of wave-uniform values
+    const bool mine = lane == (int)(k & 63);  // one compare, selects of wave-uniform values
     H0 = mine ? h0 : H0;
     H1 = mine ? h1 : H1;
-    AF = mine ? (dcur.after | (first ? 0x80000000u : 0u)) : AF;
-    MG = mine ? dcur.msg : MG;
+    AF = mine ? dcur.after : AF;
+    if (!DESC) MG = mine ? dm : MG;
   };
 
   // Finish and store the parked tiles kf .. kf+nt-1 (lane i holds tile kf + i).
   auto flush = [&](u64 kf, u32 nt) {
     const bool valid = (u32)lane < nt;
     u32 c = opmul(sbase, kRagOpZ4096, H0) ^ H1;  // the tile's 8 KiB from its two halves
-    u32 rem = valid ? (AF & 0x7FFFFFFFu) : 0u;   // shift to the message end: Z_{8192 * after}
+    u32 rem = valid ? (AF & ~kFirstTile) : 0u;   // shift to the message end: Z_{8192 * after}
     int bit = 0;
     for (; bit < kNumTileOps && __any(rem != 0u); bit++) {
       const u32 cm = opmul(sbase, kRagOpZTile + bit, c);
@@ -310,11 +302,11 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
       c = (rem & 1u) ? cm : c;
       rem >>= 1;
     }
-    if (AF >> 31) c ^= final_xor;
+    if (AF & kFirstTile) c ^= final_xor;
     if (valid) {
       if (DESC) {
         tilecrc[(kf + (u64)lane) * nw + w] = c;
-      } else if ((AF >> 31) && (AF & 0x7FFFFFFFu) == 0u) {
+      } else if (AF == kFirstTile) {
         out[MG] = c;  // single-tile message
       } else {
         atomicXor(&out[MG], c);
@@ -326,13 +318,18 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   // stores and the barrier (tile 0's latency hides behind the fill).
   LdsFill<WG, kRagLdsOpWords / 128> fill;
   fill.load(gtab, gops);
-  u32x4 dA[2], dB[2];
-  fetch_desc(0, dA);
-  fetch_desc(1, dB);
+  const u32 zv = zinv[threadIdx.x & 127];  // unconditional (a load in a branch drains vmcnt)
+  u32x4 dA, dB;
+  u32 mA, mB;
+  fetch_desc(0, dA, mA);
+  fetch_desc(1, dB, mB);
   TileDesc dcur = unpack(dA);
+  u32 mcur = mA;
   LineState A, B;
   load_line(dcur, A, nk != 0);
   fill.store(sbase);
+  if (threadIdx.x < 128) lds_st(zsb + 4u * threadIdx.x, zv);
+  asm volatile("" ::"v"(zv));
   __syncthreads();
   if (nk == 0) return;
 
@@ -344,17 +341,20 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   u64 k = 0;
   for (; k + 1 < nk; k += 2) {
     const TileDesc d1 = unpack(dB);   // tile k+1
-    fetch_desc(k + 2, dA);            // tile k+2 (clamped)
+    const u32 m1 = mB;
+    fetch_desc(k + 2, dA, mA);        // tile k+2 (clamped)
     load_line(d1, B, true);
-    process(A, dcur, k);
+    process(A, dcur, mcur, k);
     const TileDesc d2 = unpack(dA);   // tile k+2 (clamped)
-    fetch_desc(k + 3, dB);            // tile k+3 (clamped)
+    const u32 m2 = mA;
+    fetch_desc(k + 3, dB, mB);        // tile k+3 (clamped)
     load_line(d2, A, k + 2 < nk);
-    process(B, d1, k + 1);
+    process(B, d1, m1, k + 1);
     dcur = d2;
+    mcur = m2;
     if (((k + 2) & 63) == 0) flush(k + 2 - 64, 64u);
   }
-  if (k < nk) process(A, dcur, k);
+  if (k < nk) process(A, dcur, mcur, k);
   const u64 kf = nk & ~(u64)63;
   if (nk > kf) flush(kf, (u32)(nk - kf));
 }
