@@ -129,6 +129,30 @@ int subspace_crc32_slots_strided(subspace_crc_ctx* ctx, void* dev_buffer, uint64
                                  int32_t metadata_size, uint32_t mode, uint32_t* dev_status,
                                  uint32_t* dev_error_count, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * Host-memory slots: the end-to-end path. A channel's buffer lives in host shared memory
+ * (the reference maps it with shm_open/memfd, client/client_channel.h:122-172); this call
+ * takes that contiguous layout (slot i's prefix at host_buffer + i*slot_stride, payload
+ * after ComputePrefixSize bytes; host_buffer spans count * slot_stride bytes), streams it to
+ * the device in ~32 MiB chunks (one chunk's H2D copy overlaps the previous chunk's kernels)
+ * and brings back 4 B per slot:
+ *   CALCULATE: on return every prefix has kMessageHasChecksum set and its checksum stored
+ *              (what client/publisher.cc:664-675 leaves in the slot);
+ *   VERIFY:    host_status[i] (optional) and *host_error_count (optional) as for
+ *              subspace_crc32_slots_strided; the host buffer is not modified.
+ * host_message_sizes (optional, host uint64[count]) overrides message_size per slot.
+ * Synchronous: returns when every prefix / status has been written. Pin the buffer once
+ * with subspace_crc_host_register for full PCIe bandwidth (pageable memory works, slower).
+ * --------------------------------------------------------------------------------- */
+int subspace_crc32_host_slots(subspace_crc_ctx* ctx, void* host_buffer, uint64_t slot_stride, uint64_t count,
+                              uint64_t message_size, const uint64_t* host_message_sizes, int32_t checksum_size,
+                              int32_t metadata_size, uint32_t mode, uint32_t* host_status,
+                              uint32_t* host_error_count);
+
+/* Page-lock (pin) / release host memory for DMA (hipHostRegister / hipHostUnregister). */
+int subspace_crc_host_register(void* host_ptr, uint64_t bytes);
+int subspace_crc_host_unregister(void* host_ptr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -28,6 +28,9 @@ EXPORTED_SYMBOLS = (
     "subspace_crc32_batch",
     "subspace_crc32_slots",
     "subspace_crc32_slots_strided",
+    "subspace_crc32_host_slots",
+    "subspace_crc_host_register",
+    "subspace_crc_host_unregister",
 )
 
 _lib = None
@@ -68,6 +71,12 @@ def load() -> ctypes.CDLL:
     lib.subspace_crc32_slots_strided.restype = i32
     lib.subspace_crc32_slots_strided.argtypes = [vp, vp, u64, u64, u64, vp, ctypes.c_int32, ctypes.c_int32, u32,
                                                  vp, vp, vp]
+    lib.subspace_crc32_host_slots.restype = i32
+    lib.subspace_crc32_host_slots.argtypes = [vp, vp, u64, u64, u64, vp, ctypes.c_int32, ctypes.c_int32, u32, vp, vp]
+    lib.subspace_crc_host_register.restype = i32
+    lib.subspace_crc_host_register.argtypes = [vp, u64]
+    lib.subspace_crc_host_unregister.restype = i32
+    lib.subspace_crc_host_unregister.argtypes = [vp]
     lib.subspace_crc_testutil_fill_uniform.restype = i32
     lib.subspace_crc_testutil_fill_uniform.argtypes = [vp, u64, u64, u64, u64, u64, u64, vp]
     lib.subspace_crc_testutil_fill_ragged.restype = i32

@@ -29,7 +29,7 @@ __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*,
 __global__ void crc32_ragged_final_kernel(const u64*, u64, const u32*, const u32*, u32*);
 hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u32* out, u64 n, hipStream_t stream);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, int, int, u32, const u32*,
-                                         const u32*, const u32*, u32*, u32*);
+                                         const u32*, const u32*, u32*, u32*, u32*);
 __global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*);
 hipError_t ragged_scan(void* temp, size_t& temp_bytes, const u64* in, u64* out, u64 n, hipStream_t stream);
 __global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* offsets, u64* lengths);
@@ -93,6 +93,21 @@ struct subspace_crc_ctx {
   u64* d_uoff = nullptr;  // offsets/lengths materialised for non-4K uniform batches
   u64* d_ulen = nullptr;
   u64 u_capacity = 0;
+  // host-slot pipeline (subspace_crc32_host_slots): one compute stream (the kernels share
+  // the context's workspaces), a copy stream and staging per in-flight chunk
+  hipStream_t hcompute = nullptr;
+  struct HostStage {
+    hipStream_t stream = nullptr;  // H2D copies of this stage's chunks
+    hipEvent_t copied = nullptr;   // the chunk is on the device
+    hipEvent_t done = nullptr;     // its results are on the host
+    uint8_t* dbuf = nullptr;   // device copy of a chunk of slots
+    u64* dsizes = nullptr;     // its message sizes (optional)
+    u32* dres = nullptr;       // per-slot results: stored checksum (CALCULATE) / status (VERIFY)
+    u32* derr = nullptr;       // mismatch count of the chunk
+    u32* hres = nullptr;       // pinned host copies of dres / derr
+    u32* herr = nullptr;
+  } hstage[2];
+  u64 h_bytes = 0, h_slots = 0;  // staging capacities
   u32* d_crc0 = nullptr;  // slot batches: payload CRCs from init 0
   u64* d_soff = nullptr;  // slot batches: payload offsets of the contiguous layout
   u64 s_capacity = 0;
@@ -223,10 +238,11 @@ int check_slot_args(int32_t checksum_size, int32_t metadata_size, uint32_t mode)
 }
 
 int slot_finish(subspace_crc_ctx* c, const u64* slots, uint8_t* buf, u64 stride, const u64* sizes, u64 usize,
-                u64 count, int32_t cs, int32_t ms, u32 mode, u32* status, u32* err, hipStream_t st) {
+                u64 count, int32_t cs, int32_t ms, u32 mode, u32* status, u32* err, hipStream_t st,
+                u32* crc_out = nullptr) {
   if (err) HIP_TRY(hipMemsetAsync(err, 0, sizeof(u32), st));
   crc32_slot_finish_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(
-      slots, buf, stride, sizes, usize, count, cs, ms, mode, c->d_crc0, c->d_tab, c->d_pow2, status, err);
+      slots, buf, stride, sizes, usize, count, cs, ms, mode, c->d_crc0, c->d_tab, c->d_pow2, status, err, crc_out);
   HIP_TRY(hipGetLastError());
   return SUBSPACE_CRC_OK;
 }
@@ -306,6 +322,20 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
 
 void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   if (!c) return;
+  if (c->hcompute) (void)hipStreamSynchronize(c->hcompute);
+  for (auto& h : c->hstage) {
+    if (h.stream) (void)hipStreamSynchronize(h.stream);
+    if (h.copied) (void)hipEventDestroy(h.copied);
+    (void)hipFree(h.dbuf);
+    (void)hipFree(h.dsizes);
+    (void)hipFree(h.dres);
+    (void)hipFree(h.derr);
+    (void)hipHostFree(h.hres);
+    (void)hipHostFree(h.herr);
+    if (h.done) (void)hipEventDestroy(h.done);
+    if (h.stream) (void)hipStreamDestroy(h.stream);
+  }
+  if (c->hcompute) (void)hipStreamDestroy(c->hcompute);
   (void)hipFree(c->d_tab);
   (void)hipFree(c->d_rops);
   (void)hipFree(c->d_pow2);
@@ -432,15 +462,18 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
                      dev_error_count, st);
 }
 
-int subspace_crc32_slots_strided(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stride, uint64_t count,
-                                 uint64_t message_size, const uint64_t* dev_message_sizes, int32_t checksum_size,
-                                 int32_t metadata_size, uint32_t mode, uint32_t* dev_status,
-                                 uint32_t* dev_error_count, void* stream) {
-  g_err[0] = 0;
-  if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+}  // extern "C"
+
+namespace {
+
+// Device-buffer strided slots (subspace_crc32_slots_strided), with an optional compact copy
+// of the stored checksums (the host-slot path's write-back source).
+int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stride, uint64_t count,
+                       uint64_t message_size, const uint64_t* dev_message_sizes, int32_t checksum_size,
+                       int32_t metadata_size, uint32_t mode, uint32_t* dev_status, uint32_t* dev_error_count,
+                       u32* dev_crc_out, hipStream_t st) {
   int rc = check_slot_args(checksum_size, metadata_size, mode);
   if (rc) return rc;
-  hipStream_t st = (hipStream_t)stream;
   if (count == 0) {
     if (dev_error_count) HIP_TRY(hipMemsetAsync(dev_error_count, 0, sizeof(u32), st));
     return SUBSPACE_CRC_OK;
@@ -467,11 +500,183 @@ int subspace_crc32_slots_strided(subspace_crc_ctx* c, void* dev_buffer, uint64_t
     rc = ragged_run(c, buf, cap, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st);
   } else {
     rc = subspace_crc32_batch_uniform(c, buf + prefix_size, slot_stride, message_size, count, 0u, 0u, c->d_crc0,
-                                      stream);
+                                      st);
   }
   if (rc) return rc;
   return slot_finish(c, nullptr, buf, slot_stride, dev_message_sizes, message_size, count, checksum_size,
-                     metadata_size, mode, dev_status, dev_error_count, st);
+                     metadata_size, mode, dev_status, dev_error_count, st, dev_crc_out);
+}
+
+}  // namespace
+
+extern "C" {
+
+int subspace_crc32_slots_strided(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stride, uint64_t count,
+                                 uint64_t message_size, const uint64_t* dev_message_sizes, int32_t checksum_size,
+                                 int32_t metadata_size, uint32_t mode, uint32_t* dev_status,
+                                 uint32_t* dev_error_count, void* stream) {
+  g_err[0] = 0;
+  if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  return slots_strided_impl(c, dev_buffer, slot_stride, count, message_size, dev_message_sizes, checksum_size,
+                            metadata_size, mode, dev_status, dev_error_count, nullptr, (hipStream_t)stream);
+}
+
+// ------------------------------------------------------------------ host-memory slots
+int subspace_crc_host_register(void* ptr, uint64_t bytes) {
+  g_err[0] = 0;
+  if (!ptr || !bytes) return fail(SUBSPACE_CRC_EINVAL, "null pointer or zero size");
+  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  return SUBSPACE_CRC_OK;
+}
+
+int subspace_crc_host_unregister(void* ptr) {
+  g_err[0] = 0;
+  if (!ptr) return fail(SUBSPACE_CRC_EINVAL, "null pointer");
+  HIP_TRY(hipHostUnregister(ptr));
+  return SUBSPACE_CRC_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+int ensure_host_stage(subspace_crc_ctx* c, u64 bytes, u64 slots) {
+  if (!c->hcompute) HIP_TRY(hipStreamCreateWithFlags(&c->hcompute, hipStreamNonBlocking));
+  for (auto& h : c->hstage) {
+    if (!h.stream) HIP_TRY(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
+    if (!h.copied) HIP_TRY(hipEventCreateWithFlags(&h.copied, hipEventDisableTiming));
+    if (!h.done) HIP_TRY(hipEventCreateWithFlags(&h.done, hipEventDisableTiming));
+  }
+  if (bytes > c->h_bytes) {
+    for (auto& h : c->hstage) {
+      (void)hipFree(h.dbuf);
+      h.dbuf = nullptr;
+    }
+    c->h_bytes = 0;
+    for (auto& h : c->hstage) HIP_TRY(hipMalloc(&h.dbuf, bytes));
+    c->h_bytes = bytes;
+  }
+  if (slots > c->h_slots) {
+    for (auto& h : c->hstage) {
+      (void)hipFree(h.dsizes);
+      (void)hipFree(h.dres);
+      (void)hipFree(h.derr);
+      (void)hipHostFree(h.hres);
+      (void)hipHostFree(h.herr);
+      h.dsizes = nullptr;
+      h.dres = h.derr = h.hres = h.herr = nullptr;
+    }
+    c->h_slots = 0;
+    for (auto& h : c->hstage) {
+      HIP_TRY(hipMalloc(&h.dsizes, slots * sizeof(u64)));
+      HIP_TRY(hipMalloc(&h.dres, slots * sizeof(u32)));
+      HIP_TRY(hipMalloc(&h.derr, sizeof(u32)));
+      HIP_TRY(hipHostMalloc(&h.hres, slots * sizeof(u32), hipHostMallocDefault));
+      HIP_TRY(hipHostMalloc(&h.herr, sizeof(u32), hipHostMallocDefault));
+    }
+    c->h_slots = slots;
+  }
+  return SUBSPACE_CRC_OK;
+}
+
+// Host side of a finished chunk: CALCULATE writes kMessageHasChecksum and the checksum into
+// each host prefix (what the device computed them with); VERIFY copies the statuses out.
+void host_writeback(const subspace_crc_ctx::HostStage& h, uint8_t* host, u64 stride, u64 first, u64 n, u32 mode,
+                    uint32_t* host_status, u64* errors) {
+  if (mode == SUBSPACE_CRC_SLOT_CALCULATE) {
+    for (u64 i = 0; i < n; i++) {
+      uint8_t* prefix = host + (first + i) * stride;
+      int64_t flags;
+      std::memcpy(&flags, prefix + 32, sizeof(flags));  // MessagePrefix::flags (common/channel.h:88-112)
+      flags |= 4;                                        // kMessageHasChecksum
+      std::memcpy(prefix + 32, &flags, sizeof(flags));
+      std::memcpy(prefix + 48, &h.hres[i], sizeof(u32)); // checksum area, first 4 B
+      if (host_status) host_status[first + i] = SUBSPACE_CRC_SLOT_OK;
+    }
+  } else {
+    if (host_status) std::memcpy(host_status + first, h.hres, n * sizeof(u32));
+    *errors += *h.herr;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int subspace_crc32_host_slots(subspace_crc_ctx* c, void* host_buffer, uint64_t slot_stride, uint64_t count,
+                              uint64_t message_size, const uint64_t* host_message_sizes, int32_t checksum_size,
+                              int32_t metadata_size, uint32_t mode, uint32_t* host_status,
+                              uint32_t* host_error_count) {
+  g_err[0] = 0;
+  if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  int rc = check_slot_args(checksum_size, metadata_size, mode);
+  if (rc) return rc;
+  if (host_error_count) *host_error_count = 0;
+  if (count == 0) return SUBSPACE_CRC_OK;
+  if (!host_buffer) return fail(SUBSPACE_CRC_EINVAL, "null host buffer");
+  if (((uintptr_t)host_buffer % 8) || (slot_stride % 8))
+    return fail(SUBSPACE_CRC_EINVAL, "prefixes must be 8-B aligned (buffer %p, stride %llu)", host_buffer,
+                (unsigned long long)slot_stride);
+  const u64 prefix_size = ((u64)(48 + checksum_size + metadata_size) + 63) & ~63ull;
+  if (!host_message_sizes && slot_stride < prefix_size + message_size)
+    return fail(SUBSPACE_CRC_EINVAL, "slot_stride %llu < prefix %llu + message %llu",
+                (unsigned long long)slot_stride, (unsigned long long)prefix_size, (unsigned long long)message_size);
+  if (host_message_sizes)
+    for (u64 i = 0; i < count; i++)
+      if (prefix_size + host_message_sizes[i] > slot_stride)
+        return fail(SUBSPACE_CRC_EINVAL, "slot %llu: message size %llu does not fit the slot stride %llu",
+                    (unsigned long long)i, (unsigned long long)host_message_sizes[i],
+                    (unsigned long long)slot_stride);
+  HIP_TRY(hipSetDevice(c->device));
+  // ~32 MiB chunks: each H2D copy is long enough to run at the link rate, and two chunks
+  // in flight let one chunk's copy overlap the previous chunk's kernels.
+  const u64 chunk = std::max<u64>(1, std::min<u64>(count, (32ull << 20) / slot_stride));
+  rc = ensure_host_stage(c, chunk * slot_stride, chunk);
+  if (rc) return rc;
+  auto* host = static_cast<uint8_t*>(host_buffer);
+  const u64 nchunks = (count + chunk - 1) / chunk;
+  u64 errors = 0;
+  int first_rc = SUBSPACE_CRC_OK;
+  for (u64 k = 0; k < nchunks + 2; k++) {
+    auto& h = c->hstage[k & 1];
+    if (k >= 2) {  // chunk k-2 used this stage: finish it on the host
+      const u64 f = (k - 2) * chunk, n = std::min(chunk, count - f);
+      hipError_t e = hipEventSynchronize(h.done);
+      if (e != hipSuccess && !first_rc) first_rc = hip_fail(e, "hipEventSynchronize");
+      if (!first_rc) host_writeback(h, host, slot_stride, f, n, mode, host_status, &errors);
+    }
+    if (k >= nchunks || first_rc) continue;
+    const u64 f = k * chunk, n = std::min(chunk, count - f);
+    hipError_t e = hipMemcpyAsync(h.dbuf, host + f * slot_stride, n * slot_stride, hipMemcpyHostToDevice, h.stream);
+    if (e == hipSuccess && host_message_sizes)
+      e = hipMemcpyAsync(h.dsizes, host_message_sizes + f, n * sizeof(u64), hipMemcpyHostToDevice, h.stream);
+    if (e == hipSuccess) e = hipEventRecord(h.copied, h.stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->hcompute, h.copied, 0);
+    if (e != hipSuccess) {
+      first_rc = hip_fail(e, "hipMemcpyAsync (host slots to device)");
+      continue;
+    }
+    const bool calc = mode == SUBSPACE_CRC_SLOT_CALCULATE;
+    rc = slots_strided_impl(c, h.dbuf, slot_stride, n, message_size, host_message_sizes ? h.dsizes : nullptr,
+                            checksum_size, metadata_size, mode, calc ? nullptr : h.dres, calc ? nullptr : h.derr,
+                            calc ? h.dres : nullptr, c->hcompute);
+    if (rc) {
+      first_rc = rc;
+      continue;
+    }
+    e = hipMemcpyAsync(h.hres, h.dres, n * sizeof(u32), hipMemcpyDeviceToHost, c->hcompute);
+    if (e == hipSuccess && !calc)
+      e = hipMemcpyAsync(h.herr, h.derr, sizeof(u32), hipMemcpyDeviceToHost, c->hcompute);
+    if (e == hipSuccess) e = hipEventRecord(h.done, c->hcompute);
+    if (e != hipSuccess) first_rc = hip_fail(e, "hipMemcpyAsync (results to host)");
+  }
+  if (first_rc) {
+    for (auto& h : c->hstage) (void)hipStreamSynchronize(h.stream);
+    (void)hipStreamSynchronize(c->hcompute);
+    return first_rc;
+  }
+  if (host_error_count) *host_error_count = (u32)errors;
+  return SUBSPACE_CRC_OK;
 }
 
 // Tuning hook for experiments (not part of the public header): uniform-kernel workgroup

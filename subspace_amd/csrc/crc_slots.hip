@@ -50,12 +50,13 @@ __device__ u32 shift_zeros(const u32* __restrict__ gpow2, u32 v, u64 n) {
 }
 
 // Slot i: prefix = slots ? slots[3i] : buf + i*stride; payload size = slots ? slots[3i+2]
-// : (sizes ? sizes[i] : usize).
+// : (sizes ? sizes[i] : usize). CALCULATE also writes the stored value to crc_out[i] when
+// crc_out is not null.
 __global__ __launch_bounds__(kSlotWG) void crc32_slot_finish_kernel(
     const u64* __restrict__ slots, uint8_t* __restrict__ buf, u64 stride, const u64* __restrict__ sizes, u64 usize,
     u64 count, int checksum_size, int metadata_size, u32 mode, const u32* __restrict__ crc0,
     const u32* __restrict__ gtab, const u32* __restrict__ gpow2, u32* __restrict__ status,
-    u32* __restrict__ error_count) {
+    u32* __restrict__ error_count, u32* __restrict__ crc_out) {
   __shared__ u32 t[1024];
   for (int i = threadIdx.x; i < 1024; i += kSlotWG) t[i] = gtab[i];
   __syncthreads();
@@ -89,6 +90,7 @@ __global__ __launch_bounds__(kSlotWG) void crc32_slot_finish_kernel(
   if (calc) {
     pw[12] = crc;  // *reinterpret_cast<uint32_t*>(checksum.data()) = ~crc (client/checksum.h:36)
     if (status) status[i] = 0u;
+    if (crc_out) crc_out[i] = crc;  // compact copy for the host-slot path's write-back
   } else {
     const bool ok = pw[12] == crc;  // client/checksum.h:46
     if (status) status[i] = ok ? 0u : 1u;

@@ -118,6 +118,52 @@ class CrcContext:
             _ptr(status) if status is not None else None, _ptr(error_count) if error_count is not None else None,
             _stream_ptr(stream)), "subspace_crc32_slots_strided")
 
+    def crc32_host_slots(self, host, slot_stride: int, count: int, *, message_size: int = 0, sizes=None,
+                         checksum_size: int = 4, metadata_size: int = 0, mode: int = SLOT_CALCULATE,
+                         status=None) -> int:
+        """End-to-end slot checksums over a HOST buffer (numpy uint8 array, or a CPU torch
+        tensor, ideally pinned: see host_register) holding ``count`` contiguous slots.
+        CALCULATE writes the flag and checksum into the host prefixes; VERIFY fills
+        ``status`` (numpy uint32, optional). Returns the mismatch count (VERIFY)."""
+        import numpy as np
+        ptr, nbytes = _host_ptr(host)
+        if nbytes < count * slot_stride:
+            raise ValueError("host buffer is shorter than count * slot_stride")
+        if sizes is not None:
+            sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+            if sizes.size < count:
+                raise ValueError("sizes is shorter than the slot count")
+        if status is not None and (status.dtype != np.uint32 or status.size < count or not status.flags.c_contiguous):
+            raise ValueError("status must be a contiguous uint32 array of at least count entries")
+        err = ctypes.c_uint32(0)
+        _check(self._lib.subspace_crc32_host_slots(
+            self._h, ptr, slot_stride, count, message_size,
+            sizes.ctypes.data if sizes is not None else None, checksum_size, metadata_size, mode,
+            status.ctypes.data if status is not None else None, ctypes.byref(err)), "subspace_crc32_host_slots")
+        return int(err.value)
+
+
+def _host_ptr(host) -> tuple[int, int]:
+    if hasattr(host, "data_ptr"):  # torch CPU tensor
+        if host.is_cuda:
+            raise ValueError("expected a host (CPU) buffer")
+        return int(host.data_ptr()), int(host.numel() * host.element_size())
+    if not host.flags.c_contiguous:
+        raise ValueError("host buffer must be contiguous")
+    return int(host.ctypes.data), int(host.nbytes)
+
+
+def host_register(host) -> None:
+    """Pin a host buffer for DMA (hipHostRegister); release with host_unregister."""
+    ptr, n = _host_ptr(host)
+    _check(_lib.load().subspace_crc_host_register(ptr, n), "subspace_crc_host_register")
+
+
+def host_unregister(host) -> None:
+    ptr, _ = _host_ptr(host)
+    _check(_lib.load().subspace_crc_host_unregister(ptr), "subspace_crc_host_unregister")
+
+
 # ---------------------------------------------------------------- synthetic inputs (device)
 def fill_uniform(buf, stride: int, length: int, count: int, *, seed: int, first_id: int = 0, id_stride: int = 1,
                  stream=None) -> None:

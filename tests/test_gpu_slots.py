@@ -173,3 +173,64 @@ def test_empty_and_errors(gpu_ctx):
         gpu_ctx.crc32_slots_strided(buf, 4160, 1, message_size=4096, checksum_size=2)
     with pytest.raises(gpu.CrcError):
         gpu_ctx.crc32_slots_strided(buf, 4164, 2, message_size=4096)  # prefixes not 8-B aligned
+
+
+# ------------------------------------------------------------ host-memory slots (end to end)
+@pytest.mark.parametrize("count,cs,ms,pinned", [(1, 4, 0, False), (20001, 4, 0, True), (3000, 20, 32, False)])
+def test_host_slots_publish(gpu_ctx, oracle, count, cs, ms, pinned):
+    """subspace_crc32_host_slots CALCULATE over a host channel buffer (several ~32 MiB
+    chunks for 20,001 slots): byte-identical to the oracle's publisher on a copy."""
+    sizes = np.full(count, 4096, dtype=np.uint64)
+    host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=count + cs)
+    want = host.copy()
+    po, yo = offsets(count, stride, ps)
+    oracle.publish_slots(want, po, yo, sizes, cs, ms)
+    if pinned:
+        gpu.host_register(host)
+    try:
+        status = np.full(count, 7, dtype=np.uint32)
+        gpu_ctx.crc32_host_slots(host, stride, count, message_size=4096, checksum_size=cs, metadata_size=ms,
+                                 mode=gpu.SLOT_CALCULATE, status=status)
+    finally:
+        if pinned:
+            gpu.host_unregister(host)
+    assert (status == 0).all()
+    bad = np.nonzero(host != want)[0]
+    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+
+
+def test_host_slots_verify_ragged_sizes(gpu_ctx, oracle):
+    """VERIFY over a host buffer with per-slot sizes and corruptions: statuses and the
+    mismatch count equal the oracle's subscriber; the host buffer is not modified."""
+    count, slot_size, cs, ms = 12000, 5000, 4, 8
+    rng = np.random.default_rng(11)
+    sizes = rng.integers(0, slot_size + 1, count).astype(np.uint64)
+    host, ps, stride = build_channel(count, slot_size, cs, ms, sizes, seed=12)
+    po, yo = offsets(count, stride, ps)
+    oracle.publish_slots(host, po, yo, sizes, cs, ms)
+    for i in rng.choice(count, 300, replace=False):
+        b = int(po[i])
+        if sizes[i]:
+            host[b + ps + rng.integers(0, int(sizes[i]))] ^= 0x20
+        else:
+            host[b + 48] ^= 1
+    host[int(po[5]) + 32] &= 0xFB  # unflagged slot: not checked
+    want = oracle.verify_slots(host, po, yo, sizes, cs, ms)
+    before = host.copy()
+    status = np.full(count, 7, dtype=np.uint32)
+    errors = gpu_ctx.crc32_host_slots(host, stride, count, sizes=sizes, checksum_size=cs, metadata_size=ms,
+                                      mode=gpu.SLOT_VERIFY, status=status)
+    assert np.array_equal(status, want)
+    assert errors == int((want == 1).sum()) and errors > 0
+    assert np.array_equal(host, before)
+
+
+def test_host_slots_errors(gpu_ctx):
+    host = np.zeros(4160 * 2, dtype=np.uint8)
+    assert gpu_ctx.crc32_host_slots(host, 4160, 0, message_size=4096, mode=gpu.SLOT_VERIFY) == 0
+    with pytest.raises(gpu.CrcError):
+        gpu_ctx.crc32_host_slots(host, 4160, 2, message_size=4097)  # does not fit the stride
+    with pytest.raises(gpu.CrcError):
+        gpu_ctx.crc32_host_slots(host, 4160, 2, sizes=np.array([0, 9999], dtype=np.uint64))
+    with pytest.raises(ValueError):
+        gpu_ctx.crc32_host_slots(host, 4160, 3, message_size=4096)  # buffer too short
