@@ -58,7 +58,17 @@ namespace subspace {
 
 extern "C" {
 uint32_t SubspaceCRC32(uint32_t crc, const uint8_t *data, size_t length);
+// CRC-32C, the function a -msse4.2 x86 build of the reference computes in SubspaceCRC32
+// (client/checksum.cc:56-76). A deployment that must interoperate with such peers builds
+// with -DSUBSPACE_CRC_CASTAGNOLI, which routes the templates below to it.
+uint32_t SubspaceCRC32C(uint32_t crc, const uint8_t *data, size_t length);
 }
+
+#if defined(SUBSPACE_CRC_CASTAGNOLI)
+#define SUBSPACE_CRC_FN SubspaceCRC32C
+#else
+#define SUBSPACE_CRC_FN SubspaceCRC32
+#endif
 
 // The callback receives the data to be checksummed and a writable region where
 // the checksum should be stored. The default CRC32 implementation writes 4 bytes;
@@ -71,7 +81,7 @@ void CalculateCRC32Checksum(const std::array<absl::Span<const uint8_t>, N> &data
                             absl::Span<std::byte> checksum) {
   uint32_t crc = 0xFFFFFFFF;
   for (size_t i = 0; i < N; i++) {
-    crc = SubspaceCRC32(crc, data[i].data(), data[i].size());
+    crc = SUBSPACE_CRC_FN(crc, data[i].data(), data[i].size());
   }
   *reinterpret_cast<uint32_t *>(checksum.data()) = ~crc;
 }
@@ -81,7 +91,7 @@ bool VerifyCRC32Checksum(const std::array<absl::Span<const uint8_t>, N> &data,
                          absl::Span<const std::byte> checksum) {
   uint32_t crc = 0xFFFFFFFF;
   for (size_t i = 0; i < N; i++) {
-    crc = SubspaceCRC32(crc, data[i].data(), data[i].size());
+    crc = SUBSPACE_CRC_FN(crc, data[i].data(), data[i].size());
   }
   return *reinterpret_cast<const uint32_t *>(checksum.data()) == ~crc;
 }

@@ -46,14 +46,28 @@ typedef struct subspace_crc_ctx subspace_crc_ctx;
 /* Reference-compatible host CRC (client/checksum.h:18-20). */
 uint32_t SubspaceCRC32(uint32_t crc, const uint8_t* data, size_t length);
 
+/* Same, CRC-32C (Castagnoli): what a -msse4.2 / -march=native x86 build of the reference
+ * computes in SubspaceCRC32 (client/checksum.cc:56-76). Raw state in and out. */
+uint32_t SubspaceCRC32C(uint32_t crc, const uint8_t* data, size_t length);
+
+/* Reflected polynomials for subspace_crc_ctx_create_poly. */
+#define SUBSPACE_CRC_POLY_IEEE 0xEDB88320u       /* the reference's default builds */
+#define SUBSPACE_CRC_POLY_CASTAGNOLI 0x82F63B78u /* CRC-32C, -msse4.2 reference builds */
+
 /* Library version (major*10000 + minor*100 + patch). */
 int subspace_crc_version(void);
 
 /* Last error message of the calling thread ("" if none). */
 const char* subspace_crc_last_error(void);
 
-/* Create a context on HIP device `device` (uploads the CRC tables once). */
+/* Create a context on HIP device `device` (uploads the CRC tables once). Every batch and
+ * slot call on the context computes the IEEE CRC-32 of SubspaceCRC32. */
 int subspace_crc_ctx_create(int device, subspace_crc_ctx** out);
+
+/* The same for another reflected polynomial (bit 31 set, the x^0 term), e.g.
+ * SUBSPACE_CRC_POLY_CASTAGNOLI: every call on the context then computes SubspaceCRC32C's
+ * function. The kernels are table-driven; only the tables and operators differ. */
+int subspace_crc_ctx_create_poly(int device, uint32_t reflected_poly, subspace_crc_ctx** out);
 void subspace_crc_ctx_destroy(subspace_crc_ctx* ctx);
 
 /* Pre-size the ragged-batch workspace for up to `max_messages` messages and

@@ -30,6 +30,14 @@
  *
  * The synthetic-input generator lives here too so the CPU
  * checker regenerates exactly the bytes the GPU bench generates on device.
+ *
+ * CRC-32C (the *_c functions): client/checksum.cc:56-76, the path a -msse4.2 /
+ * -march=native x86 build takes -- _mm_crc32_u64 / _u32 / _u8 fold 8, 4, 1 bytes into a
+ * raw CRC-32C state (reflected Castagnoli polynomial 0x82F63B78, no init / final XOR
+ * inside), which equals the same byte loop over the Castagnoli table. Pinned by the
+ * published CRC-32C check value ("123456789" -> 0xE3069283), the RFC 3720 B.4 vectors
+ * and the reference's own -msse4.2 outputs recorded in SURVEY.md 8c ("hello" ->
+ * 0x9A71BB4C), tests/golden/crc32c_kat.json.
  */
 #include "crc32_oracle.h"
 
@@ -37,16 +45,21 @@
 #include <stdlib.h>
 #include <string.h>
 
-static uint32_t g_table[256];
+static uint32_t g_table[256], g_table_c[256];
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 
 /* Table entry b = CRC of the single byte b from state 0, reflected poly 0xEDB88320
- * (client/checksum.cc:78: "IEEE 802.3 polynomial: 0xEDB88320"). */
+ * (client/checksum.cc:78: "IEEE 802.3 polynomial: 0xEDB88320"); g_table_c the same for
+ * the reflected Castagnoli polynomial 0x82F63B78 (CRC-32C, client/checksum.cc:56-76). */
 static void build_table(void) {
   for (uint32_t b = 0; b < 256; b++) {
-    uint32_t c = b;
-    for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : (c >> 1);
+    uint32_t c = b, d = b;
+    for (int k = 0; k < 8; k++) {
+      c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : (c >> 1);
+      d = (d & 1u) ? (d >> 1) ^ 0x82F63B78u : (d >> 1);
+    }
     g_table[b] = c;
+    g_table_c[b] = d;
   }
 }
 
@@ -55,31 +68,54 @@ const uint32_t* oracle_table(void) {
   return g_table;
 }
 
-/* client/checksum.cc:125-130 */
-uint32_t oracle_crc32(uint32_t crc, const uint8_t* data, size_t length) {
-  const uint32_t* t = oracle_table();
+static const uint32_t* oracle_table_c(void) {
+  pthread_once(&g_once, build_table);
+  return g_table_c;
+}
+
+static uint32_t crc_table(const uint32_t* t, uint32_t crc, const uint8_t* data, size_t length) {
   for (size_t i = 0; i < length; i++) crc = (crc >> 8) ^ t[(crc ^ data[i]) & 0xFFu];
   return crc;
 }
 
+/* client/checksum.cc:125-130 */
+uint32_t oracle_crc32(uint32_t crc, const uint8_t* data, size_t length) {
+  return crc_table(oracle_table(), crc, data, length);
+}
+
+/* client/checksum.cc:56-76 (CRC-32C) */
+uint32_t oracle_crc32c(uint32_t crc, const uint8_t* data, size_t length) {
+  return crc_table(oracle_table_c(), crc, data, length);
+}
+
 /* client/checksum.h:29-37 */
-void oracle_calculate_checksum(const uint8_t* const* spans, const size_t* lengths, size_t nspans,
-                               uint8_t* checksum_out4) {
+static void calculate_checksum_t(const uint32_t* t, const uint8_t* const* spans, const size_t* lengths,
+                                 size_t nspans, uint8_t* checksum_out4) {
   uint32_t crc = 0xFFFFFFFFu;
-  for (size_t i = 0; i < nspans; i++) crc = oracle_crc32(crc, spans[i], lengths[i]);
+  for (size_t i = 0; i < nspans; i++) crc = crc_table(t, crc, spans[i], lengths[i]);
   crc = ~crc;
   memcpy(checksum_out4, &crc, 4);
 }
 
+void oracle_calculate_checksum(const uint8_t* const* spans, const size_t* lengths, size_t nspans,
+                               uint8_t* checksum_out4) {
+  calculate_checksum_t(oracle_table(), spans, lengths, nspans, checksum_out4);
+}
+
 /* client/checksum.h:39-47 */
-int oracle_verify_checksum(const uint8_t* const* spans, const size_t* lengths, size_t nspans,
-                           const uint8_t* checksum4) {
+static int verify_checksum_t(const uint32_t* t, const uint8_t* const* spans, const size_t* lengths, size_t nspans,
+                             const uint8_t* checksum4) {
   uint32_t crc = 0xFFFFFFFFu;
-  for (size_t i = 0; i < nspans; i++) crc = oracle_crc32(crc, spans[i], lengths[i]);
+  for (size_t i = 0; i < nspans; i++) crc = crc_table(t, crc, spans[i], lengths[i]);
   crc = ~crc;
   uint32_t stored;
   memcpy(&stored, checksum4, 4);
   return stored == crc;
+}
+
+int oracle_verify_checksum(const uint8_t* const* spans, const size_t* lengths, size_t nspans,
+                           const uint8_t* checksum4) {
+  return verify_checksum_t(oracle_table(), spans, lengths, nspans, checksum4);
 }
 
 /* common/channel.h:527-542: span [0] = prefix+4 for offsetof(checksum)-offsetof(slot_id)
@@ -99,8 +135,8 @@ void oracle_message_spans(const uint8_t* prefix, const uint8_t* payload, size_t 
 /* Publisher side of one slot (client/publisher.cc:664-675): SetHasChecksum() on the
  * prefix flags (int64 at offset 32, kMessageHasChecksum = 4, common/channel.h:65), then
  * CalculateCRC32Checksum over GetMessageChecksumData's spans into the checksum area. */
-void oracle_publish_slot(uint8_t* prefix, const uint8_t* payload, size_t message_size, int32_t checksum_size,
-                         int32_t metadata_size) {
+static void publish_slot_t(const uint32_t* t, uint8_t* prefix, const uint8_t* payload, size_t message_size,
+                           int32_t checksum_size, int32_t metadata_size) {
   int64_t flags;
   memcpy(&flags, prefix + 32, 8);
   flags |= 4;
@@ -108,36 +144,60 @@ void oracle_publish_slot(uint8_t* prefix, const uint8_t* payload, size_t message
   const uint8_t* spans[3];
   size_t lens[3];
   oracle_message_spans(prefix, payload, message_size, checksum_size, metadata_size, spans, lens);
-  oracle_calculate_checksum(spans, lens, 3, prefix + 48);
+  calculate_checksum_t(t, spans, lens, 3, prefix + 48);
+}
+
+void oracle_publish_slot(uint8_t* prefix, const uint8_t* payload, size_t message_size, int32_t checksum_size,
+                         int32_t metadata_size) {
+  publish_slot_t(oracle_table(), prefix, payload, message_size, checksum_size, metadata_size);
 }
 
 /* Subscriber side (client/client.cc:1346-1356): 2 = no kMessageHasChecksum flag (not
  * checked), else 0 = VerifyCRC32Checksum passed, 1 = "Checksum verification failed". */
-int oracle_verify_slot(const uint8_t* prefix, const uint8_t* payload, size_t message_size, int32_t checksum_size,
-                       int32_t metadata_size) {
+static int verify_slot_t(const uint32_t* t, const uint8_t* prefix, const uint8_t* payload, size_t message_size,
+                         int32_t checksum_size, int32_t metadata_size) {
   int64_t flags;
   memcpy(&flags, prefix + 32, 8);
   if (!(flags & 4)) return 2;
   const uint8_t* spans[3];
   size_t lens[3];
   oracle_message_spans(prefix, payload, message_size, checksum_size, metadata_size, spans, lens);
-  return oracle_verify_checksum(spans, lens, 3, prefix + 48) ? 0 : 1;
+  return verify_checksum_t(t, spans, lens, 3, prefix + 48) ? 0 : 1;
+}
+
+int oracle_verify_slot(const uint8_t* prefix, const uint8_t* payload, size_t message_size, int32_t checksum_size,
+                       int32_t metadata_size) {
+  return verify_slot_t(oracle_table(), prefix, payload, message_size, checksum_size, metadata_size);
 }
 
 /* Slot batches over one host buffer: slot i's prefix at base + prefix_off[i], payload at
  * base + payload_off[i], sizes[i] payload bytes. */
+void oracle_publish_slots_poly(uint8_t* base, const uint64_t* prefix_off, const uint64_t* payload_off,
+                               const uint64_t* sizes, size_t n, int32_t checksum_size, int32_t metadata_size,
+                               int castagnoli) {
+  const uint32_t* t = castagnoli ? oracle_table_c() : oracle_table();
+  for (size_t i = 0; i < n; i++)
+    publish_slot_t(t, base + prefix_off[i], base + payload_off[i], (size_t)sizes[i], checksum_size, metadata_size);
+}
+
+void oracle_verify_slots_poly(const uint8_t* base, const uint64_t* prefix_off, const uint64_t* payload_off,
+                              const uint64_t* sizes, size_t n, int32_t checksum_size, int32_t metadata_size,
+                              uint32_t* status, int castagnoli) {
+  const uint32_t* t = castagnoli ? oracle_table_c() : oracle_table();
+  for (size_t i = 0; i < n; i++)
+    status[i] = (uint32_t)verify_slot_t(t, base + prefix_off[i], base + payload_off[i], (size_t)sizes[i],
+                                        checksum_size, metadata_size);
+}
+
 void oracle_publish_slots(uint8_t* base, const uint64_t* prefix_off, const uint64_t* payload_off,
                           const uint64_t* sizes, size_t n, int32_t checksum_size, int32_t metadata_size) {
-  for (size_t i = 0; i < n; i++)
-    oracle_publish_slot(base + prefix_off[i], base + payload_off[i], (size_t)sizes[i], checksum_size, metadata_size);
+  oracle_publish_slots_poly(base, prefix_off, payload_off, sizes, n, checksum_size, metadata_size, 0);
 }
 
 void oracle_verify_slots(const uint8_t* base, const uint64_t* prefix_off, const uint64_t* payload_off,
                          const uint64_t* sizes, size_t n, int32_t checksum_size, int32_t metadata_size,
                          uint32_t* status) {
-  for (size_t i = 0; i < n; i++)
-    status[i] = (uint32_t)oracle_verify_slot(base + prefix_off[i], base + payload_off[i], (size_t)sizes[i],
-                                             checksum_size, metadata_size);
+  oracle_verify_slots_poly(base, prefix_off, payload_off, sizes, n, checksum_size, metadata_size, status, 0);
 }
 
 /* ------------------------------------------------------------------ batch */
@@ -195,18 +255,23 @@ void oracle_synth_fill(uint64_t seed, uint64_t msg, uint64_t start, uint8_t* dst
   }
 }
 
-uint32_t oracle_synth_crc(uint64_t seed, uint64_t msg, uint64_t length, uint32_t init) {
+static uint32_t synth_crc_t(const uint32_t* t, uint64_t seed, uint64_t msg, uint64_t length, uint32_t init) {
   uint8_t buf[4096];
   uint32_t crc = init;
   for (uint64_t pos = 0; pos < length; pos += sizeof(buf)) {
     const size_t n = (size_t)((length - pos) < sizeof(buf) ? (length - pos) : sizeof(buf));
     oracle_synth_fill(seed, msg, pos, buf, n);
-    crc = oracle_crc32(crc, buf, n);
+    crc = crc_table(t, crc, buf, n);
   }
   return crc;
 }
 
+uint32_t oracle_synth_crc(uint64_t seed, uint64_t msg, uint64_t length, uint32_t init) {
+  return synth_crc_t(oracle_table(), seed, msg, length, init);
+}
+
 typedef struct {
+  const uint32_t* table;
   uint64_t seed;
   const uint64_t* msg_ids;
   const uint64_t* lengths;
@@ -219,17 +284,18 @@ typedef struct {
 static void* synth_worker(void* arg) {
   synth_job* j = (synth_job*)arg;
   for (size_t i = (size_t)j->tid; i < j->n; i += (size_t)j->nthreads)
-    j->out[i] = oracle_synth_crc(j->seed, j->msg_ids ? j->msg_ids[i] : i, j->lengths[i], j->init);
+    j->out[i] = synth_crc_t(j->table, j->seed, j->msg_ids ? j->msg_ids[i] : i, j->lengths[i], j->init);
   return NULL;
 }
 
-void oracle_synth_crc_batch(uint64_t seed, const uint64_t* msg_ids, const uint64_t* lengths, size_t n,
-                            uint32_t init, uint32_t* out, int nthreads) {
+void oracle_synth_crc_batch_poly(uint64_t seed, const uint64_t* msg_ids, const uint64_t* lengths, size_t n,
+                                 uint32_t init, uint32_t* out, int nthreads, int castagnoli) {
+  const uint32_t* table = castagnoli ? oracle_table_c() : oracle_table();
   if (nthreads < 1) nthreads = 1;
   synth_job* jobs = (synth_job*)calloc((size_t)nthreads, sizeof(synth_job));
   pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
   for (int t = 0; t < nthreads; t++) {
-    synth_job s = {seed, msg_ids, lengths, n, init, out, t, nthreads};
+    synth_job s = {table, seed, msg_ids, lengths, n, init, out, t, nthreads};
     jobs[t] = s;
     if (t > 0) pthread_create(&th[t], NULL, synth_worker, &jobs[t]);
   }
@@ -237,6 +303,11 @@ void oracle_synth_crc_batch(uint64_t seed, const uint64_t* msg_ids, const uint64
   for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
   free(jobs);
   free(th);
+}
+
+void oracle_synth_crc_batch(uint64_t seed, const uint64_t* msg_ids, const uint64_t* lengths, size_t n,
+                            uint32_t init, uint32_t* out, int nthreads) {
+  oracle_synth_crc_batch_poly(seed, msg_ids, lengths, n, init, out, nthreads, 0);
 }
 
 /* Config C lengths (integer form so every implementation agrees bit for bit):

@@ -11,6 +11,7 @@ extern "C" {
 
 const uint32_t* oracle_table(void);
 uint32_t oracle_crc32(uint32_t crc, const uint8_t* data, size_t length);
+uint32_t oracle_crc32c(uint32_t crc, const uint8_t* data, size_t length);
 void oracle_calculate_checksum(const uint8_t* const* spans, const size_t* lengths, size_t nspans,
                                uint8_t* checksum_out4);
 int oracle_verify_checksum(const uint8_t* const* spans, const size_t* lengths, size_t nspans,
@@ -36,6 +37,16 @@ uint32_t oracle_synth_crc(uint64_t seed, uint64_t msg, uint64_t length, uint32_t
 void oracle_synth_crc_batch(uint64_t seed, const uint64_t* msg_ids, const uint64_t* lengths, size_t n,
                             uint32_t init, uint32_t* out, int nthreads);
 uint64_t oracle_ragged_length(uint64_t seed, uint64_t i);
+
+/* castagnoli != 0: the same with CRC-32C (client/checksum.cc:56-76) */
+void oracle_synth_crc_batch_poly(uint64_t seed, const uint64_t* msg_ids, const uint64_t* lengths, size_t n,
+                                 uint32_t init, uint32_t* out, int nthreads, int castagnoli);
+void oracle_publish_slots_poly(uint8_t* base, const uint64_t* prefix_off, const uint64_t* payload_off,
+                               const uint64_t* sizes, size_t n, int32_t checksum_size, int32_t metadata_size,
+                               int castagnoli);
+void oracle_verify_slots_poly(const uint8_t* base, const uint64_t* prefix_off, const uint64_t* payload_off,
+                              const uint64_t* sizes, size_t n, int32_t checksum_size, int32_t metadata_size,
+                              uint32_t* status, int castagnoli);
 
 #ifdef __cplusplus
 }

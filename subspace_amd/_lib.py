@@ -19,9 +19,11 @@ if os.environ.get("SUBSPACE_CRC_PROBE_LIB"):  # investigation builds (tools/uben
 # Every symbol include/subspace_crc.h declares (tests check they are all exported).
 EXPORTED_SYMBOLS = (
     "SubspaceCRC32",
+    "SubspaceCRC32C",
     "subspace_crc_version",
     "subspace_crc_last_error",
     "subspace_crc_ctx_create",
+    "subspace_crc_ctx_create_poly",
     "subspace_crc_ctx_destroy",
     "subspace_crc_ctx_reserve",
     "subspace_crc32_batch_uniform",
@@ -52,6 +54,10 @@ def load() -> ctypes.CDLL:
 
     lib.SubspaceCRC32.restype = u32
     lib.SubspaceCRC32.argtypes = [u32, ctypes.c_void_p, ctypes.c_size_t]
+    lib.SubspaceCRC32C.restype = u32
+    lib.SubspaceCRC32C.argtypes = [u32, ctypes.c_void_p, ctypes.c_size_t]
+    lib.subspace_crc_ctx_create_poly.restype = i32
+    lib.subspace_crc_ctx_create_poly.argtypes = [i32, u32, ctypes.POINTER(vp)]
     lib.subspace_crc_version.restype = i32
     lib.subspace_crc_version.argtypes = []
     lib.subspace_crc_last_error.restype = ctypes.c_char_p

@@ -55,6 +55,15 @@ def subspace_crc32(crc: int, data) -> int:
     return int(r)
 
 
+def subspace_crc32c(crc: int, data) -> int:
+    """``SubspaceCRC32C``: CRC-32C with raw state, the function a -msse4.2 build of the
+    reference computes in SubspaceCRC32 (checksum.cc:56-76)."""
+    ptr, n, keep = _buffer(data)
+    r = _lib.load().SubspaceCRC32C(crc & 0xFFFFFFFF, ptr, n)
+    del keep
+    return int(r)
+
+
 def _chain(spans: Sequence) -> int:
     crc = 0xFFFFFFFF
     for s in spans:

@@ -65,6 +65,7 @@ constexpr size_t kTileDescBytes = 16;
 
 struct subspace_crc_ctx {
   int device = 0;
+  uint32_t poly = kPoly;  // reflected CRC polynomial of every table and operator below
   int num_cus = 256;
   u32* d_tab = nullptr;  // 4 x 256 slice tables
   u32* d_rops = nullptr;  // ragged kernel: line-shift operators + Z_4096 + tile shifts (kRagOpWords)
@@ -256,9 +257,15 @@ int subspace_crc_version(void) { return 100; }  // 0.1.0
 const char* subspace_crc_last_error(void) { return g_err; }
 
 int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
+  return subspace_crc_ctx_create_poly(device, SUBSPACE_CRC_POLY_IEEE, out);
+}
+
+int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** out) {
   g_err[0] = 0;
   if (!out) return fail(SUBSPACE_CRC_EINVAL, "out is null");
   *out = nullptr;
+  // reflected form: bit 31 is the x^0 coefficient, which makes every Z_n invertible
+  if (!(poly & 0x80000000u)) return fail(SUBSPACE_CRC_EINVAL, "polynomial 0x%08x has no x^0 term", poly);
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail(SUBSPACE_CRC_ENODEV, "no HIP device available");
@@ -272,7 +279,8 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out) {
   auto* c = new subspace_crc_ctx();
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
-  c->host_tab = make_tables();
+  c->poly = poly;
+  c->host_tab = make_tables(poly);
   c->zinv1 = inverse(z_one(c->host_tab));
 
   std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kLaneOpWords, 0u), rops(kRagOpWords, 0u);

@@ -13,17 +13,19 @@
 
 namespace subspace_amd {
 
-constexpr uint32_t kPoly = 0xEDB88320u;  // reflected IEEE 802.3 (client/checksum.cc:78)
+constexpr uint32_t kPoly = 0xEDB88320u;            // reflected IEEE 802.3 (client/checksum.cc:78)
+constexpr uint32_t kPolyCastagnoli = 0x82F63B78u;  // reflected CRC-32C: what _mm_crc32_* compute
+                                                   // (client/checksum.cc:56-76, -msse4.2 builds)
 
 struct Tables {
   uint32_t t[4][256];  // t[0]: byte table; t[k][b] = CRC of byte b followed by k zero bytes
 };
 
-inline Tables make_tables() {
+inline Tables make_tables(uint32_t poly = kPoly) {
   Tables tb{};
   for (uint32_t b = 0; b < 256; b++) {
     uint32_t c = b;
-    for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ kPoly : (c >> 1);
+    for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ poly : (c >> 1);
     tb.t[0][b] = c;
   }
   for (int k = 1; k < 4; k++)

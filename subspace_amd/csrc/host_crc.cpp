@@ -6,7 +6,7 @@
 // lives in crc_kernels.hip; this host function is what per-message callers
 // (publisher.cc:673, subscriber.h:274, user callbacks such as client_test.cc:5234)
 // keep calling, because a kernel launch per 4 KiB message would cost more than
-// the CRC itself.
+// the CRC itself. SubspaceCRC32C is the same function for the CRC-32C polynomial.
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
@@ -17,8 +17,8 @@ namespace {
 
 struct Slice16 {
   uint32_t t[16][256];  // t[k][b] = CRC of byte b followed by k zero bytes
-  Slice16() {
-    const subspace_amd::Tables tb = subspace_amd::make_tables();
+  explicit Slice16(uint32_t poly) {
+    const subspace_amd::Tables tb = subspace_amd::make_tables(poly);
     for (int b = 0; b < 256; b++) t[0][b] = tb.t[0][b];
     for (int k = 1; k < 16; k++)
       for (int b = 0; b < 256; b++) t[k][b] = (t[k - 1][b] >> 8) ^ t[0][t[k - 1][b] & 0xFF];
@@ -26,7 +26,12 @@ struct Slice16 {
 };
 
 const Slice16& slice16() {
-  static const Slice16 s;  // thread-safe init (C++11 magic statics)
+  static const Slice16 s(subspace_amd::kPoly);  // thread-safe init (C++11 magic statics)
+  return s;
+}
+
+const Slice16& slice16c() {
+  static const Slice16 s(subspace_amd::kPolyCastagnoli);
   return s;
 }
 
@@ -39,10 +44,7 @@ inline uint32_t load_le32(const uint8_t* p) {
   return v;
 }
 
-}  // namespace
-
-extern "C" uint32_t SubspaceCRC32(uint32_t crc, const uint8_t* data, size_t length) {
-  const Slice16& s = slice16();
+uint32_t crc_slice16(const Slice16& s, uint32_t crc, const uint8_t* data, size_t length) {
   const auto& t = s.t;
   while (length >= 16) {
     const uint32_t a = load_le32(data) ^ crc;
@@ -58,4 +60,16 @@ extern "C" uint32_t SubspaceCRC32(uint32_t crc, const uint8_t* data, size_t leng
   }
   while (length--) crc = (crc >> 8) ^ t[0][(crc ^ *data++) & 0xFF];
   return crc;
+}
+
+}  // namespace
+
+extern "C" uint32_t SubspaceCRC32(uint32_t crc, const uint8_t* data, size_t length) {
+  return crc_slice16(slice16(), crc, data, length);
+}
+
+// CRC-32C (Castagnoli), raw state in and out: the value a -msse4.2 / -march=native x86
+// build of the reference computes with _mm_crc32_u64/u32/u8 (client/checksum.cc:56-76).
+extern "C" uint32_t SubspaceCRC32C(uint32_t crc, const uint8_t* data, size_t length) {
+  return crc_slice16(slice16c(), crc, data, length);
 }

@@ -13,6 +13,8 @@ import ctypes
 from . import _lib
 
 FINALIZE = 0x1  # SUBSPACE_CRC_FINALIZE: store ~crc (the checksum CalculateCRC32Checksum writes)
+POLY_IEEE = 0xEDB88320        # the reference's default builds (SubspaceCRC32)
+POLY_CASTAGNOLI = 0x82F63B78  # CRC-32C: -msse4.2 reference builds (SubspaceCRC32C)
 
 # message-slot checksums (include/subspace_crc.h)
 SLOT_CALCULATE = 0  # publisher: set kMessageHasChecksum, store the 3-span checksum in the prefix
@@ -43,11 +45,12 @@ def _stream_ptr(stream) -> int | None:
 class CrcContext:
     """Per-device context (reference analogue: the client library's per-process state)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, poly: int = POLY_IEEE):
         self._lib = _lib.load()
         self.device = device
+        self.poly = poly
         h = ctypes.c_void_p()
-        _check(self._lib.subspace_crc_ctx_create(device, ctypes.byref(h)), "subspace_crc_ctx_create")
+        _check(self._lib.subspace_crc_ctx_create_poly(device, poly, ctypes.byref(h)), "subspace_crc_ctx_create_poly")
         self._h = h
 
     def close(self) -> None:

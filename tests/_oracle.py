@@ -38,21 +38,27 @@ class Oracle:
         lib.oracle_ragged_length.argtypes = [u64, u64]
         lib.oracle_publish_slots.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int32, ctypes.c_int32]
         lib.oracle_verify_slots.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int32, ctypes.c_int32, vp]
+        lib.oracle_crc32c.restype = u32
+        lib.oracle_crc32c.argtypes = [u32, vp, sz]
+        lib.oracle_synth_crc_batch_poly.argtypes = [u64, vp, vp, sz, u32, vp, ctypes.c_int, ctypes.c_int]
+        lib.oracle_publish_slots_poly.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int32, ctypes.c_int32, ctypes.c_int]
+        lib.oracle_verify_slots_poly.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int32, ctypes.c_int32, vp,
+                                                 ctypes.c_int]
 
     def publish_slots(self, host: np.ndarray, prefix_off, payload_off, sizes, checksum_size: int,
-                      metadata_size: int) -> None:
+                      metadata_size: int, castagnoli: bool = False) -> None:
         """Publisher checksum (flag + 3-span CRC into the prefix) for every slot, in place."""
         assert host.dtype == np.uint8 and host.flags.c_contiguous
         po, yo, sz = (np.ascontiguousarray(a, dtype=np.uint64) for a in (prefix_off, payload_off, sizes))
-        self.lib.oracle_publish_slots(host.ctypes.data, po.ctypes.data, yo.ctypes.data, sz.ctypes.data, len(po),
-                                      checksum_size, metadata_size)
+        self.lib.oracle_publish_slots_poly(host.ctypes.data, po.ctypes.data, yo.ctypes.data, sz.ctypes.data,
+                                           len(po), checksum_size, metadata_size, int(castagnoli))
 
     def verify_slots(self, host: np.ndarray, prefix_off, payload_off, sizes, checksum_size: int,
-                     metadata_size: int) -> np.ndarray:
+                     metadata_size: int, castagnoli: bool = False) -> np.ndarray:
         po, yo, sz = (np.ascontiguousarray(a, dtype=np.uint64) for a in (prefix_off, payload_off, sizes))
         st = np.zeros(len(po), dtype=np.uint32)
-        self.lib.oracle_verify_slots(host.ctypes.data, po.ctypes.data, yo.ctypes.data, sz.ctypes.data, len(po),
-                                     checksum_size, metadata_size, st.ctypes.data)
+        self.lib.oracle_verify_slots_poly(host.ctypes.data, po.ctypes.data, yo.ctypes.data, sz.ctypes.data,
+                                          len(po), checksum_size, metadata_size, st.ctypes.data, int(castagnoli))
         return st
 
     def table(self) -> list[int]:
@@ -62,6 +68,10 @@ class Oracle:
     def crc32(self, crc: int, data: bytes) -> int:
         buf = ctypes.create_string_buffer(bytes(data), len(data))
         return int(self.lib.oracle_crc32(crc & 0xFFFFFFFF, buf, len(data)))
+
+    def crc32c(self, crc: int, data: bytes) -> int:
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        return int(self.lib.oracle_crc32c(crc & 0xFFFFFFFF, buf, len(data)))
 
     def checksum(self, spans) -> bytes:
         crc = 0xFFFFFFFF
@@ -77,7 +87,8 @@ class Oracle:
     def synth_crc(self, seed: int, msg: int, length: int, init: int = 0xFFFFFFFF) -> int:
         return int(self.lib.oracle_synth_crc(seed, msg, length, init & 0xFFFFFFFF))
 
-    def synth_crc_batch(self, seed: int, lengths, msg_ids=None, init: int = 0xFFFFFFFF, threads: int = 8) -> np.ndarray:
+    def synth_crc_batch(self, seed: int, lengths, msg_ids=None, init: int = 0xFFFFFFFF, threads: int = 8,
+                        castagnoli: bool = False) -> np.ndarray:
         lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
         n = len(lengths)
         out = np.zeros(n, dtype=np.uint32)
@@ -85,8 +96,8 @@ class Oracle:
         if msg_ids is not None:
             msg_ids = np.ascontiguousarray(msg_ids, dtype=np.uint64)
             ids_p = msg_ids.ctypes.data
-        self.lib.oracle_synth_crc_batch(seed, ids_p, lengths.ctypes.data, n, init & 0xFFFFFFFF, out.ctypes.data,
-                                        threads)
+        self.lib.oracle_synth_crc_batch_poly(seed, ids_p, lengths.ctypes.data, n, init & 0xFFFFFFFF,
+                                             out.ctypes.data, threads, int(castagnoli))
         return out
 
     def crc32_batch(self, base: np.ndarray, offsets, lengths, init: int = 0xFFFFFFFF, threads: int = 1) -> np.ndarray:

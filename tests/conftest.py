@@ -39,3 +39,15 @@ def gpu_ctx():
     ctx = CrcContext(0)
     yield ctx
     ctx.close()
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_c():
+    """A context on the CRC-32C (Castagnoli) polynomial."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from subspace_amd.gpu import POLY_CASTAGNOLI, CrcContext
+    ctx = CrcContext(0, poly=POLY_CASTAGNOLI)
+    yield ctx
+    ctx.close()

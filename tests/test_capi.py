@@ -12,7 +12,7 @@ ROOT = Path(__file__).resolve().parent.parent
 def declared_symbols():
     hdr = (ROOT / "include" / "subspace_crc.h").read_text()
     hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
-    return sorted(set(re.findall(r"\b(SubspaceCRC32|subspace_crc\w+)\s*\(", hdr)))
+    return sorted(set(re.findall(r"\b(SubspaceCRC32C?|subspace_crc\w+)\s*\(", hdr)))
 
 
 def test_header_symbols_are_exported(lib):

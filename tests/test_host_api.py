@@ -146,3 +146,34 @@ def test_header_drop_in_compiles_and_links(lib, tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip() == "ok"
+
+
+CPP_CASTAGNOLI = r"""
+#include <cstdio>
+#include <cstring>
+#include "subspace/checksum.h"
+int main() {
+  const uint8_t msg[] = {'1', '2', '3', '4', '5', '6', '7', '8', '9'};
+  std::array<absl::Span<const uint8_t>, 1> d = {absl::Span<const uint8_t>(msg, 9)};
+  std::byte c[4];
+  subspace::CalculateCRC32Checksum<1>(d, absl::Span<std::byte>(c, 4));
+  uint32_t v;
+  std::memcpy(&v, c, 4);
+  std::printf("%08x\n", v);
+  return 0;
+}
+"""
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_header_castagnoli_build(lib, tmp_path):
+    """-DSUBSPACE_CRC_CASTAGNOLI routes the header templates to SubspaceCRC32C, the function
+    a -msse4.2 reference build computes: the CRC-32C check value comes out."""
+    src = tmp_path / "c.cc"
+    src.write_text(CPP_CASTAGNOLI)
+    exe = tmp_path / "c"
+    libdir = ROOT / "subspace_amd"
+    subprocess.run(["g++", "-std=c++17", "-DSUBSPACE_CRC_CASTAGNOLI", f"-I{ROOT / 'include'}", str(src), "-o",
+                    str(exe), f"-L{libdir}", "-lsubspace_crc", f"-Wl,-rpath,{libdir}"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == "e3069283", r.stdout + r.stderr
