@@ -163,7 +163,21 @@ int subspace_crc32_host_slots(subspace_crc_ctx* ctx, void* host_buffer, uint64_t
                               int32_t metadata_size, uint32_t mode, uint32_t* host_status,
                               uint32_t* host_error_count);
 
-/* Page-lock (pin) / release host memory for DMA (hipHostRegister / hipHostUnregister). */
+/* Zero-copy slot list in host memory -- the subscriber drain hook: the slots a
+ * GetAllMessages / ProcessAllMessages drain (client/client.cc:344-397) would read, in any
+ * order and from any channels, as subspace_crc_slot records holding HOST addresses (the
+ * records themselves are a host array). Every prefix and payload must lie in a region
+ * registered with subspace_crc_host_register; the kernels read them in place over PCIe
+ * through the region's device mapping (no staging copy of the payloads). CALCULATE writes
+ * flag + checksum into the host prefixes; VERIFY fills host_status / *host_error_count
+ * (SUBSPACE_CRC_SLOT_MISMATCH = "Checksum verification failed", client/client.cc:1447).
+ * Synchronous. */
+int subspace_crc32_host_slot_list(subspace_crc_ctx* ctx, const subspace_crc_slot* host_slots, uint64_t count,
+                                  uint64_t max_message_size, int32_t checksum_size, int32_t metadata_size,
+                                  uint32_t mode, uint32_t* host_status, uint32_t* host_error_count);
+
+/* Page-lock (pin) host memory for DMA and map it for device access (hipHostRegister,
+ * mapped + portable); release with subspace_crc_host_unregister (same pointer). */
 int subspace_crc_host_register(void* host_ptr, uint64_t bytes);
 int subspace_crc_host_unregister(void* host_ptr);
 

@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "subspace_crc32_slots",
     "subspace_crc32_slots_strided",
     "subspace_crc32_host_slots",
+    "subspace_crc32_host_slot_list",
     "subspace_crc_host_register",
     "subspace_crc_host_unregister",
 )
@@ -79,6 +80,8 @@ def load() -> ctypes.CDLL:
                                                  vp, vp, vp]
     lib.subspace_crc32_host_slots.restype = i32
     lib.subspace_crc32_host_slots.argtypes = [vp, vp, u64, u64, u64, vp, ctypes.c_int32, ctypes.c_int32, u32, vp, vp]
+    lib.subspace_crc32_host_slot_list.restype = i32
+    lib.subspace_crc32_host_slot_list.argtypes = [vp, vp, u64, u64, ctypes.c_int32, ctypes.c_int32, u32, vp, vp]
     lib.subspace_crc_host_register.restype = i32
     lib.subspace_crc_host_register.argtypes = [vp, u64]
     lib.subspace_crc_host_unregister.restype = i32

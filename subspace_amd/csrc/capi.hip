@@ -59,6 +59,23 @@ int hip_fail(hipError_t e, const char* what) {
   } while (0)
 
 constexpr int kRaggedWG = 512;
+
+// Host regions registered with subspace_crc_host_register: host range -> device alias
+// (hipHostRegisterMapped), for the zero-copy host slot-list path.
+struct HostRegion {
+  uintptr_t host;
+  uint64_t bytes;
+  uintptr_t dev;
+};
+std::mutex g_regions_mu;
+std::vector<HostRegion> g_regions;
+
+// Device alias of host range [p, p+n), or 0 if no registered region holds all of it.
+uintptr_t host_alias(uintptr_t p, uint64_t n) {
+  for (const auto& r : g_regions)
+    if (p >= r.host && p - r.host <= r.bytes && n <= r.bytes - (p - r.host)) return r.dev + (p - r.host);
+  return 0;
+}
 constexpr size_t kTileDescBytes = 16;
 
 }  // namespace
@@ -109,6 +126,12 @@ struct subspace_crc_ctx {
     u32* herr = nullptr;
   } hstage[2];
   u64 h_bytes = 0, h_slots = 0;  // staging capacities
+  // host slot lists (subspace_crc32_host_slot_list): translated records and statuses
+  subspace_crc_slot* l_hrec = nullptr;
+  subspace_crc_slot* l_drec = nullptr;
+  u32* l_dstatus = nullptr;  // count statuses + the mismatch count
+  u32* l_hstatus = nullptr;
+  u64 l_capacity = 0;
   u32* d_crc0 = nullptr;  // slot batches: payload CRCs from init 0
   u64* d_soff = nullptr;  // slot batches: payload offsets of the contiguous layout
   u64 s_capacity = 0;
@@ -344,6 +367,10 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
     if (h.stream) (void)hipStreamDestroy(h.stream);
   }
   if (c->hcompute) (void)hipStreamDestroy(c->hcompute);
+  (void)hipHostFree(c->l_hrec);
+  (void)hipFree(c->l_drec);
+  (void)hipFree(c->l_dstatus);
+  (void)hipHostFree(c->l_hstatus);
   (void)hipFree(c->d_tab);
   (void)hipFree(c->d_rops);
   (void)hipFree(c->d_pow2);
@@ -533,13 +560,29 @@ int subspace_crc32_slots_strided(subspace_crc_ctx* c, void* dev_buffer, uint64_t
 int subspace_crc_host_register(void* ptr, uint64_t bytes) {
   g_err[0] = 0;
   if (!ptr || !bytes) return fail(SUBSPACE_CRC_EINVAL, "null pointer or zero size");
-  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+  void* dev = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&dev, ptr, 0);
+  if (e != hipSuccess) {
+    (void)hipHostUnregister(ptr);
+    return hip_fail(e, "hipHostGetDevicePointer");
+  }
+  std::lock_guard<std::mutex> lock(g_regions_mu);
+  g_regions.push_back({reinterpret_cast<uintptr_t>(ptr), bytes, reinterpret_cast<uintptr_t>(dev)});
   return SUBSPACE_CRC_OK;
 }
 
 int subspace_crc_host_unregister(void* ptr) {
   g_err[0] = 0;
   if (!ptr) return fail(SUBSPACE_CRC_EINVAL, "null pointer");
+  {
+    std::lock_guard<std::mutex> lock(g_regions_mu);
+    for (size_t i = 0; i < g_regions.size(); i++)
+      if (g_regions[i].host == reinterpret_cast<uintptr_t>(ptr)) {
+        g_regions.erase(g_regions.begin() + (long)i);
+        break;
+      }
+  }
   HIP_TRY(hipHostUnregister(ptr));
   return SUBSPACE_CRC_OK;
 }
@@ -684,6 +727,70 @@ int subspace_crc32_host_slots(subspace_crc_ctx* c, void* host_buffer, uint64_t s
     return first_rc;
   }
   if (host_error_count) *host_error_count = (u32)errors;
+  return SUBSPACE_CRC_OK;
+}
+
+// Zero-copy slot list in host memory (a subscriber drain): translate each record's host
+// addresses to their device aliases, then the device slot path reads payloads and prefixes
+// straight from host memory over PCIe; CALCULATE writes flag + checksum into the host
+// prefixes through the same mapping.
+int subspace_crc32_host_slot_list(subspace_crc_ctx* c, const subspace_crc_slot* host_slots, uint64_t count,
+                                  uint64_t max_message_size, int32_t checksum_size, int32_t metadata_size,
+                                  uint32_t mode, uint32_t* host_status, uint32_t* host_error_count) {
+  g_err[0] = 0;
+  if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  int rc = check_slot_args(checksum_size, metadata_size, mode);
+  if (rc) return rc;
+  if (host_error_count) *host_error_count = 0;
+  if (count == 0) return SUBSPACE_CRC_OK;
+  if (!host_slots) return fail(SUBSPACE_CRC_EINVAL, "null slot list");
+  if (count >= (1ull << 32)) return fail(SUBSPACE_CRC_EINVAL, "count %llu exceeds 2^32-1", (unsigned long long)count);
+  HIP_TRY(hipSetDevice(c->device));
+  rc = ensure_host_stage(c, 0, 0);  // the compute stream
+  if (rc) return rc;
+  if (count > c->l_capacity) {
+    (void)hipHostFree(c->l_hrec);
+    (void)hipFree(c->l_drec);
+    (void)hipFree(c->l_dstatus);
+    (void)hipHostFree(c->l_hstatus);
+    c->l_hrec = nullptr;
+    c->l_drec = nullptr;
+    c->l_dstatus = c->l_hstatus = nullptr;
+    c->l_capacity = 0;
+    HIP_TRY(hipHostMalloc(&c->l_hrec, count * sizeof(subspace_crc_slot), hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&c->l_drec, count * sizeof(subspace_crc_slot)));
+    HIP_TRY(hipMalloc(&c->l_dstatus, (count + 1) * sizeof(u32)));
+    HIP_TRY(hipHostMalloc(&c->l_hstatus, (count + 1) * sizeof(u32), hipHostMallocDefault));
+    c->l_capacity = count;
+  }
+  const u64 prefix_size = ((u64)(48 + checksum_size + metadata_size) + 63) & ~63ull;
+  {
+    std::lock_guard<std::mutex> lock(g_regions_mu);
+    for (u64 i = 0; i < count; i++) {
+      const subspace_crc_slot& h = host_slots[i];
+      const uintptr_t pre = host_alias((uintptr_t)h.prefix, prefix_size);
+      const uintptr_t pay = h.message_size ? host_alias((uintptr_t)h.payload, h.message_size) : pre;
+      if (!pre || !pay)
+        return fail(SUBSPACE_CRC_EINVAL, "slot %llu: prefix or payload outside every registered host region",
+                    (unsigned long long)i);
+      if (pre % 8) return fail(SUBSPACE_CRC_EINVAL, "slot %llu: prefix not 8-B aligned", (unsigned long long)i);
+      c->l_hrec[i] = subspace_crc_slot{(uint64_t)pre, (uint64_t)pay, h.message_size};
+    }
+  }
+  hipStream_t st = c->hcompute;
+  u32* dstatus = c->l_dstatus;
+  u32* derr = c->l_dstatus + count;
+  HIP_TRY(hipMemcpyAsync(c->l_drec, c->l_hrec, count * sizeof(subspace_crc_slot), hipMemcpyHostToDevice, st));
+  rc = subspace_crc32_slots(c, c->l_drec, count, max_message_size, checksum_size, metadata_size, mode, dstatus, derr,
+                            st);
+  if (rc) {
+    (void)hipStreamSynchronize(st);
+    return rc;
+  }
+  HIP_TRY(hipMemcpyAsync(c->l_hstatus, dstatus, (count + 1) * sizeof(u32), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (host_status) std::memcpy(host_status, c->l_hstatus, count * sizeof(u32));
+  if (host_error_count) *host_error_count = c->l_hstatus[count];
   return SUBSPACE_CRC_OK;
 }
 

@@ -146,6 +146,26 @@ class CrcContext:
         return int(err.value)
 
 
+    def crc32_host_slot_list(self, records, *, max_message_size: int, checksum_size: int = 4,
+                             metadata_size: int = 0, mode: int = SLOT_CALCULATE, status=None) -> int:
+        """Zero-copy slot list in registered host memory (the subscriber drain hook):
+        ``records`` is an (n, 3) uint64 array (slots.slot_records) of HOST addresses
+        (prefix, payload, message_size). Returns the mismatch count (VERIFY); fills
+        ``status`` if given."""
+        import numpy as np
+        records = np.ascontiguousarray(records, dtype=np.uint64)
+        if records.ndim != 2 or records.shape[1] != 3:
+            raise ValueError("records must be an (n, 3) array of subspace_crc_slot fields")
+        n = len(records)
+        if status is not None and (status.dtype != np.uint32 or status.size < n or not status.flags.c_contiguous):
+            raise ValueError("status must be a contiguous uint32 array of at least len(records) entries")
+        err = ctypes.c_uint32(0)
+        _check(self._lib.subspace_crc32_host_slot_list(
+            self._h, records.ctypes.data, n, max_message_size, checksum_size, metadata_size, mode,
+            status.ctypes.data if status is not None else None, ctypes.byref(err)), "subspace_crc32_host_slot_list")
+        return int(err.value)
+
+
 def _host_ptr(host) -> tuple[int, int]:
     if hasattr(host, "data_ptr"):  # torch CPU tensor
         if host.is_cuda:

@@ -234,3 +234,55 @@ def test_host_slots_errors(gpu_ctx):
         gpu_ctx.crc32_host_slots(host, 4160, 2, sizes=np.array([0, 9999], dtype=np.uint64))
     with pytest.raises(ValueError):
         gpu_ctx.crc32_host_slots(host, 4160, 3, message_size=4096)  # buffer too short
+
+
+def test_host_slot_list_drain(gpu_ctx, oracle):
+    """subspace_crc32_host_slot_list (the subscriber drain hook): a shuffled subset of the
+    slots of two registered host channel buffers, verified in place over PCIe; statuses and
+    the mismatch count equal the oracle's; then CALCULATE on a subset writes the same
+    prefixes as the oracle's publisher."""
+    count, slot_size, cs, ms = 4000, 3000, 4, 8
+    rng = np.random.default_rng(21)
+    chans = []
+    for k in range(2):
+        sizes = rng.integers(0, slot_size + 1, count).astype(np.uint64)
+        host, ps, stride = build_channel(count, slot_size, cs, ms, sizes, seed=30 + k)
+        po, yo = offsets(count, stride, ps)
+        oracle.publish_slots(host, po, yo, sizes, cs, ms)
+        for i in rng.choice(count, 50, replace=False):
+            host[int(po[i]) + 48] ^= 0x40  # corrupt stored checksums
+        chans.append((host, po, yo, sizes))
+    for host, *_ in chans:
+        gpu.host_register(host)
+    try:
+        picks = [(k, int(i)) for k in range(2) for i in rng.choice(count, 1500, replace=False)]
+        rng.shuffle(picks)
+        rec = slots.slot_records([chans[k][0].ctypes.data + int(chans[k][1][i]) for k, i in picks],
+                                 [chans[k][0].ctypes.data + int(chans[k][2][i]) for k, i in picks],
+                                 [chans[k][3][i] for k, i in picks])
+        status = np.full(len(picks), 7, dtype=np.uint32)
+        errors = gpu_ctx.crc32_host_slot_list(rec, max_message_size=slot_size, checksum_size=cs,
+                                              metadata_size=ms, mode=gpu.SLOT_VERIFY, status=status)
+        want = np.concatenate([oracle.verify_slots(chans[k][0], chans[k][1][[i]], chans[k][2][[i]],
+                                                   chans[k][3][[i]], cs, ms) for k, i in picks])
+        assert np.array_equal(status, want)
+        assert errors == int((want == 1).sum()) and errors > 0
+        # publish (CALCULATE) through the mapping: same bytes as the oracle's publisher
+        expect = [c[0].copy() for c in chans]
+        sub = picks[:700]
+        for k, i in sub:
+            oracle.publish_slots(expect[k], chans[k][1][[i]], chans[k][2][[i]], chans[k][3][[i]], cs, ms)
+        gpu_ctx.crc32_host_slot_list(rec[:700], max_message_size=slot_size, checksum_size=cs, metadata_size=ms,
+                                     mode=gpu.SLOT_CALCULATE)
+        for k in range(2):
+            assert np.array_equal(chans[k][0], expect[k]), k
+    finally:
+        for host, *_ in chans:
+            gpu.host_unregister(host)
+
+
+def test_host_slot_list_unregistered_rejected(gpu_ctx):
+    host = np.zeros(8192, dtype=np.uint8)
+    rec = slots.slot_records([host.ctypes.data], [host.ctypes.data + 64], [100])
+    with pytest.raises(gpu.CrcError):
+        gpu_ctx.crc32_host_slot_list(rec, max_message_size=4096, mode=gpu.SLOT_VERIFY)
