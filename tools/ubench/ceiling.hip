@@ -1,0 +1,110 @@
+// Read ceilings at config B's launch size (investigation tool): 256 MiB per launch,
+// 4 rotated windows (1 GiB), 300 back-to-back launches per variant after a 40 ms warm-up
+// of the same variant, variants interleaved twice. Compared with the production CRC kernel
+// (through the C ABI) under the same schedule.
+//   hipcc --offload-arch=gfx950 -O3 -o ceiling ceiling.hip -I../../include -L../../subspace_amd -lsubspace_crc
+#include <hip/hip_runtime.h>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstdint>
+#include <functional>
+#include <vector>
+
+#include "subspace_crc.h"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
+typedef unsigned int u32;
+typedef unsigned long long u64;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+
+__device__ __forceinline__ u64 front(u32 b, u32 G, u32 wid) { return ((u64)b + (u64)G * (wid >> 1)) * 2 + (wid & 1u); }
+
+// SHAPE 0: lane <-> 128-B line (lane reads 8 consecutive 16-B blocks);
+// SHAPE 1: coalesced (instruction i reads 1 KiB: lane l gets block 64*i + l).
+// PF: explicit ping-pong prefetch of the next tile (as the CRC kernel does).
+template <int SHAPE, bool PF>
+__global__ __launch_bounds__(512) void readk(const u32x4* __restrict__ p, u64 ntiles, u32* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u64 w = front(blockIdx.x, gridDim.x, wid), nw = (u64)gridDim.x * 8;
+  const u32 nk = w < ntiles ? (u32)((ntiles - w + nw - 1) / nw) : 0u;
+  auto addr = [&](u32 k, int i) -> const u32x4* {
+    const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
+    const u64 t = nk ? w + (u64)kk * nw : 0;
+    return SHAPE == 0 ? p + t * 512 + lane * 8 + i : p + t * 512 + i * 64 + lane;
+  };
+  u32 acc = 0;
+  if (!PF) {
+    for (u32 k = 0; k < nk; k++) {
+      u32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) v[i] = *addr(k, i);
+#pragma unroll
+      for (int i = 0; i < 8; i++) acc ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+    }
+  } else {
+    u32x4 a[8], b[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) a[i] = *addr(0, i);
+    u32 k = 0;
+    for (; k + 1 < nk; k += 2) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) b[i] = *addr(k + 1, i);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; i++) acc ^= a[i].x ^ a[i].y ^ a[i].z ^ a[i].w;
+#pragma unroll
+      for (int i = 0; i < 8; i++) a[i] = *addr(k + 2, i);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; i++) acc ^= b[i].x ^ b[i].y ^ b[i].z ^ b[i].w;
+    }
+    if (k < nk)
+#pragma unroll
+      for (int i = 0; i < 8; i++) acc ^= a[i].x ^ a[i].y ^ a[i].z ^ a[i].w;
+  }
+  out[blockIdx.x * 512 + threadIdx.x] = acc;
+}
+
+int main() {
+  const u64 win = 256ull << 20, nwin = 4, ntiles = win / 8192;
+  u32x4* buf; CK(hipMalloc(&buf, win * nwin));
+  u32* out; CK(hipMalloc(&out, 256 * 512 * 4));
+  u32* crc; CK(hipMalloc(&crc, 65536 * 4));
+  CK(hipMemset(buf, 0x5A, win * nwin));
+  subspace_crc_ctx* ctx;
+  if (subspace_crc_ctx_create(0, &ctx)) { fprintf(stderr, "ctx: %s\n", subspace_crc_last_error()); return 1; }
+  CK(hipDeviceSynchronize());
+  struct V { const char* name; std::function<void(const u32x4*)> f; };
+  std::vector<V> vs = {
+      {"lines", [&](const u32x4* p) { readk<0, false><<<256, 512>>>(p, ntiles, out); }},
+      {"lines+pf", [&](const u32x4* p) { readk<0, true><<<256, 512>>>(p, ntiles, out); }},
+      {"coalesced", [&](const u32x4* p) { readk<1, false><<<256, 512>>>(p, ntiles, out); }},
+      {"coalesced+pf", [&](const u32x4* p) { readk<1, true><<<256, 512>>>(p, ntiles, out); }},
+      {"crc32_uniform4k (production)", [&](const u32x4* p) {
+         subspace_crc32_batch_uniform(ctx, p, 4096, 4096, 65536, 0xFFFFFFFFu, 1, crc, nullptr); }},
+  };
+  for (int rep = 0; rep < 2; rep++)
+    for (auto& v : vs) {
+      u64 r = 0;
+      auto t0 = std::chrono::steady_clock::now();
+      while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < 0.04) {
+        for (int i = 0; i < 16; i++) v.f(buf + (r++ % nwin) * (win / 16));
+        CK(hipDeviceSynchronize());
+      }
+      hipEvent_t a, b;
+      CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+      CK(hipEventRecord(a));
+      const int n = 300;
+      for (int i = 0; i < n; i++) v.f(buf + (r++ % nwin) * (win / 16));
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      float ms; CK(hipEventElapsedTime(&ms, a, b));
+      printf("%-30s %7.2f us/launch %6.3f TB/s\n", v.name, ms * 1e3 / n, win / (ms * 1e-3 / n) / 1e12);
+      fflush(stdout);
+    }
+  subspace_crc_ctx_destroy(ctx);
+  return 0;
+}
