@@ -151,6 +151,11 @@ __device__ __forceinline__ u32 step1(u32 crc, u32 b, u32 lc1) {
   return (crc >> 8) ^ lds_ld(__builtin_amdgcn_perm(x, lc1, 0x0c020400u) + 128);
 }
 
+// Wait until every vector-memory access of this wave has completed. Issued right before a
+// tile's loads, so a wave never has more than one tile of loads outstanding. Inline asm
+// is invisible to hipcc's waitcnt pass, which keeps its own (weaker) waits.
+__device__ __forceinline__ void drain_before_issue() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

@@ -340,11 +340,13 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   // whenever all 64 slots are full, and once more at the end.
   u64 k = 0;
   for (; k + 1 < nk; k += 2) {
+    drain_before_issue();             // at most one tile of loads in flight (crc_uniform.hip)
     const TileDesc d1 = unpack(dB);   // tile k+1
     const u32 m1 = mB;
     fetch_desc(k + 2, dA, mA);        // tile k+2 (clamped)
     load_line(d1, B, true);
     process(A, dcur, mcur, k);
+    drain_before_issue();
     const TileDesc d2 = unpack(dA);   // tile k+2 (clamped)
     const u32 m2 = mA;
     fetch_desc(k + 3, dB, mB);        // tile k+3 (clamped)

@@ -138,11 +138,16 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
 
   // Ping-pong buffers, loop unrolled by two (no early exit: a break between the halves
   // would give the loop head a predecessor with fewer loads in flight, and hipcc's waitcnt
-  // merge would drain the prefetch there); the ring is stored when full.
+  // merge would drain the prefetch there); the ring is stored when full. Tile k has
+  // landed before tile k+1 is issued (drain_before_issue): each wave keeps at most one
+  // tile in flight, which HBM serves faster than two (45.5 vs 47.3 us per 256 MiB launch,
+  // profiles/r01/ceiling.md), and tile k+1's latency still hides behind tile k's compute.
   u32 k = 0, kf = 0;
   for (; k + 1 < nk; k += 2) {
+    drain_before_issue();
     load_tile(B, k + 1);
     tile_result(line_crc(A), k, kf);
+    drain_before_issue();
     load_tile(A, k + 2);
     tile_result(line_crc(B), k + 1, kf);
     if (k + 2 - kf == (u32)(kRing / 2)) {
@@ -163,6 +168,6 @@ template __global__ void crc32_uniform4k_kernel<512>(const uint8_t*, u64, u64, c
 template __global__ void crc32_uniform4k_kernel<768>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
                                                      int);
 template __global__ void crc32_uniform4k_kernel<1024>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                      int);
+                                                     int);
 
 }  // namespace subspace_amd
