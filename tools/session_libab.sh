@@ -1,0 +1,18 @@
+#!/bin/bash
+# A/B of two library builds on the config-B uniform launch (sweep_uniform, 512 threads,
+# order 0), interleaved A B A B in separate processes.
+#   bash tools/session_libab.sh <tag> <libA.so> <libB.so>
+set -u
+TAG=$1; A=$2; B=$3
+OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/$TAG
+mkdir -p $OUT
+for i in 1 2; do
+  for v in A B; do
+    lib=$A; [ $v = B ] && lib=$B
+    SUBSPACE_CRC_PROBE_LIB=$lib timeout -k 10 200 python tools/sweep_uniform.py 65536 512 7 0 > $OUT/$v$i.out 2> $OUT/$v$i.err
+    rc=$?
+    echo "$v$i rc=$rc" >> $OUT/status.txt
+    if [ $rc -ne 0 ]; then exit $rc; fi
+  done
+done
+echo done >> $OUT/status.txt

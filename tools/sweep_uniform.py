@@ -18,6 +18,7 @@ def main():
     wgs = [int(x) for x in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["512", "768", "1024"])]
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
     orders = [int(x) for x in (sys.argv[4].split(",") if len(sys.argv) > 4 else ["0"])]
+    blocks = [int(x) for x in (sys.argv[5].split(",") if len(sys.argv) > 5 else ["0"])]
     ctx = gpu.CrcContext(0)
     lib = _lib.load()
     dev = torch.device("cuda", 0)
@@ -30,10 +31,13 @@ def main():
         out = torch.empty(count, dtype=torch.int32, device=dev)
         torch.cuda.synchronize()
         iters = max(8, int(2e9 // (count * 4096)))
+        for i in range(max(400, int(16e9 // (count * 4096)))):  # >= ~20 ms of warm-up (sustained.md)
+            ctx.crc32_uniform(bufs[i % nb], 4096, 4096, count, out)
+        torch.cuda.synchronize()
         ref = None
         for r in range(rounds):
-            for wg, order in [(a, b) for a in wgs for b in orders]:
-                if lib.subspace_crc_testutil_tune(ctx._h, wg, 0, order) != 0:
+            for wg, order, nb_cap in [(a, b, c) for a in wgs for b in orders for c in blocks]:
+                if lib.subspace_crc_testutil_tune(ctx._h, wg, nb_cap, order) != 0:
                     raise SystemExit(f"bad variant wg={wg} order={order}")
                 if r == 0:  # every variant must produce the same CRCs
                     ctx.crc32_uniform(bufs[0], 4096, 4096, count, out)
@@ -41,7 +45,7 @@ def main():
                     if ref is None:
                         ref = got
                     elif not torch.equal(ref, got):
-                        raise SystemExit(f"variant wg={wg} order={order} differs")
+                        raise SystemExit(f"variant wg={wg} order={order} blocks={nb_cap} differs")
                 for i in range(3):
                     ctx.crc32_uniform(bufs[i % nb], 4096, 4096, count, out)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -51,12 +55,13 @@ def main():
                 b.record()
                 torch.cuda.synchronize()
                 ms = a.elapsed_time(b) / iters
-                res.setdefault((count, wg, order), []).append(ms)
+                res.setdefault((count, wg, order, nb_cap), []).append(ms)
         del bufs
         torch.cuda.empty_cache()
-    for (count, wg, order), v in sorted(res.items()):
+    for (count, wg, order, nb_cap), v in sorted(res.items()):
         med, best = float(np.median(v)), float(np.min(v))
-        print(json.dumps({"count": count, "wg": wg, "order": order, "median_ms": round(med, 4), "best_ms": round(best, 4),
+        print(json.dumps({"count": count, "wg": wg, "order": order, "blocks": nb_cap or "all CUs",
+                          "median_ms": round(med, 4), "best_ms": round(best, 4),
                           "TBps_median": round(count * 4096 / med / 1e9, 3),
                           "TBps_best": round(count * 4096 / best / 1e9, 3)}), flush=True)
 

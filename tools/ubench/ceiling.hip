@@ -1,8 +1,9 @@
 // Read ceilings at config B's launch size (investigation tool): 256 MiB per launch,
 // 4 rotated windows (1 GiB), 300 back-to-back launches per variant after a 40 ms warm-up
-// of the same variant, variants interleaved twice. Compared with the production CRC kernel
-// (through the C ABI) under the same schedule.
-//   hipcc --offload-arch=gfx950 -O3 -o ceiling ceiling.hip -I../../include -L../../subspace_amd -lsubspace_crc
+// of the same variant, variants interleaved twice. Compared with the CRC kernel of every
+// library build named in CEILING_LIBS (comma-separated .so paths, dlopen'ed side by side;
+// default: the in-tree subspace_amd/libsubspace_crc.so) under the same schedule.
+//   hipcc --offload-arch=gfx950 -O3 -o ceiling ceiling.hip -I../../include -ldl
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
@@ -10,6 +11,10 @@
 #include <cstdint>
 #include <functional>
 #include <vector>
+
+#include <dlfcn.h>
+#include <cstring>
+#include <string>
 
 #include "subspace_crc.h"
 
@@ -68,14 +73,74 @@ __global__ __launch_bounds__(512) void readk(const u32x4* __restrict__ p, u64 nt
   out[blockIdx.x * 512 + threadIdx.x] = acc;
 }
 
+// lines (drain, then issue the next tile) + optional LDS fill prologue + optional dependent
+// VALU work per tile (overlapping the next tile's loads, like the CRC kernel's compute).
+template <int FILL, int WORK>
+__global__ __launch_bounds__(512) void linesx(const u32x4* __restrict__ p, u64 ntiles, u32* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) u32 smem[];
+  const int lane = threadIdx.x & 63;
+  const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u64 w = front(blockIdx.x, gridDim.x, wid), nw = (u64)gridDim.x * 8;
+  const u32 nk = w < ntiles ? (u32)((ntiles - w + nw - 1) / nw) : 0u;
+  u32x4 a[8];
+  const u64 t0 = nk ? w : 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) a[i] = p[t0 * 512 + lane * 8 + i];
+  if (FILL) {
+    for (int i = threadIdx.x; i < 32768; i += 512) smem[i] = (u32)i * 2654435761u;
+    __syncthreads();
+  }
+  u32 acc = 0;
+  for (u32 k = 0; k < nk; k++) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    u32x4 b[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) b[i] = a[i];
+    const u64 tn = w + (u64)(k + 1 < nk ? k + 1 : k) * nw;
+#pragma unroll
+    for (int i = 0; i < 8; i++) a[i] = p[tn * 512 + lane * 8 + i];
+    __builtin_amdgcn_sched_barrier(0);
+    u32 x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) x ^= b[i].x ^ b[i].y ^ b[i].z ^ b[i].w;
+    for (int r = 0; r < WORK; r++) x = x * 2654435761u + (x >> 7);
+    acc ^= x;
+  }
+  if (FILL) acc ^= smem[lane];
+  out[blockIdx.x * 512 + threadIdx.x] = acc;
+}
+
 int main() {
   const u64 win = 256ull << 20, nwin = 4, ntiles = win / 8192;
   u32x4* buf; CK(hipMalloc(&buf, win * nwin));
   u32* out; CK(hipMalloc(&out, 256 * 512 * 4));
   u32* crc; CK(hipMalloc(&crc, 65536 * 4));
   CK(hipMemset(buf, 0x5A, win * nwin));
-  subspace_crc_ctx* ctx;
-  if (subspace_crc_ctx_create(0, &ctx)) { fprintf(stderr, "ctx: %s\n", subspace_crc_last_error()); return 1; }
+  typedef int (*create_t)(int, subspace_crc_ctx**);
+  typedef int (*uni_t)(subspace_crc_ctx*, const void*, uint64_t, uint64_t, uint64_t, uint32_t, uint32_t, uint32_t*,
+                       void*);
+  struct Lib { std::string path; uni_t uni; subspace_crc_ctx* ctx; };
+  std::vector<Lib> libs;
+  {
+    const char* env = getenv("CEILING_LIBS");
+    std::string all = env ? env : "subspace_amd/libsubspace_crc.so";
+    size_t pos = 0;
+    while (pos <= all.size()) {
+      size_t e = all.find(',', pos);
+      if (e == std::string::npos) e = all.size();
+      std::string path = all.substr(pos, e - pos);
+      pos = e + 1;
+      if (path.empty()) continue;
+      void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+      if (!h) { fprintf(stderr, "dlopen %s: %s\n", path.c_str(), dlerror()); return 1; }
+      auto create = (create_t)dlsym(h, "subspace_crc_ctx_create");
+      Lib L{path, (uni_t)dlsym(h, "subspace_crc32_batch_uniform"), nullptr};
+      if (!create || !L.uni || create(0, &L.ctx)) { fprintf(stderr, "ctx for %s failed\n", path.c_str()); return 1; }
+      libs.push_back(L);
+    }
+  }
+  CK(hipFuncSetAttribute((const void*)linesx<1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024));
+  CK(hipFuncSetAttribute((const void*)linesx<1, 800>, hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024));
   CK(hipDeviceSynchronize());
   struct V { const char* name; std::function<void(const u32x4*)> f; };
   std::vector<V> vs = {
@@ -83,9 +148,11 @@ int main() {
       {"lines+pf", [&](const u32x4* p) { readk<0, true><<<256, 512>>>(p, ntiles, out); }},
       {"coalesced", [&](const u32x4* p) { readk<1, false><<<256, 512>>>(p, ntiles, out); }},
       {"coalesced+pf", [&](const u32x4* p) { readk<1, true><<<256, 512>>>(p, ntiles, out); }},
-      {"crc32_uniform4k (production)", [&](const u32x4* p) {
-         subspace_crc32_batch_uniform(ctx, p, 4096, 4096, 65536, 0xFFFFFFFFu, 1, crc, nullptr); }},
+      {"lines + 152 KiB LDS fill", [&](const u32x4* p) { linesx<1, 0><<<256, 512, 152 * 1024>>>(p, ntiles, out); }},
   };
+  for (auto& L : libs)
+    vs.push_back({strdup(("crc " + L.path).c_str()), [&L, crc](const u32x4* p) {
+                    L.uni(L.ctx, p, 4096, 4096, 65536, 0xFFFFFFFFu, 1, crc, nullptr); }});
   for (int rep = 0; rep < 2; rep++)
     for (auto& v : vs) {
       u64 r = 0;
@@ -102,9 +169,8 @@ int main() {
       CK(hipEventRecord(b));
       CK(hipEventSynchronize(b));
       float ms; CK(hipEventElapsedTime(&ms, a, b));
-      printf("%-30s %7.2f us/launch %6.3f TB/s\n", v.name, ms * 1e3 / n, win / (ms * 1e-3 / n) / 1e12);
+      printf("%-50s %7.2f us/launch %6.3f TB/s\n", v.name, ms * 1e3 / n, win / (ms * 1e-3 / n) / 1e12);
       fflush(stdout);
     }
-  subspace_crc_ctx_destroy(ctx);
   return 0;
 }
