@@ -45,11 +45,13 @@ ROTATE = 4  # 4 x 256 MiB > the 256 MiB Infinity Cache: every step reads HBM
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # Defaults measure steady state: after an idle spell the first ~300 back-to-back launches
-    # of this kernel run up to 25 % slower while the GPU's power management settles
-    # (profiles/r01/sustained.md); 400 untimed launches take ~20 ms.
     ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=20)
+    # After an idle spell the first ~300 back-to-back launches of this kernel run up to 25 %
+    # slower while the GPU's power management settles (profiles/r01/sustained.md). Before
+    # the W warm-up steps the bench runs untimed settle launches until SETTLE launches have
+    # run in all; reported as "settle_launches" (0 disables).
+    ap.add_argument("--settle", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="budget for the CPU baseline legs")
@@ -177,6 +179,9 @@ def main():
         k = i % nbuf
         ctx.crc32_uniform(bufs[k], MSG_BYTES, MSG_BYTES, nmsg, outs[k])
 
+    settle = max(0, args.settle - args.warmup)
+    for i in range(settle):
+        step(i)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -278,6 +283,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_launches": settle,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": scaling,

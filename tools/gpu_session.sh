@@ -43,7 +43,7 @@ for s in $STEPS; do
     pmc)
       for ctr in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $ctr -d "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr" -o run \
-          --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline \
+          --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 2 --settle 0 --no-cpu-baseline \
           --no-e2e > "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.json" 2> "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr.err")
         stop_if_fault $? "pmc_$ctr"
       done ;;

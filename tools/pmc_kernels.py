@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Small fixed workload for PMC passes (investigation tool): 3 launches each of the
-uniform kernel (1 Mi x 4 KiB = 4 GiB) and the ragged kernel (32 x 64 MiB = 2 GiB,
-config D's shape). Run under `rocprofv3 --pmc ...`, one counter group per pass."""
+uniform kernel (1 Mi x 4 KiB = 4 GiB), the ragged kernel on config D's shape (32 x 64 MiB
+= 2 GiB) and on config C's shape (10,000 log-uniform messages, ~1 GiB, unaligned ends).
+Run under `rocprofv3 --pmc ...`, one counter group per pass."""
 import sys
 from pathlib import Path
 
@@ -29,7 +30,17 @@ def main():
     for _ in range(3):
         ctx.crc32_ragged(buf[: m * L], offs, lens, rout)
     torch.cuda.synchronize()
-    print("ok", int(out[0].item()) & 0xFFFFFFFF, int(rout[0].item()) & 0xFFFFFFFF)
+    # config C's shape (log-uniform 64 B - 1 MiB, unaligned ends) over ~1 GiB
+    from subspace_amd import synth
+    lens = synth.ragged_lengths(synth.SEED_C, 10000)
+    offs, total = synth.packed_offsets(lens, 64)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int64)).to(dev)
+    cout = torch.empty(len(lens), dtype=torch.int32, device=dev)
+    for _ in range(3):
+        ctx.crc32_ragged(buf[: int(total) + 64], d_off, d_len, cout)
+    torch.cuda.synchronize()
+    print("ok", int(out[0].item()) & 0xFFFFFFFF, int(rout[0].item()) & 0xFFFFFFFF, int(total))
     ctx.close()
 
 
