@@ -92,6 +92,8 @@ def load() -> ctypes.CDLL:
     lib.subspace_crc_testutil_fill_ragged.argtypes = [vp, vp, vp, u64, u64, u64, u64, vp]
     lib.subspace_crc_testutil_tune.restype = i32
     lib.subspace_crc_testutil_tune.argtypes = [vp, i32, i32, i32]
+    lib.subspace_crc_testutil_set.restype = i32
+    lib.subspace_crc_testutil_set.argtypes = [vp, ctypes.c_char_p, i32]
     lib.subspace_crc_testutil_stream_read.restype = i32
     lib.subspace_crc_testutil_stream_read.argtypes = [vp, u64, vp, vp]
     _lib = lib

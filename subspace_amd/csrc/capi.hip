@@ -33,6 +33,9 @@ __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, 
 __global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*);
 hipError_t ragged_scan(void* temp, size_t& temp_bytes, const u64* in, u64* out, u64 n, hipStream_t stream);
 __global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* offsets, u64* lengths);
+template <int WG>
+__global__ void crc32_long_kernel(const uint8_t*, u64, u32, u32, const u32*, const u32*, u32, u32, u32*);
+__global__ void crc32_long_final_kernel(const u32*, u32, u32, u32*);
 
 }  // namespace subspace_amd
 
@@ -108,6 +111,7 @@ struct subspace_crc_ctx {
   int uniform_wg = 512;    // workgroup size of the uniform kernel (256/512/640/768/1024)
   int uniform_blocks = 0;  // 0 = one workgroup per CU
   int uniform_order = 0;   // tile order: 0 XCD-spread sweep, 1 per-workgroup region, 2 plain sweep
+  bool long_path = true;   // whole-8 KiB-piece uniform batches take crc32_long_kernel
   u64* d_uoff = nullptr;  // offsets/lengths materialised for non-4K uniform batches
   u64* d_ulen = nullptr;
   u64 u_capacity = 0;
@@ -343,6 +347,9 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_ragged_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)ragged_lds_bytes());
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_long_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)ragged_lds_bytes());
   if (e != hipSuccess) {
     subspace_crc_ctx_destroy(c);
     return hip_fail(e, "context setup");
@@ -451,6 +458,27 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
       default: LAUNCH(512); break;
     }
 #undef LAUNCH
+    HIP_TRY(hipGetLastError());
+    return SUBSPACE_CRC_OK;
+  }
+  // Long messages in whole 8 KiB pieces, 16-B aligned (config D): the long-message kernel
+  // (implicit tiles, plain loads), then the XOR-scan combine of the ragged path.
+  const u64 pieces = length / 8192;
+  const bool long_fast = length >= 8192 && length % 8192 == 0 && (stride % 16) == 0 &&
+                         ((uintptr_t)dev_base % 16) == 0 && pieces <= (1ull << kNumTileOps) &&
+                         count < (1ull << 32) && pieces * count < (1ull << 32);
+  if (long_fast && c->long_path) {
+    const u64 tiles = pieces * count;
+    int rc = ensure_ragged_ws(c, 0, tiles);
+    if (rc) return rc;
+    crc32_long_kernel<kRaggedWG><<<c->num_cus, kRaggedWG, ragged_lds_bytes(), st>>>(
+        static_cast<const uint8_t*>(dev_base), stride, (u32)pieces, (u32)count, c->d_tab, c->d_rops, init, final_xor,
+        c->d_tilecrc);
+    HIP_TRY(hipGetLastError());
+    size_t xtmp = c->xscan_tmp_bytes;
+    HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, c->d_px, tiles, st));
+    crc32_long_final_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(c->d_px, (u32)pieces, (u32)count,
+                                                                              dev_out);
     HIP_TRY(hipGetLastError());
     return SUBSPACE_CRC_OK;
   }
@@ -792,6 +820,18 @@ int subspace_crc32_host_slot_list(subspace_crc_ctx* c, const subspace_crc_slot* 
   if (host_status) std::memcpy(host_status, c->l_hstatus, count * sizeof(u32));
   if (host_error_count) *host_error_count = c->l_hstatus[count];
   return SUBSPACE_CRC_OK;
+}
+
+// Experiment hook (not part of the public header): named knobs.
+//   "long_path": 1 (default) whole-8 KiB-piece uniform batches take crc32_long_kernel,
+//                0 they take the ragged path
+int subspace_crc_testutil_set(subspace_crc_ctx* c, const char* key, int value) {
+  if (!c || !key) return SUBSPACE_CRC_EINVAL;
+  if (!std::strcmp(key, "long_path")) {
+    c->long_path = value != 0;
+    return SUBSPACE_CRC_OK;
+  }
+  return SUBSPACE_CRC_EINVAL;
 }
 
 // Tuning hook for experiments (not part of the public header): uniform-kernel workgroup

@@ -96,7 +96,7 @@ def main():
             ms = timed(lambda: ctx.crc32_ragged(buf, d_off, d_len, out), args.iters)
             report("D", n * L, ms, out.cpu().numpy().view(np.uint32), "D", {"messages": n})
             ms_u = timed(lambda: ctx.crc32_uniform(buf, L, L, n, out), args.iters)
-            report("D via batch_uniform", n * L, ms_u, out.cpu().numpy().view(np.uint32), "D")
+            report("D via batch_uniform (long-message kernel)", n * L, ms_u, out.cpu().numpy().view(np.uint32), "D")
             del buf, d_off, d_len, out
         elif cfg == "E":
             n, G = GOLD["E"]["count"], 8
