@@ -13,7 +13,7 @@ CPP_SRCS := $(CSRC)/host_crc.cpp
 HDRS := $(CSRC)/crc_device.h $(CSRC)/crc_math.h include/subspace_crc.h
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))
 
-all: $(LIB) oracle
+all: $(LIB) oracle tools/config_a
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -29,11 +29,16 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# config A (CPU plumbing: 1 pub x 1 sub calc+verify latency through the drop-in header)
+tools/config_a: tools/config_a.cpp include/subspace/checksum.h $(LIB)
+	g++ -O2 -std=c++17 -Iinclude -o $@ tools/config_a.cpp -Lsubspace_amd -lsubspace_crc \
+	    -Wl,-rpath,'$$ORIGIN/../subspace_amd' -ldl
+
 test-cpu: all
 	python -m pytest tests/ -x -q -m "not gpu"
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) tools/config_a
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle test-cpu clean

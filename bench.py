@@ -87,6 +87,24 @@ def cpu_baseline(batches_host: list[np.ndarray], seconds: float) -> dict:
 
     r1, b1 = rate(1, seconds / 2)
     rn, bn = rate(threads, seconds / 2)
+    sse = None
+    if orc.has_sse42():  # informational: the reference's -msse4.2 path computes CRC-32C
+        done, t0, i = 0, time.perf_counter(), 0
+        while time.perf_counter() - t0 < min(1.0, seconds / 4):
+            orc.crc32c_sse42_batch(batches_host[i % len(batches_host)], offs, lens, threads=threads)
+            done += BATCH_BYTES
+            i += 1
+        sse = round(done / (time.perf_counter() - t0) / 2**30, 3)
+    config_a = None  # BASELINE configs[0]: the per-message CPU path (tools/config_a.cpp)
+    exe = ROOT / "tools" / "config_a"
+    if exe.exists():
+        import subprocess
+        try:
+            r = subprocess.run([str(exe), "20000", str(ROOT / "oracle" / "liboracle_crc.so")], capture_output=True,
+                               text=True, timeout=120)
+            config_a = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None
+        except (subprocess.SubprocessError, ValueError, IndexError):
+            config_a = None
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -97,6 +115,10 @@ def cpu_baseline(batches_host: list[np.ndarray], seconds: float) -> dict:
         pass
     return {"value": round(rn, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "value_1core": round(r1, 3),
+            "sse42_crc32c_value": sse,
+            "config_a": config_a,
+            "sse42_crc32c_note": "client/checksum.cc:56-76 (-msse4.2 builds) restated on the same batches and "
+                                 "threads: CRC-32C, NOT bit-exact with the IEEE parity path; informational",
             "sample": f"config-B batches (65,536 x 4 KiB, host copies of the device batches): "
                       f"{bn / 2**30:.2f} GiB on {threads} threads, {b1 / 2**30:.2f} GiB on 1 thread; "
                       f"oracle/crc32_oracle.c byte-table loop (reference client/checksum.cc:125-130), "

@@ -38,6 +38,12 @@ void oracle_synth_crc_batch(uint64_t seed, const uint64_t* msg_ids, const uint64
                             uint32_t init, uint32_t* out, int nthreads);
 uint64_t oracle_ragged_length(uint64_t seed, uint64_t i);
 
+/* crc32c_sse42.c: the reference's -msse4.2 path (client/checksum.cc:56-76), informational */
+int oracle_has_sse42(void);
+uint32_t oracle_crc32c_sse42(uint32_t crc, const uint8_t* data, size_t length);
+void oracle_crc32c_sse42_batch(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, size_t n,
+                               uint32_t init, uint32_t* out, int nthreads);
+
 /* castagnoli != 0: the same with CRC-32C (client/checksum.cc:56-76) */
 void oracle_synth_crc_batch_poly(uint64_t seed, const uint64_t* msg_ids, const uint64_t* lengths, size_t n,
                                  uint32_t init, uint32_t* out, int nthreads, int castagnoli);

@@ -38,6 +38,10 @@ class Oracle:
         lib.oracle_ragged_length.argtypes = [u64, u64]
         lib.oracle_publish_slots.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int32, ctypes.c_int32]
         lib.oracle_verify_slots.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int32, ctypes.c_int32, vp]
+        lib.oracle_has_sse42.restype = ctypes.c_int
+        lib.oracle_crc32c_sse42.restype = u32
+        lib.oracle_crc32c_sse42.argtypes = [u32, vp, sz]
+        lib.oracle_crc32c_sse42_batch.argtypes = [vp, vp, vp, sz, u32, vp, ctypes.c_int]
         lib.oracle_crc32c.restype = u32
         lib.oracle_crc32c.argtypes = [u32, vp, sz]
         lib.oracle_synth_crc_batch_poly.argtypes = [u64, vp, vp, sz, u32, vp, ctypes.c_int, ctypes.c_int]
@@ -72,6 +76,22 @@ class Oracle:
     def crc32c(self, crc: int, data: bytes) -> int:
         buf = ctypes.create_string_buffer(bytes(data), len(data))
         return int(self.lib.oracle_crc32c(crc & 0xFFFFFFFF, buf, len(data)))
+
+    def has_sse42(self) -> bool:
+        return bool(self.lib.oracle_has_sse42())
+
+    def crc32c_sse42(self, crc: int, data: bytes) -> int:
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        return int(self.lib.oracle_crc32c_sse42(crc & 0xFFFFFFFF, buf, len(data)))
+
+    def crc32c_sse42_batch(self, base: np.ndarray, offsets, lengths, init: int = 0xFFFFFFFF,
+                           threads: int = 1) -> np.ndarray:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+        out = np.zeros(len(offsets), dtype=np.uint32)
+        self.lib.oracle_crc32c_sse42_batch(base.ctypes.data, offsets.ctypes.data, lengths.ctypes.data, len(offsets),
+                                           init & 0xFFFFFFFF, out.ctypes.data, threads)
+        return out
 
     def checksum(self, spans) -> bytes:
         crc = 0xFFFFFFFF

@@ -38,3 +38,17 @@ def test_host_crc32c_matches_oracle_and_chains(oracle):
 
 def test_crc32c_differs_from_ieee(oracle):
     assert oracle.crc32c(M32, b"123456789") != oracle.crc32(M32, b"123456789")
+
+
+def test_sse42_restatement_matches_table_crc32c(oracle):
+    """The informational -msse4.2 restatement (client/checksum.cc:56-76) computes CRC-32C:
+    equal to the table restatement, and to the published check value."""
+    import pytest
+    if not oracle.has_sse42():
+        pytest.skip("CPU without SSE4.2")
+    assert (~oracle.crc32c_sse42(M32, b"123456789")) & M32 == 0xE3069283
+    rng = np.random.default_rng(42)
+    for n in (0, 1, 3, 4, 5, 7, 8, 9, 15, 16, 17, 100, 4096, 4099):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        seed = int(rng.integers(0, 2**32))
+        assert oracle.crc32c_sse42(seed, data) == oracle.crc32c(seed, data), n

@@ -177,3 +177,18 @@ def test_header_castagnoli_build(lib, tmp_path):
                     str(exe), f"-L{libdir}", "-lsubspace_crc", f"-Wl,-rpath,{libdir}"], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0 and r.stdout.strip() == "e3069283", r.stdout + r.stderr
+
+
+def test_config_a_harness(lib):
+    """tools/config_a (BASELINE configs[0]): 1 pub x 1 sub calc+verify through the drop-in
+    header over a memfd channel; every message verifies, both legs report latencies."""
+    import json
+    exe = ROOT / "tools" / "config_a"
+    if not exe.exists():
+        subprocess.run(["make", "-C", str(ROOT), "tools/config_a"], check=True)
+    r = subprocess.run([str(exe), "500", str(ROOT / "oracle" / "liboracle_crc.so")], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout)
+    assert d["failures"] == 0 and d["messages"] == 500
+    assert d["dropin"]["p50_ns"] > 0 and d["reference"]["p50_ns"] > 0
