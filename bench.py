@@ -274,8 +274,10 @@ def main():
         cpu = cpu_baseline([b.cpu().numpy() for b in bufs], args.cpu_seconds)
 
     traffic = None
+    # PMC-measured HBM bytes per config-B launch (tools/summarize_profile.py); other
+    # workloads' launches are a different size, so no figure for them
     tfile = ROOT / "profiles" / "traffic_uniform4k.json"
-    if tfile.exists():
+    if tfile.exists() and args.workload == "B":
         try:
             traffic = json.loads(tfile.read_text()).get("hbm_bytes_per_launch")
         except Exception:
