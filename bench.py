@@ -52,6 +52,11 @@ def parse():
     # the W warm-up steps the bench runs untimed settle launches until SETTLE launches have
     # run in all; reported as "settle_launches" (0 disables).
     ap.add_argument("--settle", type=int, default=400)
+    # --streams 2: consecutive steps alternate between two HIP streams (independent batches)
+    # and overlap (45.2 vs 46.7 us per launch in profiles/r01/ceiling.md). Off by default:
+    # overlapping dispatches make rocprofv3's per-dispatch duration (~2x, both kernels
+    # resident) disagree with the roofline's per-launch interval.
+    ap.add_argument("--streams", type=int, default=1, choices=[1, 2])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="budget for the CPU baseline legs")
@@ -197,9 +202,17 @@ def main():
     step_bytes = nmsg * MSG_BYTES
     torch.cuda.synchronize()
 
+    if nbuf % args.streams:  # workload E has one buffer: its steps stay on one stream
+        args.streams = 1
+    streams = [stream] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
+    for s2 in streams[1:]:
+        s2.wait_stream(stream)
+
     def step(i):
+        # batch i % nbuf always runs on stream i % len(streams): nbuf is a multiple of the
+        # stream count, so a batch's buffers are only ever used in order on one stream
         k = i % nbuf
-        ctx.crc32_uniform(bufs[k], MSG_BYTES, MSG_BYTES, nmsg, outs[k])
+        ctx.crc32_uniform(bufs[k], MSG_BYTES, MSG_BYTES, nmsg, outs[k], stream=streams[i % len(streams)])
 
     settle = max(0, args.settle - args.warmup)
     for i in range(settle):
@@ -218,6 +231,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     region[0].record(stream)
+    for s2 in streams[1:]:
+        s2.wait_stream(stream)  # every stream starts after the region's first event
     for i in range(args.steps):
         e = ev.get(i)
         if e:
@@ -225,6 +240,8 @@ def main():
         step(i)
         if e:
             e[1].record(stream)
+    for s2 in streams[1:]:
+        stream.wait_stream(s2)  # ... and the last event after every stream's last launch
     region[1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -234,9 +251,11 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # Launch duration of the CRC kernel: the HIP-event span of the K back-to-back launches on
-    # their stream / K. It includes the inter-launch gaps, so `achieved` is a lower bound on
-    # the kernel's own rate (rocprofv3's per-dispatch average is the upper one).
+    # Launch interval of the CRC kernel: the HIP-event span of the K back-to-back launches /
+    # K (events on the first stream, joined with the second). With two streams consecutive
+    # launches overlap, so this effective interval is shorter than rocprofv3's per-dispatch
+    # duration (which then counts the overlapped part twice); with one stream it includes
+    # the inter-launch gaps.
     avg_kern_ms = region[0].elapsed_time(region[1]) / args.steps
     sampled_ms = float(np.mean([a.elapsed_time(b) for a, b in ev.values()])) if ev else None
 
@@ -289,7 +308,7 @@ def main():
             workload = {"workload": "B: 65,536 x 4 KiB payloads per GPU per step, one CRC32 (IEEE, "
                                     "client/checksum.cc default build) each", "messages_per_gpu": nmsg,
                         "message_bytes": MSG_BYTES, "batches_rotated": ROTATE,
-                        "parallelism": f"independent message shards x{world}"}
+                        "parallelism": f"independent message shards x{world}", "streams": args.streams}
             scaling = "weak"
         else:
             total_bytes = (8 << 20) * MSG_BYTES * args.steps  # the whole 8 Mi batch per step
@@ -321,7 +340,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "subspace_amd::crc32_uniform4k_kernel<512>", "avg_launch_ms": round(avg_kern_ms, 4),
-                         "launch_ms_source": "HIP events around the timed region on the launch stream / K",
+                         "launch_ms_source": f"HIP event span of the timed region / K ({args.streams} stream(s), "
+                                             "consecutive launches overlap when 2)",
                          "sampled_launch_ms": round(sampled_ms, 4) if sampled_ms else None},
             "cpu_baseline": cpu,
             "e2e_pcie": e2e,

@@ -150,9 +150,20 @@ int main() {
       {"coalesced+pf", [&](const u32x4* p) { readk<1, true><<<256, 512>>>(p, ntiles, out); }},
       {"lines + 152 KiB LDS fill", [&](const u32x4* p) { linesx<1, 0><<<256, 512, 152 * 1024>>>(p, ntiles, out); }},
   };
-  for (auto& L : libs)
+  hipStream_t s2[2];
+  CK(hipStreamCreateWithFlags(&s2[0], hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&s2[1], hipStreamNonBlocking));
+  u32* crc2; CK(hipMalloc(&crc2, 65536 * 4));
+  int flip = 0;
+  for (auto& L : libs) {
     vs.push_back({strdup(("crc " + L.path).c_str()), [&L, crc](const u32x4* p) {
                     L.uni(L.ctx, p, 4096, 4096, 65536, 0xFFFFFFFFu, 1, crc, nullptr); }});
+    // consecutive launches alternate between two streams (independent batches): the next
+    // launch may start on CUs the previous one has released
+    vs.push_back({strdup(("crc 2 streams " + L.path).c_str()), [&L, crc, crc2, &s2, &flip](const u32x4* p) {
+                    flip ^= 1;
+                    L.uni(L.ctx, p, 4096, 4096, 65536, 0xFFFFFFFFu, 1, flip ? crc : crc2, s2[flip]); }});
+  }
   for (int rep = 0; rep < 2; rep++)
     for (auto& v : vs) {
       u64 r = 0;
@@ -161,14 +172,12 @@ int main() {
         for (int i = 0; i < 16; i++) v.f(buf + (r++ % nwin) * (win / 16));
         CK(hipDeviceSynchronize());
       }
-      hipEvent_t a, b;
-      CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
-      CK(hipEventRecord(a));
+      CK(hipDeviceSynchronize());
       const int n = 300;
+      auto w0 = std::chrono::steady_clock::now();
       for (int i = 0; i < n; i++) v.f(buf + (r++ % nwin) * (win / 16));
-      CK(hipEventRecord(b));
-      CK(hipEventSynchronize(b));
-      float ms; CK(hipEventElapsedTime(&ms, a, b));
+      CK(hipDeviceSynchronize());
+      const float ms = (float)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
       printf("%-50s %7.2f us/launch %6.3f TB/s\n", v.name, ms * 1e3 / n, win / (ms * 1e-3 / n) / 1e12);
       fflush(stdout);
     }
