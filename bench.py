@@ -315,7 +315,10 @@ def main():
             workload = {"workload": "E: 8 Mi x 4 KiB payloads per step, round-robin over the GPUs, one CRC32 each",
                         "messages_total": 8 << 20, "messages_per_gpu": nmsg, "message_bytes": MSG_BYTES,
                         "parallelism": f"round-robin message shards x{world}, RCCL all_gather of CRCs (untimed)",
-                        "gather_ms": round(gather_ms, 3) if gather_ms is not None else None}
+                        "gather_ms": round(gather_ms, 3) if gather_ms is not None else None,
+                        # the same rate with one gather of every step's CRCs to rank 0 added per step
+                        "value_incl_gather": round(total_bytes / (elapsed + args.steps * gather_ms * 1e-3) / 2**30, 2)
+                        if gather_ms is not None else None}
             scaling = "strong"
         value = total_bytes / elapsed / 2**30
         achieved = step_bytes / (avg_kern_ms * 1e-3) / 1e9
