@@ -89,6 +89,9 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
     const bool valid = (u32)lane < nt;
     u32 c = opmul(sbase, kRagOpZ4096, H0) ^ H1;
     u32 rem = valid ? (AF & 0x7FFFFFFFu) : 0u;  // Z_{8192 * pieces after}; pieces < 2^21 (host check)
+#ifdef SUBSPACE_PROBE_NOSHIFT
+    rem = 0;
+#endif
     for (int bit = 0; bit < kNumTileOps && __any(rem != 0u); bit++) {
       const u32 cm = opmul(sbase, kRagOpZTile + bit, c);
       c = (rem & 1u) ? cm : c;

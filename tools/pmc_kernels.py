@@ -30,6 +30,10 @@ def main():
     for _ in range(3):
         ctx.crc32_ragged(buf[: m * L], offs, lens, rout)
     torch.cuda.synchronize()
+    # config D's shape through the uniform API: the long-message kernel
+    for _ in range(3):
+        ctx.crc32_uniform(buf[: m * L], L, L, m, rout)
+    torch.cuda.synchronize()
     # config C's shape (log-uniform 64 B - 1 MiB, unaligned ends) over ~1 GiB
     from subspace_amd import synth
     lens = synth.ragged_lengths(synth.SEED_C, 10000)

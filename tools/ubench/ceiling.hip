@@ -115,6 +115,10 @@ int main() {
   u32x4* buf; CK(hipMalloc(&buf, win * nwin));
   u32* out; CK(hipMalloc(&out, 256 * 512 * 4));
   u32* crc; CK(hipMalloc(&crc, 65536 * 4));
+  // CEILING_MSG = message length for the library variants (default 4096: config B's
+  // 65,536 messages; e.g. 67108864 = config D's 64 MiB messages, 4 per 256 MiB launch)
+  const u64 msg = getenv("CEILING_MSG") ? strtoull(getenv("CEILING_MSG"), nullptr, 10) : 4096;
+  const u64 nmsg = win / msg;
   CK(hipMemset(buf, 0x5A, win * nwin));
   typedef int (*create_t)(int, subspace_crc_ctx**);
   typedef int (*uni_t)(subspace_crc_ctx*, const void*, uint64_t, uint64_t, uint64_t, uint32_t, uint32_t, uint32_t*,
@@ -156,13 +160,13 @@ int main() {
   u32* crc2; CK(hipMalloc(&crc2, 65536 * 4));
   int flip = 0;
   for (auto& L : libs) {
-    vs.push_back({strdup(("crc " + L.path).c_str()), [&L, crc](const u32x4* p) {
-                    L.uni(L.ctx, p, 4096, 4096, 65536, 0xFFFFFFFFu, 1, crc, nullptr); }});
+    vs.push_back({strdup(("crc " + L.path).c_str()), [&L, crc, msg, nmsg](const u32x4* p) {
+                    L.uni(L.ctx, p, msg, msg, nmsg, 0xFFFFFFFFu, 1, crc, nullptr); }});
     // consecutive launches alternate between two streams (independent batches): the next
     // launch may start on CUs the previous one has released
-    vs.push_back({strdup(("crc 2 streams " + L.path).c_str()), [&L, crc, crc2, &s2, &flip](const u32x4* p) {
+    vs.push_back({strdup(("crc 2 streams " + L.path).c_str()), [&L, crc, crc2, &s2, &flip, msg, nmsg](const u32x4* p) {
                     flip ^= 1;
-                    L.uni(L.ctx, p, 4096, 4096, 65536, 0xFFFFFFFFu, 1, flip ? crc : crc2, s2[flip]); }});
+                    L.uni(L.ctx, p, msg, msg, nmsg, 0xFFFFFFFFu, 1, flip ? crc : crc2, s2[flip]); }});
   }
   for (int rep = 0; rep < 2; rep++)
     for (auto& v : vs) {
