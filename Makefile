@@ -13,7 +13,7 @@ CPP_SRCS := $(CSRC)/host_crc.cpp
 HDRS := $(CSRC)/crc_device.h $(CSRC)/crc_math.h include/subspace_crc.h
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))
 
-all: $(LIB) oracle tools/config_a
+all: $(LIB) oracle tools/config_a tools/drain_demo
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -34,11 +34,16 @@ tools/config_a: tools/config_a.cpp include/subspace/checksum.h $(LIB)
 	g++ -O2 -std=c++17 -Iinclude -o $@ tools/config_a.cpp -Lsubspace_amd -lsubspace_crc \
 	    -Wl,-rpath,'$$ORIGIN/../subspace_amd' -ldl
 
+# subscriber drain / batch publish through the header-only C++ helper (a GPU test runs it)
+tools/drain_demo: tools/drain_demo.cpp include/subspace/checksum.h include/subspace/checksum_batch.h include/subspace_crc.h $(LIB)
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ tools/drain_demo.cpp -Lsubspace_amd -lsubspace_crc \
+	    -Wl,-rpath,'$$ORIGIN/../subspace_amd'
+
 test-cpu: all
 	python -m pytest tests/ -x -q -m "not gpu"
 
 clean:
-	rm -rf build $(LIB) tools/config_a
+	rm -rf build $(LIB) tools/config_a tools/drain_demo
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle test-cpu clean

@@ -286,3 +286,23 @@ def test_host_slot_list_unregistered_rejected(gpu_ctx):
     rec = slots.slot_records([host.ctypes.data], [host.ctypes.data + 64], [100])
     with pytest.raises(gpu.CrcError):
         gpu_ctx.crc32_host_slot_list(rec, max_message_size=4096, mode=gpu.SLOT_VERIFY)
+
+
+def test_drain_helper_cpp(gpu_ctx):
+    """include/subspace/checksum_batch.h from C++ (tools/drain_demo): a 64-slot memfd channel
+    published in one BatchChecksum::Calculate, every slot verified by the drop-in header's
+    VerifyCRC32Checksum<3> on the host; a shuffled 48-slot drain with corrupted payload and
+    prefix bytes, a cleared checksum flag and truncated delivered sizes verified in one call:
+    per-slot results, mismatch count and checksum_error flags equal the host templates';
+    after UnregisterBuffer the drain is rejected."""
+    import json
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parent.parent / "tools" / "drain_demo"
+    assert exe.exists(), "build tools/drain_demo first (make)"
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["device"] and d["failures"] == 0
+    assert d["mismatches"] == d["expected_mismatches"] >= 3 and d["unchecked"] >= 1
+    assert d["unregistered_rejected"]

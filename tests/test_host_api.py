@@ -192,3 +192,20 @@ def test_config_a_harness(lib):
     d = json.loads(r.stdout)
     assert d["failures"] == 0 and d["messages"] == 500
     assert d["dropin"]["p50_ns"] > 0 and d["reference"]["p50_ns"] > 0
+
+
+def test_drain_helper_builds_and_reports_no_device(lib):
+    """tools/drain_demo (include/subspace/checksum_batch.h, the header-only drain helper)
+    builds; without a usable device the helper reports the context error instead of
+    touching memory (exit 77, "device": false). On a GPU machine it runs the whole drain
+    (the GPU test checks its results)."""
+    import json
+    exe = ROOT / "tools" / "drain_demo"
+    if not exe.exists():
+        subprocess.run(["make", "-C", str(ROOT), "tools/drain_demo"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    if r.returncode == 77:
+        assert d["device"] is False and d["error"]
+    else:
+        assert r.returncode == 0 and d["failures"] == 0, r.stdout + r.stderr
