@@ -25,8 +25,9 @@ __global__ void crc32_ragged_count_kernel(const u64*, u32, u64, u32, u32, u64*, 
 __global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, u64, u64, TileDesc*, u32*);
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
-                                    const TileDesc*, const u32*, const u32*, const u32*, const u32*, u32, u32*, u32*);
-__global__ void crc32_ragged_final_kernel(const u64*, u64, const u32*, const u32*, u32*);
+                                    const TileDesc*, const u32*, const u32*, const u32*, u32, u32*, u32*);
+__global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, u64, const u32*, const u32*, const u32*, u32,
+                                          u32*);
 hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u32* out, u64 n, hipStream_t stream);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, int, int, u32, const u32*,
                                          const u32*, const u32*, u32*, u32*, u32*);
@@ -88,13 +89,10 @@ struct subspace_crc_ctx {
   uint32_t poly = kPoly;  // reflected CRC polynomial of every table and operator below
   int num_cus = 256;
   u32* d_tab = nullptr;  // 4 x 256 slice tables
-  u32* d_rops = nullptr;  // ragged kernel: line-shift operators + Z_4096 + tile shifts (kRagOpWords)
+  u32* d_rops = nullptr;  // ragged kernel: line-shift operators, Z_4096, tile shifts, padding inverses
   u32* d_pow2 = nullptr;  // Z_{2^k}, k = 0..63, nibble operators (slot checksums)
   u32* d_laneops = nullptr;  // uniform kernel: Z_{128*s}, s = 0..31, as [nibble][value][s]
-  // zinv[r] = Z_r^{-1}(init), r = 0..127, cached per init value
-  std::unordered_map<u32, u32*> zinv;
   Tables host_tab;
-  Mat32 zinv1;  // Z_1^{-1}
   // ragged workspace
   u64* d_ntiles = nullptr;   // count + 1
   u64* d_tbase = nullptr;    // count + 1
@@ -142,26 +140,6 @@ struct subspace_crc_ctx {
 };
 
 namespace {
-
-int get_zinv(subspace_crc_ctx* c, u32 init, const u32** out) {
-  auto it = c->zinv.find(init);
-  if (it != c->zinv.end()) {
-    *out = it->second;
-    return SUBSPACE_CRC_OK;
-  }
-  u32 h[128];
-  u32 v = init;
-  for (int r = 0; r < 128; r++) {  // h[r] = Z_1^{-r}(init)
-    h[r] = v;
-    v = apply(c->zinv1, v);
-  }
-  u32* d = nullptr;
-  HIP_TRY(hipMalloc(&d, sizeof(h)));
-  HIP_TRY(hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice));
-  c->zinv.emplace(init, d);
-  *out = d;
-  return SUBSPACE_CRC_OK;
-}
 
 int ensure_ragged_ws(subspace_crc_ctx* c, u64 messages, u64 tiles) {
   if (messages > c->ws_messages) {
@@ -214,10 +192,7 @@ int grid_for(subspace_crc_ctx* c, u64 work_units, int waves_per_block) {
 // `cap` sizes the descriptor workspace; a batch with more tiles takes the search path.
 int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* offsets, u32 ostride, const u64* lengths,
                u32 lstride, u64 count, u32 init, u32 final_xor, u32* out, hipStream_t st) {
-  const u32* zinv;
-  int rc = get_zinv(c, init, &zinv);
-  if (rc) return rc;
-  rc = ensure_ragged_ws(c, count, cap);
+  int rc = ensure_ragged_ws(c, count, cap);
   if (rc) return rc;
   const u64 n1 = count + 1;
   crc32_ragged_count_kernel<<<(unsigned)((n1 + 255) / 256), 256, 0, st>>>(lengths, lstride, count, init, final_xor,
@@ -232,14 +207,15 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU
   crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, ragged_lds_bytes(), st>>>(
       base, offsets, ostride, lengths, lstride, c->d_tbase, count, reinterpret_cast<const TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_tab, c->d_rops, zinv, final_xor, out, c->d_tilecrc);
+      c->d_overflow, c->d_tab, c->d_rops, init, out, c->d_tilecrc);
   HIP_TRY(hipGetLastError());
-  // message CRC = XOR of its tiles' values = difference of two XOR-scan entries (entries
-  // past the batch's real tile count are scanned but never read)
+  // padded message CRC = XOR of its tiles' values = difference of two XOR-scan entries
+  // (entries past the batch's real tile count are scanned but never read); the final
+  // kernel undoes the last tile's zero padding and applies the final XOR
   size_t xtmp = c->xscan_tmp_bytes;
   HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, c->d_px, cap, st));
-  crc32_ragged_final_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(c->d_tbase, count, c->d_px,
-                                                                              c->d_overflow, out);
+  crc32_ragged_final_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(
+      c->d_tbase, lengths, lstride, count, c->d_px, c->d_overflow, c->d_rops, final_xor, out);
   HIP_TRY(hipGetLastError());
   return SUBSPACE_CRC_OK;
 }
@@ -308,7 +284,6 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   c->num_cus = prop.multiProcessorCount;
   c->poly = poly;
   c->host_tab = make_tables(poly);
-  c->zinv1 = inverse(z_one(c->host_tab));
 
   std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kLaneOpWords, 0u), rops(kRagOpWords, 0u);
   for (int k = 0; k < 4; k++)
@@ -329,6 +304,9 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   std::copy(laneops.begin(), laneops.end(), rops.begin());
   nibble_tables(z_bytes(c->host_tab, 4096), &rops[kLaneOpWords]);
   for (int k = 0; k < 31; k++) nibble_tables(z_bytes(c->host_tab, 8192ull << k), &rops[kLaneOpWords + 128 * (1 + k)]);
+  // the ragged final kernel's padding inverses Z_{2^b}^{-1}, b = 0..12
+  for (int b = 0; b < kNumInvOps; b++)
+    nibble_tables(inverse(z_bytes(c->host_tab, 1ull << b)), &rops[kRagInvOps + 128 * b]);
 
   hipError_t e = hipMalloc(&c->d_tab, tab.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_laneops, laneops.size() * 4);
@@ -384,7 +362,6 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_laneops);
   (void)hipFree(c->d_crc0);
   (void)hipFree(c->d_soff);
-  for (auto& kv : c->zinv) (void)hipFree(kv.second);
   (void)hipFree(c->d_ntiles);
   (void)hipFree(c->d_tbase);
   (void)hipFree(c->d_scan_tmp);
@@ -402,9 +379,6 @@ int subspace_crc_ctx_reserve(subspace_crc_ctx* c, uint64_t max_messages, uint64_
   g_err[0] = 0;
   if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
   HIP_TRY(hipSetDevice(c->device));
-  const u32* z;
-  int rc = get_zinv(c, 0xFFFFFFFFu, &z);
-  if (rc) return rc;
   return ensure_ragged_ws(c, max_messages, max_tiles);
 }
 

@@ -37,15 +37,17 @@ constexpr size_t uniform_lds_bytes(int waves) { return kUniRing + (size_t)waves 
 
 // Ragged-kernel layout: tables, the same line-shift operators, then opmul slots Z_4096 and
 // Z_{8192 * 2^k}, k = 0..20 (8 KiB .. 8 GiB). The device operator array continues with
-// Z_{8192 * 2^k}, k = 21..30, read from global memory (messages of 16 GiB and more).
+// Z_{8192 * 2^k}, k = 21..30, read from global memory (messages of 16 GiB and more), and
+// the padding inverses Z_{2^b}^{-1}, b = 0..12, of the ragged final kernel.
 constexpr int kNumTileOps = 21;
 constexpr int kRagOpZ4096 = kLaneOpWords * 4 / 512;  // opmul slot 32
 constexpr int kRagOpZTile = kRagOpZ4096 + 1;
 constexpr int kRagLdsOpWords = kLaneOpWords + (1 + kNumTileOps) * 128;
 constexpr int kRagHighOps = kRagLdsOpWords;  // word offset of Z_{8192 * 2^21} in the device array
-constexpr int kRagOpWords = kRagLdsOpWords + (31 - kNumTileOps) * 128;
-constexpr u32 kRagZinv = kLdsOps + (u32)kRagLdsOpWords * 4u;  // then zinv[0..127] of the batch's init
-constexpr size_t ragged_lds_bytes() { return kRagZinv + 128u * 4u; }
+constexpr int kNumInvOps = 13;
+constexpr int kRagInvOps = kRagHighOps + (31 - kNumTileOps) * 128;  // word offset of Z_1^{-1}
+constexpr int kRagOpWords = kRagInvOps + kNumInvOps * 128;
+constexpr size_t ragged_lds_bytes() { return kLdsOps + (size_t)kRagLdsOpWords * 4u; }
 static_assert(ragged_lds_bytes() <= 160u * 1024u, "ragged kernel LDS exceeds 160 KiB");
 
 typedef __attribute__((address_space(3))) u32 lds_u32_t;

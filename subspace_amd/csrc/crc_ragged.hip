@@ -2,16 +2,19 @@
 // alignment (BASELINE configs C and D; any subspace_crc32_batch call).
 //
 // Decomposition (DESIGN.md "Ragged kernel"):
-//  * Message m = bytes [s, e). Its n = ceil(L/128) "virtual lines" are aligned to the
-//    message END: line g covers [e - 128(n-g), e - 128(n-1-g)). Only line 0 can start
-//    before s; its r = 128n - L leading bytes are zero-masked and its lane starts from
-//    zinv[r] = Z_r^{-1}(init), so after the r zero bytes the state is exactly init:
-//      crc_raw(zinv[r], 0^r || D) = crc_raw(init, D).
-//    Every line is a full 128-byte unit, so the combine is uniform:
-//      crc(m) = XOR_g Z_{128(n-1-g)}(line_g)                       (linearity)
-//  * A tile is 64 consecutive virtual lines of ONE message (end-aligned, so only a
-//    message's first tile is partial). Lane i <-> line i of the tile, exactly like the
-//    uniform kernel: 64 consecutive 128-B lines per wave load instruction.
+//  * Message m = bytes [s, e), L = e - s. Its nt = ceil(L/8192) tiles are aligned to the
+//    message START: tile j covers [s + 8192j, s + 8192(j+1)), and only the last tile can
+//    be short (len = L - 8192(nt-1) bytes). Lane l of a tile owns the 128-B line
+//    [s + 8192j + 128l, +128): 64 consecutive lines per wave load instruction, exactly like
+//    the uniform kernel. Line 0 of tile 0 starts from `init`, every other line from 0.
+//  * The last tile is read as if it were zero-padded to 8 KiB: its bytes at and past e are
+//    zero-masked. The tiles then compute the padded message's CRC,
+//      crc_raw(init, D || 0^p) = Z_p(crc_raw(init, D)),        p = 8192*nt - L < 8192,
+//    and the final kernel undoes the padding with p's binary decomposition over the
+//    inverse operators Z_{2^b}^{-1} (b = 0..12; Z_n is invertible since P has an x^0 term)
+//    before the final XOR. Leading data needs no seed or mask, and a message whose start
+//    is 16-B aligned (packed arenas, slot payloads) needs no realignment at all: its
+//    lines are whole aligned 16-B blocks, whatever its length.
 //  * Waves stream the global tile list in sweep order (tau = k*nw + w), one tile of
 //    loads in flight ahead. Per-tile 16-B descriptors (tile end, tiles after, first-tile
 //    flag, message start offset in the first tile) are precomputed by
@@ -22,18 +25,19 @@
 //    lane, in registers (lane k&63 keeps tile k); every 64 tiles each lane finishes its own tile,
 //      tile value = Z_{8192*T}( Z_4096(half0) ^ half1 )     (T = tiles after it)
 //    with a per-lane binary decomposition of T over nibble operators -- one wave pass
-//    shifts 64 tiles -- and stores tilecrc[tau]. A message's CRC is the XOR of its tiles'
-//    values, i.e. the difference of two entries of the inclusive XOR-scan of tilecrc
-//    (crc32_ragged_final_kernel). No atomics: huge messages (config D: 8192 tiles each,
-//    all in flight at once) would otherwise serialise every tile on one output word.
+//    shifts 64 tiles -- and stores tilecrc[tau]. A message's padded CRC is the XOR of its
+//    tiles' values, i.e. the difference of two entries of the inclusive XOR-scan of
+//    tilecrc (crc32_ragged_final_kernel). No atomics: huge messages (config D: 8192 tiles
+//    each, all in flight at once) would otherwise serialise every tile on one output word.
 //    (Batches whose tiles overflow the workspace -- overlapping messages -- fall back to
 //    atomicXor into pre-zeroed words.)
-//  * End-aligned lines are 16-B misaligned when e is. Each lane loads the 8 aligned 16-B
-//    blocks starting at or below its line; the line's last e&15 bytes sit in the next
-//    lane's first block, which arrives by a DPP wave shift, and for lane 63 in the tile's
-//    last (partial) block, one load shared by the whole wave. The words are realigned
-//    with v_alignbyte_b32 (the dword shift (e&15)>>2 is wave-uniform: a 4-way uniform
-//    switch). Loads never touch a 16-B block that holds no message byte.
+//  * A message start that is not 16-B aligned makes every line misaligned by mis = s & 15
+//    (wave-uniform per tile). Each lane then loads the 8 aligned 16-B blocks starting at or
+//    below its line; the line's last mis bytes sit in the next lane's first block, which
+//    arrives by a DPP wave shift, and for lane 63 in the block after the tile, one load
+//    shared by the whole wave. The words are realigned with v_alignbyte_b32 (the dword
+//    shift mis>>2 is wave-uniform: a 4-way uniform switch). Loads never touch a 16-B block
+//    that holds no byte of the message.
 #include <hipcub/hipcub.hpp>
 
 #include "crc_device.h"
@@ -42,17 +46,17 @@ namespace subspace_amd {
 
 // 16 B per tile: one vector load and four readfirstlanes per tile in the main kernel.
 struct TileDesc {
-  u64 tile_end;  // absolute offset (from base) one past the tile's last byte
-  u32 after;     // tiles after this one in the message | kFirstTile for its first tile
-  u32 lead;      // first tile: message start - tile start (0..8191), else 0
+  u64 tile_start;  // absolute offset (from base) of the tile's first byte
+  u32 after;       // tiles after this one in the message | kFirstTile for its first tile
+  u32 len;         // message bytes in the tile: 8192, or 1..8192 for the last tile
 };
 static_assert(sizeof(TileDesc) == 16, "TileDesc is 16 B");
 constexpr u32 kFirstTile = 0x80000000u;
 
 __host__ __device__ inline u64 tiles_for_length(u64 len) { return (len + 8191) >> 13; }
 
-// Per message: tile count; zero-length messages get their (constant) result here,
-// multi-tile messages get their output word zeroed for the tiles' atomicXor.
+// Per message: tile count; zero-length messages get their (constant) result here, every
+// other output word is zeroed (the overflow path XORs tile values into it).
 // `lengths` (and `offsets` below) are read with an element stride (1 for plain arrays, 3 for
 // the lengths/payload fields of subspace_crc_slot records).
 __global__ void crc32_ragged_count_kernel(const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
@@ -63,11 +67,9 @@ __global__ void crc32_ragged_count_kernel(const u64* __restrict__ lengths, u32 l
     ntiles[i] = 0;  // scan sentinel: tile_base[count] = total tiles
     return;
   }
-  const u64 len = lengths[i * lstride];
-  const u64 nt = tiles_for_length(len);
+  const u64 nt = tiles_for_length(lengths[i * lstride]);
   ntiles[i] = nt;
-  if (nt == 0) out[i] = init ^ final_xor;
-  else if (nt > 1) out[i] = 0u;
+  out[i] = nt == 0 ? init ^ final_xor : 0u;
 }
 
 __device__ inline u64 find_msg(const u64* __restrict__ tile_base, u64 count, u64 tau) {
@@ -85,15 +87,11 @@ __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, u32 ostrid
                                      u32 lstride, const u64* __restrict__ tile_base, u64 m, u64 tau) {
   const u64 nt = tile_base[m + 1] - tile_base[m];
   const u64 j = tau - tile_base[m];
-  const u64 s = offsets[m * ostride];
-  const u64 e = s + lengths[m * lstride];
+  const u64 rest = lengths[m * lstride] - (j << 13);  // message bytes from the tile start on
   TileDesc d;
-  d.tile_end = e - ((nt - 1 - j) << 13);
+  d.tile_start = offsets[m * ostride] + (j << 13);
   d.after = (u32)(nt - 1 - j) | (j == 0 ? kFirstTile : 0u);
-  // first tile: the message starts `lead` bytes into it; the line holding byte s is line
-  // lead >> 7 and starts r = lead & 127 bytes before s (lines are end-aligned), so its lane
-  // starts from zinv[r]
-  d.lead = j == 0 ? (u32)((i64)s - ((i64)d.tile_end - 8192)) : 0u;
+  d.len = rest < 8192 ? (u32)rest : 8192u;
   return d;
 }
 
@@ -112,7 +110,7 @@ __global__ void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, u32 os
 // ------------------------------------------------------------------ main kernel
 struct LineState {
   u32x4 d[8];  // the 8 aligned 16-B blocks starting at or below the lane's line
-  u32x4 x;     // the tile's last aligned block (the same for every lane)
+  u32x4 x;     // the block after the tile (the same for every lane)
 };
 
 template <int Q>
@@ -135,7 +133,7 @@ __device__ __forceinline__ u32 crc_line(const u32x4 (&d)[9], u32 crc, u32 m3, u3
 }
 
 // Nibble operator read from global memory (the tile-shift operators for 2^21 tiles and
-// more, which only messages of 16 GiB and more need).
+// more, which only messages of 16 GiB and more need; the padding inverses).
 __device__ __forceinline__ u32 opmul_global(const u32* __restrict__ op, u32 v) {
   u32 r = op[v & 15u];
 #pragma unroll
@@ -148,15 +146,13 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
                                             u32 ostride, const u64* __restrict__ lengths, u32 lstride,
                                             const u64* __restrict__ tile_base, u64 count,
                                             const TileDesc* __restrict__ desc, const u32* __restrict__ gtab,
-                                            const u32* __restrict__ gops, const u32* __restrict__ zinv,
-                                            u32 final_xor, u32* __restrict__ out, u32* __restrict__ tilecrc,
-                                            u32 sbase) {
+                                            const u32* __restrict__ gops, u32 init, u32* __restrict__ out,
+                                            u32* __restrict__ tilecrc, u32 sbase) {
   const int lane = threadIdx.x & 63;
   const u32 wid = rfl(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
   const u32 lop = sbase + kLdsOps + 4u * (u32)(31 - (lane & 31));  // this lane's line-shift operator
-  const u32 zsb = sbase + kRagZinv;  // zinv[r], r = 0..127 (first-line seeds of this batch's init)
   const u64 total = tile_base[count];
   const u64 w = front_slot(blockIdx.x, gridDim.x, wid);  // sweep front slot (crc_device.h)
   const u64 nw = (u64)gridDim.x * (WG / 64);
@@ -179,43 +175,38 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
     } else {
       const u64 m = find_msg(tile_base, count, tau);
       const TileDesc t = make_desc(offsets, ostride, lengths, lstride, tile_base, m, tau);
-      d = u32x4{(u32)t.tile_end, (u32)(t.tile_end >> 32), t.after, t.lead};
+      d = u32x4{(u32)t.tile_start, (u32)(t.tile_start >> 32), t.after, t.len};
       dm = (u32)m;
     }
   };
   auto unpack = [&](const u32x4& d) {
     TileDesc t;
-    t.tile_end = rfl64(d[0], d[1]);
+    t.tile_start = rfl64(d[0], d[1]);
     t.after = rfl(d[2]);
-    t.lead = rfl(d[3]);
+    t.len = rfl(d[3]);
     return t;
   };
   // Issue the loads of tile d, as buffer loads against a scalar resource spanning exactly
-  // the tile's blocks that hold message bytes:
-  //   [max(aligned tile start, aligned message start), tile end rounded up to 16).
-  // Lane l loads the 8 blocks from a - 128*(64-l) (a = tile end rounded down to 16); blocks
-  // before the range start (before the message) read as zeros without touching memory (a
-  // per-lane offset below the start wraps to a huge value), so every lane issues every
-  // load (no divergent branch around loads). The 9th load is the same for all lanes: the
-  // tile's last block [a, a+16) when the end is misaligned (it is inside the range), else
-  // the dummy [a-16, a). `live` false (a prefetch past the wave's last tile) gives an
-  // empty range.
+  // the 16-B blocks that hold the tile's bytes:
+  //   [tile start rounded down to 16, tile end rounded up to 16).
+  // Lane l loads the 8 blocks from 128*l; blocks past the range (past the message end)
+  // read as zeros without touching memory, so every lane issues every load (no divergent
+  // branch around loads). The 9th load is the same for all lanes: the block at 8192, which
+  // holds the tile's last bytes when its start is misaligned (in range then), else it is
+  // out of range (zeros, no access). `live` false (a prefetch past the wave's last tile)
+  // gives an empty range.
   auto load_line = [&](const TileDesc& d, LineState& L, bool live) {
-    const i64 tile_start = (i64)d.tile_end - 8192;
-    const i64 t0a = tile_start & ~(i64)15;
-    const i64 rb = (d.after & kFirstTile) ? ((tile_start + (i64)d.lead) & ~(i64)15) : t0a;
-    const i64 a = (i64)d.tile_end & ~(i64)15;
-    const i64 rend = ((i64)d.tile_end + 15) & ~(i64)15;
-    const u32 nrec = live ? (u32)(rend - rb) : 0u;
-    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + rb), (short)0, (int)nrec,
+    const u64 t0a = d.tile_start & ~(u64)15;
+    const u64 rend = (d.tile_start + d.len + 15) & ~(u64)15;
+    const u32 nrec = live ? (u32)(rend - t0a) : 0u;
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + t0a), (short)0, (int)nrec,
                                                      kBufferRsrcFlags);
-    const u32 vo = (u32)lane * 128u - (u32)(rb - t0a);
+    const u32 vo = (u32)lane * 128u;
 #pragma unroll
     for (int b = 0; b < 8; b++) L.d[b] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16u * b, 0, 0);
     // the shared block's offset goes in the VGPR (not the scalar offset), so the range
     // check sees it whichever offsets the hardware includes
-    const u32 xo = vzero + (u32)((rend > a ? a : a - 16) - rb);
-    L.x = __builtin_amdgcn_raw_buffer_load_b128(r, xo, 0, 0);
+    L.x = __builtin_amdgcn_raw_buffer_load_b128(r, vzero + 8192u, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -224,7 +215,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
 
   auto process = [&](const LineState& cur, const TileDesc& dcur, u32 dm, u64 k) {
     const bool first = (dcur.after & kFirstTile) != 0;  // wave-uniform, like everything below
-    const u32 mis = (u32)(dcur.tile_end & 15);
+    const u32 mis = (u32)(dcur.tile_start & 15);
     u32x4 d[9];
 #pragma unroll
     for (int b = 0; b < 8; b++) d[b] = cur.d[b];
@@ -235,31 +226,26 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
     } else {
       d[8] = u32x4{0u, 0u, 0u, 0u};
     }
-    u32 crc = 0;
-    if (first) {
-      // The message starts `lead` bytes into the tile: zero every byte of each lane's 144-B
-      // window below it (the window starts lead + mis - 128*lane bytes before the message),
-      // and start the lane holding the first byte from zinv[lead & 127]. Lanes wholly
-      // before the message then compute crc_raw(0, zeros) = 0.
-      const u32 lead = dcur.lead;
-      if (lead) {
-        const int zb0 = (int)(lead + mis) - 128 * lane;
-        const u32 zb = zb0 <= 0 ? 0u : (zb0 >= 144 ? 144u : (u32)zb0);
+    // A short last tile whose end is not 16-B aligned: its last loaded block also holds
+    // bytes past the message; zero every byte of each lane's 144-B window from the
+    // message end on (the lane's line is window bytes [mis, mis + 128), and its first
+    // `valid` bytes are message bytes), so the tile reads as zero-padded.
+    if (dcur.len < 8192u && ((u32)(dcur.tile_start + dcur.len) & 15u)) {
+      const int v0 = (int)dcur.len - 128 * lane;
+      const u32 zb = mis + (v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0));  // keep window bytes < zb
 #pragma unroll
-        for (int b = 0; b < 9; b++) {
+      for (int b = 0; b < 9; b++) {
 #pragma unroll
-          for (int x = 0; x < 4; x++) {
-            const u32 p = 16u * b + 4u * x;
-            u32 keep = 0xFFFFFFFFu;
-            if (p + 4u <= zb) keep = 0;
-            else if (p < zb) keep = 0xFFFFFFFFu << (8u * (zb - p));
-            d[b][x] &= keep;
-          }
+        for (int x = 0; x < 4; x++) {
+          const u32 p = 16u * b + 4u * x;
+          u32 keep = 0u;
+          if (p + 4u <= zb) keep = 0xFFFFFFFFu;
+          else if (p < zb) keep = 0xFFFFFFFFu >> (8u * (p + 4u - zb));
+          d[b][x] &= keep;
         }
       }
-      const u32 seed = lds_ld(zsb + 4u * (lead & 127u));
-      crc = (u32)lane == (lead >> 7) ? seed : 0u;
     }
+    u32 crc = (first && lane == 0) ? init : 0u;
     const u32 m3 = mis & 3;
     switch (mis >> 2) {
       case 0: crc = mis ? crc_line<0, true>(d, crc, m3, lc0, lc1) : crc_line<0, false>(d, crc, m3, lc0, lc1); break;
@@ -290,7 +276,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   auto flush = [&](u64 kf, u32 nt) {
     const bool valid = (u32)lane < nt;
     u32 c = opmul(sbase, kRagOpZ4096, H0) ^ H1;  // the tile's 8 KiB from its two halves
-    u32 rem = valid ? (AF & ~kFirstTile) : 0u;   // shift to the message end: Z_{8192 * after}
+    u32 rem = valid ? (AF & ~kFirstTile) : 0u;   // shift to the (padded) message end: Z_{8192 * after}
     int bit = 0;
     for (; bit < kNumTileOps && __any(rem != 0u); bit++) {
       const u32 cm = opmul(sbase, kRagOpZTile + bit, c);
@@ -302,15 +288,9 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
       c = (rem & 1u) ? cm : c;
       rem >>= 1;
     }
-    if (AF & kFirstTile) c ^= final_xor;
     if (valid) {
-      if (DESC) {
-        tilecrc[(kf + (u64)lane) * nw + w] = c;
-      } else if (AF == kFirstTile) {
-        out[MG] = c;  // single-tile message
-      } else {
-        atomicXor(&out[MG], c);
-      }
+      if (DESC) tilecrc[(kf + (u64)lane) * nw + w] = c;
+      else atomicXor(&out[MG], c);
     }
   };
 
@@ -318,7 +298,6 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   // stores and the barrier (tile 0's latency hides behind the fill).
   LdsFill<WG, kRagLdsOpWords / 128> fill;
   fill.load(gtab, gops);
-  const u32 zv = zinv[threadIdx.x & 127];  // unconditional (a load in a branch drains vmcnt)
   u32x4 dA, dB;
   u32 mA, mB;
   fetch_desc(0, dA, mA);
@@ -328,8 +307,6 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   LineState A, B;
   load_line(dcur, A, nk != 0);
   fill.store(sbase);
-  if (threadIdx.x < 128) lds_st(zsb + 4u * threadIdx.x, zv);
-  asm volatile("" ::"v"(zv));
   __syncthreads();
   if (nk == 0) return;
 
@@ -369,34 +346,42 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
                                                           const TileDesc* __restrict__ desc,
                                                           const u32* __restrict__ overflow,
                                                           const u32* __restrict__ gtab, const u32* __restrict__ gops,
-                                                          const u32* __restrict__ zinv, u32 final_xor,
-                                                          u32* __restrict__ out, u32* __restrict__ tilecrc) {
+                                                          u32 init, u32* __restrict__ out,
+                                                          u32* __restrict__ tilecrc) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
   // Precomputed descriptors unless the batch had more tiles than the workspace holds
   // (overlapping messages); then every tile is located by binary search.
   if (*overflow == 0u)
-    ragged_body<WG, true>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, zinv,
-                          final_xor, out, tilecrc, sbase);
+    ragged_body<WG, true>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, init, out,
+                          tilecrc, sbase);
   else
-    ragged_body<WG, false>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, zinv,
-                           final_xor, out, tilecrc, sbase);
+    ragged_body<WG, false>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, init, out,
+                           tilecrc, sbase);
 }
 
 template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
-                                                  const TileDesc*, const u32*, const u32*, const u32*, const u32*,
-                                                  u32, u32*, u32*);
+                                                  const TileDesc*, const u32*, const u32*, const u32*, u32, u32*,
+                                                  u32*);
 
-// Per message with tiles: out[m] = XOR of its tiles' values = px[last] ^ px[first - 1],
-// px = inclusive XOR-scan of tilecrc. Skipped when the batch overflowed the workspace
-// (those results were produced with atomics).
-__global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, u64 count, const u32* __restrict__ px,
-                                          const u32* __restrict__ overflow, u32* __restrict__ out) {
+// Per message with tiles: its padded CRC = XOR of its tiles' values = px[last] ^
+// px[first - 1] (px = inclusive XOR-scan of tilecrc), or the XOR the overflow path
+// accumulated in out[m]; then the padding undone -- Z_p^{-1} for p = (-L) mod 8192, as
+// p's bits over the inverse operators Z_{2^b}^{-1} -- and the final XOR applied.
+__global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, const u64* __restrict__ lengths,
+                                          u32 lstride, u64 count, const u32* __restrict__ px,
+                                          const u32* __restrict__ overflow, const u32* __restrict__ gops,
+                                          u32 final_xor, u32* __restrict__ out) {
   const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= count || *overflow) return;
+  if (m >= count) return;
   const u64 t0 = tile_base[m], t1 = tile_base[m + 1];
   if (t1 == t0) return;  // empty message: written by the count kernel
-  out[m] = px[t1 - 1] ^ (t0 ? px[t0 - 1] : 0u);
+  u32 v = *overflow ? out[m] : px[t1 - 1] ^ (t0 ? px[t0 - 1] : 0u);
+  const u32 pad = (u32)(0 - lengths[m * lstride]) & 8191u;
+#pragma unroll 1
+  for (int b = 0; b < kNumInvOps; b++)
+    if ((pad >> b) & 1u) v = opmul_global(gops + kRagInvOps + 128 * b, v);
+  out[m] = v ^ final_xor;
 }
 
 // hipcub scan wrappers: exclusive prefix sum of per-message tile counts; inclusive XOR

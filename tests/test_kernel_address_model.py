@@ -14,41 +14,36 @@ def tiles_for_length(n):
 
 def ragged_loads(s, e):
     """For message [s, e): (tile j, lane, block, address or None) for every load of
-    load_line -- buffer loads against the range [rb, rend), offsets are 32-bit (wrapping);
-    an offset >= the range size reads zeros without a memory access (None). Blocks 0..7
-    are the lane's own; block 8 is the load shared by the wave (same address in every
-    lane): the tile's last block [a, a+16) if the end is misaligned, else [a-16, a)."""
+    load_line. Tiles are aligned to the message start (tile j starts at ts = s + 8192j and
+    holds min(8192, e - ts) bytes); loads are buffer loads against the range [t0a, rend) =
+    [ts rounded down, tile end rounded up to 16 B), and an offset >= the range size reads
+    zeros without a memory access (None). Blocks 0..7 are the lane's own (offsets 128*lane
+    + 16*b); block 8 is the load shared by the wave, at offset 8192."""
     n = e - s
     nt = tiles_for_length(n)
     for j in range(nt):
-        tile_end = e - ((nt - 1 - j) << 13)
-        t0a = (tile_end - 8192) & ~15
-        sa = s & ~15
-        rb = max(t0a, sa)
-        a = tile_end & ~15
-        rend = (tile_end + 15) & ~15
-        nrec = rend - rb
-        xo = ((a if rend > a else a - 16) - rb) % M32
+        ts = s + (j << 13)
+        ln = min(8192, e - ts)
+        t0a = ts & ~15
+        nrec = ((ts + ln + 15) & ~15) - t0a
         for lane in range(64):
-            vo = (lane * 128 - (rb - t0a)) % M32
             for b in range(8):
-                off = (vo + 16 * b) % M32
-                yield j, lane, b, (rb + off if off < nrec else None)
-            yield j, lane, 8, (rb + xo if xo < nrec else None)
+                off = lane * 128 + 16 * b
+                yield j, lane, b, (t0a + off if off < nrec else None)
+            yield j, lane, 8, (t0a + 8192 if 8192 < nrec else None)
 
 
 def ragged_line_window(s, e, j, lane):
     """The 9 blocks process() realigns for (tile j, lane): its own 8, then lane+1's block
-    0 (DPP wave_shl:1) or, for lane 63, the shared block (zeros when the tile end is
+    0 (DPP wave_shl:1) or, for lane 63, the shared block (zeros when the message start is
     16-B aligned) -- as addresses (None = zeros)."""
     loads = {}
     for jj, ln, b, addr in ragged_loads(s, e):
         if jj == j:
             loads[(ln, b)] = addr
     own = [loads[(lane, b)] for b in range(8)]
-    nt = tiles_for_length(e - s)
-    if ((e - ((nt - 1 - j) << 13)) & 15) == 0:
-        return own + [None]  # aligned tile end: the 9th block is not used (zeros)
+    if (s & 15) == 0:
+        return own + [None]  # aligned start: the 9th block is not used (zeros)
     nxt = loads[(lane + 1, 0)] if lane < 63 else loads[(63, 8)]
     return own + [nxt]
 
@@ -72,18 +67,17 @@ def test_every_ragged_load_stays_in_its_message_blocks(seed):
 @pytest.mark.parametrize("s,n", [(0, 1), (3, 100), (17, 8192), (5, 8193), (0, 4096), (1, 65536 + 7), (15, 24577),
                                  (64, 16384 + 9), (7, 8192 * 3)])
 def test_ragged_line_windows_hold_each_line(s, n):
-    """Every lane's realigned 128-B line [E - 128(64-l), +128) is read from its 9-block
-    window: blocks at consecutive 16-B steps from the aligned start, the 9th through the
-    wave shift -- and every message byte of the line comes from a real load."""
+    """Every lane's realigned 128-B line [ts + 128l, +128) is read from its 9-block window:
+    blocks at consecutive 16-B steps from the aligned start, the 9th through the wave
+    shift -- and every message byte of the line comes from a real load."""
     e = s + n
     nt = tiles_for_length(n)
     for j in range(nt):
-        tile_end = e - ((nt - 1 - j) << 13)
-        a = tile_end & ~15
+        ts = s + (j << 13)
         for lane in range(64):
             win = ragged_line_window(s, e, j, lane)
-            base = a - 128 * (64 - lane)
-            line = range(tile_end - 128 * (64 - lane), tile_end - 128 * (63 - lane))
+            base = (ts & ~15) + 128 * lane
+            line = range(ts + 128 * lane, ts + 128 * lane + 128)
             for b, addr in enumerate(win):
                 if addr is not None:
                     assert addr == base + 16 * b, (s, n, j, lane, b)

@@ -1,7 +1,7 @@
 """CPU model of the kernels' CRC decomposition (the algebra, not the HIP code):
-the ragged kernel's end-aligned virtual lines, zero-masked first line seeded with
-zinv[r], per-lane line-shift operators + DPP half reduction, Z_4096 join, Z_{8192*T}
-shift and XOR combine; the uniform kernel's per-line
+the ragged kernel's start-aligned tiles with a zero-padded last tile, per-lane line-shift
+operators + DPP half reduction, Z_4096 join, Z_{8192*T} shift, XOR combine and the
+padding undone with Z_{2^b}^{-1}; the uniform kernel's per-line
 CRCs and transposed tree. Each must equal the reference CRC (zlib) bit for bit."""
 import zlib
 
@@ -67,7 +67,7 @@ def inverse(m):
     return [sum(((inv[r] >> c) & 1) << r for r in range(32)) for c in range(32)]
 
 
-ZINV1 = inverse(Z1)
+ZINV_POW2 = [inverse(zbytes(1 << b)) for b in range(13)]  # the final kernel's padding inverses
 ZTREE = [zbytes(128 << k) for k in range(6)]
 ZTILE = [zbytes(8192 << k) for k in range(8)]
 LANE_OPS = [zbytes(128 * sl) for sl in range(32)]
@@ -78,31 +78,20 @@ def ragged_model(buf: bytes, s: int, L: int, init: int) -> int:
     e = s + L
     if L == 0:
         return init
-    zinv = []
-    v = init
-    for _ in range(128):
-        zinv.append(v)
-        v = apply(ZINV1, v)
     nt = (L + 8191) >> 13
     out = 0
     for j in range(nt):
-        tile_end = e - ((nt - 1 - j) << 13)
-        tile_start = tile_end - 8192
+        ts = s + (j << 13)  # tiles are aligned to the message start
         lines = []
         for lane in range(64):
-            ls = tile_start + 128 * lane
-            if ls + 128 <= s:
-                lines.append(0)
-                continue
-            data = bytes(buf[max(ls, 0):ls + 128]) if ls >= 0 else bytes(-ls) + bytes(buf[0:ls + 128])
-            data = bytearray(data)
-            for i in range(128):  # zero bytes below the message start
-                if ls + i < s:
-                    data[i] = 0
-            seed = zinv[s - ls] if ls <= s else 0
-            lines.append(crc_raw(seed, data))
+            ls = ts + 128 * lane
+            data = bytearray(128)  # bytes past the message end stay zero (padded last tile)
+            for i in range(128):
+                if ls + i < e:
+                    data[i] = buf[ls + i]
+            lines.append(crc_raw(init if (j == 0 and lane == 0) else 0, bytes(data)))
         # per lane: Z_{128*(31 - l%32)} on its line; XOR over each half (DPP); the halves
-        # joined with Z_4096; then the shift to the message end, Z_{8192*T}
+        # joined with Z_4096; then the shift to the padded message end, Z_{8192*T}
         shifted = [apply(LANE_OPS[31 - (lane & 31)], lines[lane]) for lane in range(64)]
         red = dpp_half_xor(shifted)
         t = apply(Z4096, red[31]) ^ red[63]
@@ -114,6 +103,11 @@ def ragged_model(buf: bytes, s: int, L: int, init: int) -> int:
             after >>= 1
             k += 1
         out ^= t
+    # out = crc_raw(init, D || 0^p) = Z_p(crc_raw(init, D)), p = 8192*nt - L: undo the padding
+    pad = (-L) % 8192
+    for b in range(13):
+        if (pad >> b) & 1:
+            out = apply(ZINV_POW2[b], out)
     return out
 
 

@@ -74,16 +74,19 @@ def main():
     dev = torch.device("cuda", 0)
     ctx = gpu.CrcContext(0)
     for cfg in args.configs.split(","):
-        if cfg in ("C", "Cu"):
+        if cfg in ("C", "Cu", "C16"):
             lengths = synth.ragged_lengths(synth.SEED_C, GOLD["C"]["count"])
+            if cfg == "C16":  # probe (no fixture): every message end 16-B aligned
+                lengths = lengths & ~np.uint64(15)
             offsets, total = synth.packed_offsets(lengths, 1 if cfg == "Cu" else 64)
             buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
             d_off, d_len = u64t(offsets, dev), u64t(lengths, dev)
             gpu.fill_ragged(buf, d_off, d_len, seed=synth.SEED_C)
             out = torch.empty(len(lengths), dtype=torch.int32, device=dev)
             ms = timed(lambda: ctx.crc32_ragged(buf, d_off, d_len, out), args.iters)
-            report("C" + (" unaligned" if cfg == "Cu" else ""), int(lengths.sum()), ms,
-                   out.cpu().numpy().view(np.uint32), "C", {"messages": len(lengths)})
+            name = {"C": "C", "Cu": "C unaligned", "C16": "C, lengths rounded to 16 B (probe)"}[cfg]
+            report(name, int(lengths.sum()), ms, out.cpu().numpy().view(np.uint32), "C" if cfg != "C16" else None,
+                   {"messages": len(lengths)})
             del buf, d_off, d_len, out
         elif cfg == "D":
             n, L = GOLD["D"]["count"], 64 << 20
