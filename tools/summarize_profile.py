@@ -42,6 +42,21 @@ def per_dispatch(pmc_dir: Path, counter: str):
     return by_kernel
 
 
+def timed_launches(trace: Path, name_part: str, k: int):
+    """(average duration us, start-to-start interval us, n) over the last k dispatches of
+    the kernel whose name contains name_part, from a --kernel-trace CSV."""
+    if not trace.exists():
+        return None
+    rows = [r for r in csv.DictReader(open(trace)) if name_part in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    last = rows[-k:]
+    if len(last) < 2:
+        return None
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last]
+    span = int(last[-1]["End_Timestamp"]) - int(last[0]["Start_Timestamp"])
+    return sum(durs) / len(durs) / 1e3, span / len(last) / 1e3, len(last)
+
+
 def main():
     sess, tag = Path(sys.argv[1]), sys.argv[2]
     out = ROOT / "profiles" / tag
@@ -58,6 +73,14 @@ def main():
     for r in rows:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
                      f"{float(r['MinNs']) / 1e3:.2f} | {float(r['MaxNs']) / 1e3:.2f} |")
+    timed = timed_launches(sess / "prof" / "run_kernel_trace.csv", "crc32_uniform4k_kernel", 1000)
+    if timed:
+        avg, per, n = timed
+        lines += ["", f"bench.py's timed region = the last {n} dispatches of the uniform kernel (the earlier "
+                  "ones are the settle and warm-up launches, which include the power-management ramp): "
+                  f"average kernel duration {avg:.2f} us, dispatch-to-dispatch interval {per:.2f} us "
+                  f"(= {65536 * 4096 / per / 1e3:.0f} GB/s of payload; bench.py's roofline.achieved uses the "
+                  "HIP-event span of the same region / K)."]
     lines += ["", "| kernel | dispatches | FETCH_SIZE KiB/launch (raw) | HBM read bytes/launch (x2, gfx950) | "
               "WRITE_SIZE KiB/launch |", "|---|---|---|---|---|"]
     traffic = {}
