@@ -8,7 +8,6 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
-#include <unordered_map>
 #include <vector>
 
 #include "../../include/subspace_crc.h"
@@ -25,17 +24,18 @@ __global__ void crc32_ragged_count_kernel(const u64*, u32, u64, u32, u32, u64*, 
 __global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, u64, u64, TileDesc*, u32*);
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
-                                    const TileDesc*, const u32*, const u32*, const u32*, u32, u32*, u32*);
+                                    const TileDesc*, const u32*, const u32*, const u32*, u32, u32*, u32*, u64);
 __global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, u64, const u32*, const u32*, const u32*, u32,
                                           u32*);
-hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u32* out, u64 n, hipStream_t stream);
+hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u64 nw, u64 nkmax, u32* out, u64 n,
+                    hipStream_t stream);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, int, int, u32, const u32*,
                                          const u32*, const u32*, u32*, u32*, u32*);
 __global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*);
 hipError_t ragged_scan(void* temp, size_t& temp_bytes, const u64* in, u64* out, u64 n, hipStream_t stream);
 __global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* offsets, u64* lengths);
 template <int WG>
-__global__ void crc32_long_kernel(const uint8_t*, u64, u32, u32, const u32*, const u32*, u32, u32, u32*);
+__global__ void crc32_long_kernel(const uint8_t*, u64, u32, u32, const u32*, const u32*, u32, u32, u32*, u32);
 __global__ void crc32_long_final_kernel(const u32*, u32, u32, u32*);
 
 }  // namespace subspace_amd
@@ -100,7 +100,7 @@ struct subspace_crc_ctx {
   size_t scan_tmp_bytes = 0;
   u64 ws_messages = 0;
   uint8_t* d_desc = nullptr;
-  u32* d_tilecrc = nullptr;  // per-tile values (desc_capacity)
+  u32* d_tilecrc = nullptr;  // per-tile values, wave-major (desc_capacity + one tile per wave)
   u32* d_px = nullptr;       // their inclusive XOR-scan
   void* d_xscan_tmp = nullptr;
   size_t xscan_tmp_bytes = 0;
@@ -168,10 +168,11 @@ int ensure_ragged_ws(subspace_crc_ctx* c, u64 messages, u64 tiles) {
     c->d_xscan_tmp = nullptr;
     c->desc_capacity = 0;
     HIP_TRY(hipMalloc(&c->d_desc, tiles * kTileDescBytes));
-    HIP_TRY(hipMalloc(&c->d_tilecrc, tiles * sizeof(u32)));
+    // wave-major: nw * ceil(tiles / nw) < tiles + nw entries (nw = waves of a persistent grid)
+    HIP_TRY(hipMalloc(&c->d_tilecrc, (tiles + (u64)c->num_cus * (kRaggedWG / 64)) * sizeof(u32)));
     HIP_TRY(hipMalloc(&c->d_px, tiles * sizeof(u32)));
     size_t tmp = 0;
-    HIP_TRY(xor_scan(nullptr, tmp, c->d_tilecrc, c->d_px, tiles, nullptr));
+    HIP_TRY(xor_scan(nullptr, tmp, c->d_tilecrc, 1, tiles, c->d_px, tiles, nullptr));
     HIP_TRY(hipMalloc(&c->d_xscan_tmp, tmp));
     c->xscan_tmp_bytes = tmp;
     c->desc_capacity = tiles;
@@ -205,15 +206,16 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
       c->d_overflow);
   HIP_TRY(hipGetLastError());
   const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU
+  const u64 nw = (u64)blocks * (kRaggedWG / 64), nkmax = (cap + nw - 1) / nw;  // wave-major tile values
   crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, ragged_lds_bytes(), st>>>(
       base, offsets, ostride, lengths, lstride, c->d_tbase, count, reinterpret_cast<const TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_tab, c->d_rops, init, out, c->d_tilecrc);
+      c->d_overflow, c->d_tab, c->d_rops, init, out, c->d_tilecrc, nkmax);
   HIP_TRY(hipGetLastError());
   // padded message CRC = XOR of its tiles' values = difference of two XOR-scan entries
   // (entries past the batch's real tile count are scanned but never read); the final
   // kernel undoes the last tile's zero padding and applies the final XOR
   size_t xtmp = c->xscan_tmp_bytes;
-  HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, c->d_px, cap, st));
+  HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, nw, nkmax, c->d_px, cap, st));
   crc32_ragged_final_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(
       c->d_tbase, lengths, lstride, count, c->d_px, c->d_overflow, c->d_rops, final_xor, out);
   HIP_TRY(hipGetLastError());
@@ -445,12 +447,13 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     const u64 tiles = pieces * count;
     int rc = ensure_ragged_ws(c, 0, tiles);
     if (rc) return rc;
+    const u64 nw = (u64)c->num_cus * (kRaggedWG / 64), nkmax = (tiles + nw - 1) / nw;
     crc32_long_kernel<kRaggedWG><<<c->num_cus, kRaggedWG, ragged_lds_bytes(), st>>>(
         static_cast<const uint8_t*>(dev_base), stride, (u32)pieces, (u32)count, c->d_tab, c->d_rops, init, final_xor,
-        c->d_tilecrc);
+        c->d_tilecrc, (u32)nkmax);
     HIP_TRY(hipGetLastError());
     size_t xtmp = c->xscan_tmp_bytes;
-    HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, c->d_px, tiles, st));
+    HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, nw, nkmax, c->d_px, tiles, st));
     crc32_long_final_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(c->d_px, (u32)pieces, (u32)count,
                                                                               dev_out);
     HIP_TRY(hipGetLastError());

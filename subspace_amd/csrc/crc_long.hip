@@ -14,9 +14,9 @@
 //  * combine exactly as crc_ragged.hip: per-lane line-shift operators Z_{128*(31-l)} and a
 //    DPP reduction give the two 4 KiB halves in lanes 31 and 63; tiles are parked one per
 //    lane and finished every 64 tiles: Z_{8192 * (P-1-j)}( Z_4096(h0) ^ h1 ), final XOR on
-//    the message's first piece, stored to tilecrc[tau];
+//    the message's first piece, stored to tilecrc wave-major (w * nkmax + k);
 //  * message m's CRC = XOR of its P values = px[(m+1)P - 1] ^ px[mP - 1] over the inclusive
-//    XOR-scan px of tilecrc (crc32_long_final_kernel).
+//    XOR-scan px of the values in tile order (crc_ragged.hip xor_scan; crc32_long_final_kernel).
 #include "crc_device.h"
 
 namespace subspace_amd {
@@ -25,7 +25,7 @@ template <int WG>
 __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restrict__ base, u64 stride, u32 pieces,
                                                         u32 count, const u32* __restrict__ gtab,
                                                         const u32* __restrict__ gops, u32 init, u32 final_xor,
-                                                        u32* __restrict__ tilecrc) {
+                                                        u32* __restrict__ tilecrc, u32 nkmax) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
   const int lane = threadIdx.x & 63;
@@ -80,10 +80,15 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
     const u32 h0 = (u32)__builtin_amdgcn_readlane((int)v, 31), h1 = (u32)__builtin_amdgcn_readlane((int)v, 63);
+#ifdef SUBSPACE_PROBE_NOPARK
+    H0 ^= h0 ^ h1;  // cost probe: no per-lane park (wrong results)
+    (void)k;
+#else
     const bool mine = lane == (int)(k & 63);
     H0 = mine ? h0 : H0;
     H1 = mine ? h1 : H1;
     AF = mine ? ((pieces - 1 - j) | (j == 0 ? 0x80000000u : 0u)) : AF;
+#endif
   };
   auto flush = [&](u32 kf, u32 nt) {
     const bool valid = (u32)lane < nt;
@@ -98,7 +103,11 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
       rem >>= 1;
     }
     if (AF >> 31) c ^= final_xor;
-    if (valid) tilecrc[(u64)(kf + (u32)lane) * nw + w] = c;
+#ifdef SUBSPACE_PROBE_NOSTORE
+    if (valid && c == 0x12345678u) tilecrc[(u64)w * nkmax + kf + (u32)lane] = c;  // cost probe: (almost) no stores
+#else
+    if (valid) tilecrc[(u64)w * nkmax + kf + (u32)lane] = c;  // wave-major (crc_ragged.hip xor_scan)
+#endif
   };
 
   LdsFill<WG, kRagLdsOpWords / 128> fill;
@@ -110,25 +119,32 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
   __syncthreads();
   if (nk == 0) return;
 
+  // The parked tiles are finished when all 64 slots are full, right after the next tile's
+  // loads are issued: the flush's stores then have a whole tile of compute to retire before
+  // the next drain (vmcnt counts stores with the loads; a store issued just before a drain
+  // stalls it for the write's round trip -- 3.6 % of the kernel at config D, r01au).
   u32 k = 0;
   for (; k + 1 < nk; k += 2) {
     drain_before_issue();
     load_next(B, mB, jB);
+    if (k && (k & 63u) == 0) flush(k - 64, 64u);
     process(A, jA, k);
     drain_before_issue();
     load_next(A, mA, jA);
     process(B, jB, k + 1);
-    if (((k + 2) & 63) == 0) flush(k + 2 - 64, 64u);
   }
-  if (k < nk) process(A, jA, k);
-  const u32 kf = nk & ~63u;
-  if (nk > kf) flush(kf, nk - kf);
+  if (k < nk) {
+    if (k && (k & 63u) == 0) flush(k - 64, 64u);
+    process(A, jA, k);
+  }
+  const u32 kf = (nk - 1) & ~63u;  // the last window (1..64 tiles), not flushed yet
+  flush(kf, nk - kf);
   (void)mA;
   (void)mB;
 }
 
 template __global__ void crc32_long_kernel<512>(const uint8_t*, u64, u32, u32, const u32*, const u32*, u32, u32,
-                                                u32*);
+                                                u32*, u32);
 
 // out[m] = XOR of message m's pieces = px[(m+1)P - 1] ^ px[mP - 1].
 __global__ void crc32_long_final_kernel(const u32* __restrict__ px, u32 pieces, u32 count, u32* __restrict__ out) {

@@ -16,19 +16,20 @@
 //    is 16-B aligned (packed arenas, slot payloads) needs no realignment at all: its
 //    lines are whole aligned 16-B blocks, whatever its length.
 //  * Waves stream the global tile list in sweep order (tau = k*nw + w), one tile of
-//    loads in flight ahead. Per-tile 16-B descriptors (tile end, tiles after, first-tile
-//    flag, message start offset in the first tile) are precomputed by
-//    crc32_ragged_desc_kernel.
+//    loads in flight ahead. Per-tile 16-B descriptors (tile start, tiles after, first-tile
+//    flag, message bytes in the tile) are precomputed by crc32_ragged_desc_kernel.
 //  * Per tile, lane l of half h applies its own line-shift operator Z_{128*(31-l)} (the
 //    uniform kernel's conflict-free [nibble][value][lane] tables) and a DPP reduction
 //    leaves the two half-tile values in lanes 31 and 63. They are parked, one tile per
 //    lane, in registers (lane k&63 keeps tile k); every 64 tiles each lane finishes its own tile,
 //      tile value = Z_{8192*T}( Z_4096(half0) ^ half1 )     (T = tiles after it)
 //    with a per-lane binary decomposition of T over nibble operators -- one wave pass
-//    shifts 64 tiles -- and stores tilecrc[tau]. A message's padded CRC is the XOR of its
-//    tiles' values, i.e. the difference of two entries of the inclusive XOR-scan of
-//    tilecrc (crc32_ragged_final_kernel). No atomics: huge messages (config D: 8192 tiles
-//    each, all in flight at once) would otherwise serialise every tile on one output word.
+//    shifts 64 tiles -- and stores them to tilecrc, wave-major ([w][k]: one wave's 64
+//    values are 256 contiguous bytes). A message's padded CRC is the XOR of its tiles'
+//    values, i.e. the difference of two entries of the inclusive XOR-scan of the values in
+//    tile order tau (gathered from the wave-major array; crc32_ragged_final_kernel). No
+//    atomics: huge messages (config D: 8192 tiles each, all in flight at once) would
+//    otherwise serialise every tile on one output word.
 //    (Batches whose tiles overflow the workspace -- overlapping messages -- fall back to
 //    atomicXor into pre-zeroed words.)
 //  * A message start that is not 16-B aligned makes every line misaligned by mis = s & 15
@@ -147,7 +148,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
                                             const u64* __restrict__ tile_base, u64 count,
                                             const TileDesc* __restrict__ desc, const u32* __restrict__ gtab,
                                             const u32* __restrict__ gops, u32 init, u32* __restrict__ out,
-                                            u32* __restrict__ tilecrc, u32 sbase) {
+                                            u32* __restrict__ tilecrc, u64 nkmax, u32 sbase) {
   const int lane = threadIdx.x & 63;
   const u32 wid = rfl(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
@@ -289,7 +290,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
       rem >>= 1;
     }
     if (valid) {
-      if (DESC) tilecrc[(kf + (u64)lane) * nw + w] = c;
+      if (DESC) tilecrc[w * nkmax + kf + (u64)lane] = c;  // wave-major: contiguous per flush
       else atomicXor(&out[MG], c);
     }
   };
@@ -314,7 +315,9 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   // has no early exit (a break between the halves would give the loop head a predecessor
   // with fewer loads in flight, and hipcc's waitcnt merge would drain the prefetch there);
   // an odd last tile, already loaded, follows the loop. The parked tiles are finished
-  // whenever all 64 slots are full, and once more at the end.
+  // whenever all 64 slots are full -- right after the next tile's loads are issued, so the
+  // stores retire during that tile's compute instead of stalling the next drain
+  // (crc_long.hip) -- and once more at the end.
   u64 k = 0;
   for (; k + 1 < nk; k += 2) {
     drain_before_issue();             // at most one tile of loads in flight (crc_uniform.hip)
@@ -322,6 +325,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
     const u32 m1 = mB;
     fetch_desc(k + 2, dA, mA);        // tile k+2 (clamped)
     load_line(d1, B, true);
+    if (k && (k & 63) == 0) flush(k - 64, 64u);
     process(A, dcur, mcur, k);
     drain_before_issue();
     const TileDesc d2 = unpack(dA);   // tile k+2 (clamped)
@@ -331,11 +335,13 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
     process(B, d1, m1, k + 1);
     dcur = d2;
     mcur = m2;
-    if (((k + 2) & 63) == 0) flush(k + 2 - 64, 64u);
   }
-  if (k < nk) process(A, dcur, mcur, k);
-  const u64 kf = nk & ~(u64)63;
-  if (nk > kf) flush(kf, (u32)(nk - kf));
+  if (k < nk) {
+    if (k && (k & 63) == 0) flush(k - 64, 64u);
+    process(A, dcur, mcur, k);
+  }
+  const u64 kf = (nk - 1) & ~(u64)63;  // the last window (1..64 tiles), not flushed yet
+  flush(kf, (u32)(nk - kf));
 }
 
 template <int WG>
@@ -347,22 +353,22 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
                                                           const u32* __restrict__ overflow,
                                                           const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                           u32 init, u32* __restrict__ out,
-                                                          u32* __restrict__ tilecrc) {
+                                                          u32* __restrict__ tilecrc, u64 nkmax) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
   // Precomputed descriptors unless the batch had more tiles than the workspace holds
   // (overlapping messages); then every tile is located by binary search.
   if (*overflow == 0u)
     ragged_body<WG, true>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, init, out,
-                          tilecrc, sbase);
+                          tilecrc, nkmax, sbase);
   else
     ragged_body<WG, false>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, init, out,
-                           tilecrc, sbase);
+                           tilecrc, nkmax, sbase);
 }
 
 template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
                                                   const TileDesc*, const u32*, const u32*, const u32*, u32, u32*,
-                                                  u32*);
+                                                  u32*, u64);
 
 // Per message with tiles: its padded CRC = XOR of its tiles' values = px[last] ^
 // px[first - 1] (px = inclusive XOR-scan of tilecrc), or the XOR the overflow path
@@ -385,7 +391,11 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
 }
 
 // hipcub scan wrappers: exclusive prefix sum of per-message tile counts; inclusive XOR
-// scan of per-tile values.
+// scan of per-tile values in tile order tau, gathered from the kernels' wave-major array
+// (tile tau = k*nw + w sits at w*nkmax + k). The flush stores are the reason for that
+// layout: 64 lanes storing tilecrc[tau] directly hit 64 lines 4*nw bytes apart, each
+// shared by waves of every XCD, and cost 8 % of the long kernel's time at config D
+// (r01aw); the gather costs the scan a few microseconds.
 hipError_t ragged_scan(void* temp, size_t& temp_bytes, const u64* in, u64* out, u64 n, hipStream_t stream) {
   return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, stream);
 }
@@ -394,8 +404,18 @@ struct XorOp {
   __host__ __device__ u32 operator()(u32 a, u32 b) const { return a ^ b; }
 };
 
-hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u32* out, u64 n, hipStream_t stream) {
-  return hipcub::DeviceScan::InclusiveScan(temp, temp_bytes, in, out, XorOp(), (int)n, stream);
+struct TileGather {
+  const u32* v;
+  u64 nw, nkmax;
+  __host__ __device__ u32 operator()(u64 tau) const { return v[(tau % nw) * nkmax + tau / nw]; }
+};
+
+hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u64 nw, u64 nkmax, u32* out, u64 n,
+                    hipStream_t stream) {
+  hipcub::CountingInputIterator<u64> tau(0);
+  hipcub::TransformInputIterator<u32, TileGather, hipcub::CountingInputIterator<u64>> it(tau,
+                                                                                       TileGather{in, nw, nkmax});
+  return hipcub::DeviceScan::InclusiveScan(temp, temp_bytes, it, out, XorOp(), (int)n, stream);
 }
 
 }  // namespace subspace_amd

@@ -142,21 +142,30 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // landed before tile k+1 is issued (drain_before_issue): each wave keeps at most one
   // tile in flight, which HBM serves faster than two (45.5 vs 47.3 us per 256 MiB launch,
   // profiles/r01/ceiling.md), and tile k+1's latency still hides behind tile k's compute.
+  // A full ring is stored right after the next tile's loads are issued, so the stores
+  // retire during that tile's compute instead of stalling the next drain (crc_long.hip).
   u32 k = 0, kf = 0;
   for (; k + 1 < nk; k += 2) {
     drain_before_issue();
     load_tile(B, k + 1);
+    if (k - kf == (u32)(kRing / 2)) {
+      wave_lds_sync();
+      flush(kf, kRing / 2);
+      kf = k;
+    }
     tile_result(line_crc(A), k, kf);
     drain_before_issue();
     load_tile(A, k + 2);
     tile_result(line_crc(B), k + 1, kf);
-    if (k + 2 - kf == (u32)(kRing / 2)) {
+  }
+  if (k < nk) {  // odd last tile, already loaded
+    if (k - kf == (u32)(kRing / 2)) {
       wave_lds_sync();
       flush(kf, kRing / 2);
-      kf = k + 2;
+      kf = k;
     }
+    tile_result(line_crc(A), k, kf);
   }
-  if (k < nk) tile_result(line_crc(A), k, kf);  // odd last tile, already loaded
   wave_lds_sync();
   if (nk > kf) flush(kf, nk - kf);
 }
