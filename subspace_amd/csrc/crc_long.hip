@@ -80,34 +80,22 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
     const u32 h0 = (u32)__builtin_amdgcn_readlane((int)v, 31), h1 = (u32)__builtin_amdgcn_readlane((int)v, 63);
-#ifdef SUBSPACE_PROBE_NOPARK
-    H0 ^= h0 ^ h1;  // cost probe: no per-lane park (wrong results)
-    (void)k;
-#else
     const bool mine = lane == (int)(k & 63);
     H0 = mine ? h0 : H0;
     H1 = mine ? h1 : H1;
     AF = mine ? ((pieces - 1 - j) | (j == 0 ? 0x80000000u : 0u)) : AF;
-#endif
   };
   auto flush = [&](u32 kf, u32 nt) {
     const bool valid = (u32)lane < nt;
     u32 c = opmul(sbase, kRagOpZ4096, H0) ^ H1;
     u32 rem = valid ? (AF & 0x7FFFFFFFu) : 0u;  // Z_{8192 * pieces after}; pieces < 2^21 (host check)
-#ifdef SUBSPACE_PROBE_NOSHIFT
-    rem = 0;
-#endif
     for (int bit = 0; bit < kNumTileOps && __any(rem != 0u); bit++) {
       const u32 cm = opmul(sbase, kRagOpZTile + bit, c);
       c = (rem & 1u) ? cm : c;
       rem >>= 1;
     }
     if (AF >> 31) c ^= final_xor;
-#ifdef SUBSPACE_PROBE_NOSTORE
-    if (valid && c == 0x12345678u) tilecrc[(u64)w * nkmax + kf + (u32)lane] = c;  // cost probe: (almost) no stores
-#else
     if (valid) tilecrc[(u64)w * nkmax + kf + (u32)lane] = c;  // wave-major (crc_ragged.hip xor_scan)
-#endif
   };
 
   LdsFill<WG, kRagLdsOpWords / 128> fill;
