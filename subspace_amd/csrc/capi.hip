@@ -108,7 +108,7 @@ struct subspace_crc_ctx {
   u32* d_overflow = nullptr;
   int uniform_wg = 512;    // workgroup size of the uniform kernel (256/512/640/768/1024)
   int uniform_blocks = 0;  // 0 = one workgroup per CU
-  int uniform_order = 0;   // tile order: 0 XCD-spread sweep, 1 per-workgroup region, 2 plain sweep
+  int uniform_order = 0;   // tile order: 0 XCD-spread sweep, 1 per-workgroup region, 2 plain sweep, 3 XCD-grouped
   bool long_path = true;   // whole-8 KiB-piece uniform batches take crc32_long_kernel
   u64* d_uoff = nullptr;  // offsets/lengths materialised for non-4K uniform batches
   u64* d_ulen = nullptr;
@@ -816,7 +816,7 @@ int subspace_crc_testutil_set(subspace_crc_ctx* c, const char* key, int value) {
 int subspace_crc_testutil_tune(subspace_crc_ctx* c, int uniform_wg, int uniform_blocks, int uniform_order) {
   if (!c) return SUBSPACE_CRC_EINVAL;
   if (uniform_wg != 256 && uniform_wg != 512 && uniform_wg != 768 && uniform_wg != 1024) return SUBSPACE_CRC_EINVAL;
-  if (uniform_order < 0 || uniform_order > 2) return SUBSPACE_CRC_EINVAL;
+  if (uniform_order < 0 || uniform_order > 3) return SUBSPACE_CRC_EINVAL;
   c->uniform_wg = uniform_wg;
   c->uniform_blocks = uniform_blocks;
   c->uniform_order = uniform_order;

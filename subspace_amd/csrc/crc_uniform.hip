@@ -55,8 +55,18 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   constexpr u64 wpb = WG / 64;
   const u64 nw = (u64)gridDim.x * wpb;
   u64 t0, tstep, tend;
+  // order 3 needs whole XCD groups: 8 | G and 16 | (G/8)*wpb; otherwise it is order 0
+  if (order == 3 && ((gridDim.x & 7u) || ((((u64)gridDim.x >> 3) * wpb) & 15u))) order = 0;
   if (order == 0) {
     t0 = front_slot(blockIdx.x, gridDim.x, (u32)wid);
+    tstep = nw;
+    tend = ntiles;
+  } else if (order == 3) {
+    // Sweep in XCD groups: each aligned group of 16 front slots (16 tiles = 32 messages =
+    // one 128-B line of results) lands on one XCD (two workgroups b, b+8), groups rotating
+    // over the 8 XCDs, so every output line is written from a single L2.
+    const u32 x = blockIdx.x & 7u, local = (blockIdx.x >> 3) * (u32)wpb + (u32)wid;
+    t0 = ((u64)(local >> 4) * 8u + x) * 16u + (local & 15u);
     tstep = nw;
     tend = ntiles;
   } else if (order == 2) {

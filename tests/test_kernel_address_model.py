@@ -189,3 +189,24 @@ def test_front_slot_tiles_covered_exactly_once():
             nk = (total - w + nw - 1) // nw if w < total else 0
             seen += [k * nw + w for k in range(nk)]
     assert sorted(seen) == list(range(total))
+
+
+def xcd_group_slot(b, G, wid, wpb):
+    """crc_uniform.hip order 3: aligned groups of 16 front slots on one XCD (b % 8), groups
+    rotating over the XCDs; only for 8 | G and 16 | (G/8)*wpb (else the kernel uses order 0)."""
+    x, local = b & 7, (b >> 3) * wpb + wid
+    return ((local >> 4) * 8 + x) * 16 + (local & 15)
+
+
+@pytest.mark.parametrize("wg", [256, 512, 768, 1024])
+@pytest.mark.parametrize("grid", [8, 16, 64, 128, 256])
+def test_xcd_group_slot_is_a_bijection(wg, grid):
+    wpb = wg // 64
+    if ((grid // 8) * wpb) % 16:
+        pytest.skip("the kernel falls back to order 0 for this grid")
+    slots = [xcd_group_slot(b, grid, wid, wpb) for b in range(grid) for wid in range(wpb)]
+    assert sorted(slots) == list(range(grid * wpb))
+    # every group of 16 consecutive slots (one 128-B line of results) is on one XCD
+    xcd = {xcd_group_slot(b, grid, wid, wpb): b & 7 for b in range(grid) for wid in range(wpb)}
+    for g in range(grid * wpb // 16):
+        assert len({xcd[16 * g + i] for i in range(16)}) == 1

@@ -135,11 +135,23 @@ int main() {
       std::string path = all.substr(pos, e - pos);
       pos = e + 1;
       if (path.empty()) continue;
+      int order = -1;  // "lib.so@N": uniform kernel tile order N (subspace_crc_testutil_tune)
+      const size_t at = path.find('@');
+      if (at != std::string::npos) {
+        order = std::atoi(path.c_str() + at + 1);
+        path = path.substr(0, at);
+      }
       void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
       if (!h) { fprintf(stderr, "dlopen %s: %s\n", path.c_str(), dlerror()); return 1; }
       auto create = (create_t)dlsym(h, "subspace_crc_ctx_create");
       Lib L{path, (uni_t)dlsym(h, "subspace_crc32_batch_uniform"), nullptr};
       if (!create || !L.uni || create(0, &L.ctx)) { fprintf(stderr, "ctx for %s failed\n", path.c_str()); return 1; }
+      if (order >= 0) {
+        typedef int (*tune_t)(subspace_crc_ctx*, int, int, int);
+        auto tune = (tune_t)dlsym(h, "subspace_crc_testutil_tune");
+        if (!tune || tune(L.ctx, 512, 0, order)) { fprintf(stderr, "tune %s failed\n", path.c_str()); return 1; }
+        L.path += "@" + std::to_string(order);
+      }
       libs.push_back(L);
     }
   }
