@@ -20,13 +20,13 @@ template <int WG>
 __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
 
 struct TileDesc;
-__global__ void crc32_ragged_count_kernel(const u64*, u32, u64, u32, u32, u64*, u32*);
+__global__ void crc32_ragged_count_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*);
 __global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, u64, u64, TileDesc*, u32*);
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
-                                    const TileDesc*, const u32*, const u32*, const u32*, u32, u32*, u32*, u64);
-__global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, u64, const u32*, const u32*, const u32*, u32,
-                                          u32*);
+                                    const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds, u32*, u32*, u64);
+__global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, const u64*, u32, u64, const u32*, const u32*,
+                                          const u32*, u32, u32*);
 hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u64 nw, u64 nkmax, u32* out, u64 n,
                     hipStream_t stream);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, int, int, u32, const u32*,
@@ -93,6 +93,7 @@ struct subspace_crc_ctx {
   u32* d_pow2 = nullptr;  // Z_{2^k}, k = 0..63, nibble operators (slot checksums)
   u32* d_laneops = nullptr;  // uniform kernel: Z_{128*s}, s = 0..31, as [nibble][value][s]
   Tables host_tab;
+  Mat32 zinv1;  // Z_1^{-1}: the ragged kernel's head seeds Z_r^{-1}(init)
   // ragged workspace
   u64* d_ntiles = nullptr;   // count + 1
   u64* d_tbase = nullptr;    // count + 1
@@ -196,8 +197,8 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   int rc = ensure_ragged_ws(c, count, cap);
   if (rc) return rc;
   const u64 n1 = count + 1;
-  crc32_ragged_count_kernel<<<(unsigned)((n1 + 255) / 256), 256, 0, st>>>(lengths, lstride, count, init, final_xor,
-                                                                           c->d_ntiles, out);
+  crc32_ragged_count_kernel<<<(unsigned)((n1 + 255) / 256), 256, 0, st>>>(offsets, ostride, lengths, lstride, count,
+                                                                           init, final_xor, c->d_ntiles, out);
   HIP_TRY(hipGetLastError());
   size_t tmp = c->scan_tmp_bytes;
   HIP_TRY(ragged_scan(c->d_scan_tmp, tmp, c->d_ntiles, c->d_tbase, n1, st));
@@ -206,10 +207,13 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
       c->d_overflow);
   HIP_TRY(hipGetLastError());
   const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU
+  HeadSeeds seeds;  // Z_r^{-1}(init), r = 0..15: the seed of a message's first line, mis = r
+  seeds.v[0] = init;
+  for (int r = 1; r < 16; r++) seeds.v[r] = apply(c->zinv1, seeds.v[r - 1]);
   const u64 nw = (u64)blocks * (kRaggedWG / 64), nkmax = (cap + nw - 1) / nw;  // wave-major tile values
   crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, ragged_lds_bytes(), st>>>(
       base, offsets, ostride, lengths, lstride, c->d_tbase, count, reinterpret_cast<const TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_tab, c->d_rops, init, out, c->d_tilecrc, nkmax);
+      c->d_overflow, c->d_tab, c->d_rops, seeds, out, c->d_tilecrc, nkmax);
   HIP_TRY(hipGetLastError());
   // padded message CRC = XOR of its tiles' values = difference of two XOR-scan entries
   // (entries past the batch's real tile count are scanned but never read); the final
@@ -217,7 +221,7 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   size_t xtmp = c->xscan_tmp_bytes;
   HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, nw, nkmax, c->d_px, cap, st));
   crc32_ragged_final_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(
-      c->d_tbase, lengths, lstride, count, c->d_px, c->d_overflow, c->d_rops, final_xor, out);
+      c->d_tbase, offsets, ostride, lengths, lstride, count, c->d_px, c->d_overflow, c->d_rops, final_xor, out);
   HIP_TRY(hipGetLastError());
   return SUBSPACE_CRC_OK;
 }
@@ -286,6 +290,7 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   c->num_cus = prop.multiProcessorCount;
   c->poly = poly;
   c->host_tab = make_tables(poly);
+  c->zinv1 = inverse(z_one(c->host_tab));
 
   std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kLaneOpWords, 0u), rops(kRagOpWords, 0u);
   for (int k = 0; k < 4; k++)
@@ -399,7 +404,8 @@ int subspace_crc32_batch(subspace_crc_ctx* c, const void* dev_base, uint64_t are
   const u32 final_xor = (flags & SUBSPACE_CRC_FINALIZE) ? 0xFFFFFFFFu : 0u;
   // Tile capacity: exact for non-overlapping messages inside the arena; if the device
   // finds more tiles (overlapping messages) the kernel falls back to per-tile search.
-  const u64 cap = arena_bytes / 8192 + count + 1;
+  // (a message's tiles cover its extended length L + (offset & 15))
+  const u64 cap = (arena_bytes + 15 * count) / 8192 + count + 1;
   return ragged_run(c, static_cast<const uint8_t*>(dev_base), cap, dev_offsets, 1, dev_lengths, 1, count, init,
                     final_xor, dev_out, st);
 }
@@ -495,7 +501,7 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
   if (rc) return rc;
   // payload CRCs from init 0 at absolute addresses (base 0; fields 1 and 2 of each record)
   const u64* rec = reinterpret_cast<const u64*>(dev_slots);
-  const u64 cap = count * ((max_message_size + 8191) / 8192) + 1;
+  const u64 cap = count * ((max_message_size + 15 + 8191) / 8192) + 1;
   rc = ragged_run(c, nullptr, cap, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st);
   if (rc) return rc;
   return slot_finish(c, rec, nullptr, 0, nullptr, 0, count, checksum_size, metadata_size, mode, dev_status,
@@ -536,7 +542,7 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
     slot_payload_offsets_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(slot_stride, prefix_size, count,
                                                                                 c->d_soff);
     HIP_TRY(hipGetLastError());
-    const u64 cap = (slot_stride * count) / 8192 + count + 1;
+    const u64 cap = (slot_stride * count + 15 * count) / 8192 + count + 1;
     rc = ragged_run(c, buf, cap, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st);
   } else {
     rc = subspace_crc32_batch_uniform(c, buf + prefix_size, slot_stride, message_size, count, 0u, 0u, c->d_crc0,

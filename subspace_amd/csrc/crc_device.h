@@ -50,6 +50,11 @@ constexpr int kRagOpWords = kRagInvOps + kNumInvOps * 128;
 constexpr size_t ragged_lds_bytes() { return kLdsOps + (size_t)kRagLdsOpWords * 4u; }
 static_assert(ragged_lds_bytes() <= 160u * 1024u, "ragged kernel LDS exceeds 160 KiB");
 
+// Ragged kernel head seeds of one call: v[r] = Z_r^{-1}(init), r = 0..15 (a kernel argument).
+struct HeadSeeds {
+  u32 v[16];
+};
+
 typedef __attribute__((address_space(3))) u32 lds_u32_t;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
 

@@ -2,22 +2,26 @@
 // alignment (BASELINE configs C and D; any subspace_crc32_batch call).
 //
 // Decomposition (DESIGN.md "Ragged kernel"):
-//  * Message m = bytes [s, e), L = e - s. Its nt = ceil(L/8192) tiles are aligned to the
-//    message START: tile j covers [s + 8192j, s + 8192(j+1)), and only the last tile can
-//    be short (len = L - 8192(nt-1) bytes). Lane l of a tile owns the 128-B line
-//    [s + 8192j + 128l, +128): 64 consecutive lines per wave load instruction, exactly like
-//    the uniform kernel. Line 0 of tile 0 starts from `init`, every other line from 0.
-//  * The last tile is read as if it were zero-padded to 8 KiB: its bytes at and past e are
-//    zero-masked. The tiles then compute the padded message's CRC,
-//      crc_raw(init, D || 0^p) = Z_p(crc_raw(init, D)),        p = 8192*nt - L < 8192,
+//  * Message m = bytes [s, e), L = e - s, mis = s & 15. It is read as the EXTENDED message
+//    [s0, e), s0 = s - mis (the 16-B block holding s), whose first mis bytes are masked to
+//    zero, cut into nt = ceil((L + mis)/8192) tiles: tile j covers [s0 + 8192j, +8192), and
+//    only the last tile can be short (len = L + mis - 8192(nt-1) bytes). Lane l of a tile
+//    owns the 128-B line [s0 + 8192j + 128l, +128): 64 consecutive lines per wave load
+//    instruction, exactly like the uniform kernel, and every line is whole aligned 16-B
+//    blocks -- no realignment, whatever the message's alignment and length.
+//  * Head: line 0 of tile 0 starts from seed[mis] = Z_mis^{-1}(init) (host-computed), so
+//    after its mis zero bytes the state is exactly init:
+//      crc_raw(Z_mis^{-1}(init), 0^mis || D) = crc_raw(init, D);
+//    every other line starts from 0 (zero data from state 0 stays 0).
+//  * Tail: the last tile is read as if zero-padded to 8 KiB (bytes at and past e masked),
+//    so the tiles compute
+//      crc_raw(init, D || 0^p) = Z_p(crc_raw(init, D)),   p = 8192*nt - (L + mis) < 8192,
 //    and the final kernel undoes the padding with p's binary decomposition over the
 //    inverse operators Z_{2^b}^{-1} (b = 0..12; Z_n is invertible since P has an x^0 term)
-//    before the final XOR. Leading data needs no seed or mask, and a message whose start
-//    is 16-B aligned (packed arenas, slot payloads) needs no realignment at all: its
-//    lines are whole aligned 16-B blocks, whatever its length.
+//    before the final XOR.
 //  * Waves stream the global tile list in sweep order (tau = k*nw + w), one tile of
 //    loads in flight ahead. Per-tile 16-B descriptors (tile start, tiles after, first-tile
-//    flag, message bytes in the tile) are precomputed by crc32_ragged_desc_kernel.
+//    flag, bytes in the tile and mis) are precomputed by crc32_ragged_desc_kernel.
 //  * Per tile, lane l of half h applies its own line-shift operator Z_{128*(31-l)} (the
 //    uniform kernel's conflict-free [nibble][value][lane] tables) and a DPP reduction
 //    leaves the two half-tile values in lanes 31 and 63. They are parked, one tile per
@@ -32,13 +36,7 @@
 //    otherwise serialise every tile on one output word.
 //    (Batches whose tiles overflow the workspace -- overlapping messages -- fall back to
 //    atomicXor into pre-zeroed words.)
-//  * A message start that is not 16-B aligned makes every line misaligned by mis = s & 15
-//    (wave-uniform per tile). Each lane then loads the 8 aligned 16-B blocks starting at or
-//    below its line; the line's last mis bytes sit in the next lane's first block, which
-//    arrives by a DPP wave shift, and for lane 63 in the block after the tile, one load
-//    shared by the whole wave. The words are realigned with v_alignbyte_b32 (the dword
-//    shift mis>>2 is wave-uniform: a 4-way uniform switch). Loads never touch a 16-B block
-//    that holds no byte of the message.
+//  * Loads never touch a 16-B block that holds no byte of the message.
 #include <hipcub/hipcub.hpp>
 
 #include "crc_device.h"
@@ -47,20 +45,22 @@ namespace subspace_amd {
 
 // 16 B per tile: one vector load and four readfirstlanes per tile in the main kernel.
 struct TileDesc {
-  u64 tile_start;  // absolute offset (from base) of the tile's first byte
+  u64 tile_start;  // absolute offset (from base) of the tile's first byte (16-B aligned)
   u32 after;       // tiles after this one in the message | kFirstTile for its first tile
-  u32 len;         // message bytes in the tile: 8192, or 1..8192 for the last tile
+  u32 len;         // bytes of the extended message in the tile (1..8192) | mis << 16
 };
 static_assert(sizeof(TileDesc) == 16, "TileDesc is 16 B");
 constexpr u32 kFirstTile = 0x80000000u;
 
-__host__ __device__ inline u64 tiles_for_length(u64 len) { return (len + 8191) >> 13; }
+// Tiles of message (s, L): its extended length L + (s & 15) in 8 KiB tiles (0 if L = 0).
+__host__ __device__ inline u64 tiles_for(u64 s, u64 len) { return len ? (len + (s & 15) + 8191) >> 13 : 0; }
 
 // Per message: tile count; zero-length messages get their (constant) result here, every
 // other output word is zeroed (the overflow path XORs tile values into it).
-// `lengths` (and `offsets` below) are read with an element stride (1 for plain arrays, 3 for
-// the lengths/payload fields of subspace_crc_slot records).
-__global__ void crc32_ragged_count_kernel(const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
+// `offsets` and `lengths` are read with an element stride (1 for plain arrays, 3 for the
+// payload/size fields of subspace_crc_slot records).
+__global__ void crc32_ragged_count_kernel(const u64* __restrict__ offsets, u32 ostride,
+                                          const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
                                           u32 final_xor, u64* __restrict__ ntiles, u32* __restrict__ out) {
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (i > count) return;
@@ -68,7 +68,7 @@ __global__ void crc32_ragged_count_kernel(const u64* __restrict__ lengths, u32 l
     ntiles[i] = 0;  // scan sentinel: tile_base[count] = total tiles
     return;
   }
-  const u64 nt = tiles_for_length(lengths[i * lstride]);
+  const u64 nt = tiles_for(offsets[i * ostride], lengths[i * lstride]);
   ntiles[i] = nt;
   out[i] = nt == 0 ? init ^ final_xor : 0u;
 }
@@ -88,11 +88,13 @@ __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, u32 ostrid
                                      u32 lstride, const u64* __restrict__ tile_base, u64 m, u64 tau) {
   const u64 nt = tile_base[m + 1] - tile_base[m];
   const u64 j = tau - tile_base[m];
-  const u64 rest = lengths[m * lstride] - (j << 13);  // message bytes from the tile start on
+  const u64 s = offsets[m * ostride];
+  const u32 mis = (u32)(s & 15);
+  const u64 rest = lengths[m * lstride] + mis - (j << 13);  // extended bytes from the tile start on
   TileDesc d;
-  d.tile_start = offsets[m * ostride] + (j << 13);
+  d.tile_start = (s & ~(u64)15) + (j << 13);
   d.after = (u32)(nt - 1 - j) | (j == 0 ? kFirstTile : 0u);
-  d.len = rest < 8192 ? (u32)rest : 8192u;
+  d.len = (rest < 8192 ? (u32)rest : 8192u) | (mis << 16);
   return d;
 }
 
@@ -109,29 +111,6 @@ __global__ void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, u32 os
 }
 
 // ------------------------------------------------------------------ main kernel
-struct LineState {
-  u32x4 d[8];  // the 8 aligned 16-B blocks starting at or below the lane's line
-  u32x4 x;     // the block after the tile (the same for every lane)
-};
-
-template <int Q>
-__device__ __forceinline__ u32 word_at(const u32x4 (&d)[9], int j, u32 m3) {
-  // word j of the realigned line: bytes [4(j+Q) + m3, +4) of the aligned window
-  const int x = j + Q;
-  const u32 lo = d[x >> 2][x & 3];
-  const u32 hi = d[(x + 1) >> 2][(x + 1) & 3];
-  return __builtin_amdgcn_alignbyte(hi, lo, m3);
-}
-
-template <int Q, bool MIS>
-__device__ __forceinline__ u32 crc_line(const u32x4 (&d)[9], u32 crc, u32 m3, u32 lc0, u32 lc1) {
-#pragma unroll
-  for (int j = 0; j < 32; j++) {
-    const u32 w = MIS ? word_at<Q>(d, j, m3) : d[j >> 2][j & 3];
-    crc = step4(crc ^ w, lc0, lc1);
-  }
-  return crc;
-}
 
 // Nibble operator read from global memory (the tile-shift operators for 2^21 tiles and
 // more, which only messages of 16 GiB and more need; the padding inverses).
@@ -142,13 +121,31 @@ __device__ __forceinline__ u32 opmul_global(const u32* __restrict__ op, u32 v) {
   return r;
 }
 
+// Keep the bytes of a 128-B line window at positions [lo, hi) (0 <= lo, hi <= 128).
+__device__ __forceinline__ void keep_bytes(u32x4 (&d)[8], u32 lo, u32 hi) {
+#pragma unroll
+  for (int b = 0; b < 8; b++) {
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+      const u32 p = 16u * b + 4u * x;
+      u32 keep = 0u;
+      if (p + 4u <= hi) keep = 0xFFFFFFFFu;
+      else if (p < hi) keep = 0xFFFFFFFFu >> (8u * (p + 4u - hi));
+      if (p + 4u <= lo) keep = 0u;
+      else if (p < lo) keep &= 0xFFFFFFFFu << (8u * (lo - p));
+      d[b][x] &= keep;
+    }
+  }
+}
+
 template <int WG, bool DESC>
 __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, const u64* __restrict__ offsets,
                                             u32 ostride, const u64* __restrict__ lengths, u32 lstride,
                                             const u64* __restrict__ tile_base, u64 count,
                                             const TileDesc* __restrict__ desc, const u32* __restrict__ gtab,
-                                            const u32* __restrict__ gops, u32 init, u32* __restrict__ out,
-                                            u32* __restrict__ tilecrc, u64 nkmax, u32 sbase) {
+                                            const u32* __restrict__ gops, const HeadSeeds& seeds,
+                                            u32* __restrict__ out, u32* __restrict__ tilecrc, u64 nkmax,
+                                            u32 sbase) {
   const int lane = threadIdx.x & 63;
   const u32 wid = rfl(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
@@ -187,73 +184,45 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
     t.len = rfl(d[3]);
     return t;
   };
-  // Issue the loads of tile d, as buffer loads against a scalar resource spanning exactly
-  // the 16-B blocks that hold the tile's bytes:
-  //   [tile start rounded down to 16, tile end rounded up to 16).
-  // Lane l loads the 8 blocks from 128*l; blocks past the range (past the message end)
-  // read as zeros without touching memory, so every lane issues every load (no divergent
-  // branch around loads). The 9th load is the same for all lanes: the block at 8192, which
-  // holds the tile's last bytes when its start is misaligned (in range then), else it is
-  // out of range (zeros, no access). `live` false (a prefetch past the wave's last tile)
-  // gives an empty range.
-  auto load_line = [&](const TileDesc& d, LineState& L, bool live) {
-    const u64 t0a = d.tile_start & ~(u64)15;
-    const u64 rend = (d.tile_start + d.len + 15) & ~(u64)15;
-    const u32 nrec = live ? (u32)(rend - t0a) : 0u;
-    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + t0a), (short)0, (int)nrec,
-                                                     kBufferRsrcFlags);
+  // Issue the loads of tile d: buffer loads against a scalar resource spanning exactly the
+  // 16-B blocks that hold the tile's bytes, [tile start, tile end rounded up to 16). Lane l
+  // loads the 8 blocks from 128*l; blocks past the range (past the message end) read as
+  // zeros without touching memory, so every lane issues every load (no divergent branch
+  // around loads). `live` false (a prefetch past the wave's last tile) gives an empty range.
+  auto load_line = [&](const TileDesc& d, u32x4 (&L)[8], bool live) {
+    const u32 nrec = live ? (((d.len & 0xFFFFu) + 15u) & ~15u) : 0u;
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + d.tile_start), (short)0,
+                                                     (int)nrec, kBufferRsrcFlags);
     const u32 vo = (u32)lane * 128u;
 #pragma unroll
-    for (int b = 0; b < 8; b++) L.d[b] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16u * b, 0, 0);
-    // the shared block's offset goes in the VGPR (not the scalar offset), so the range
-    // check sees it whichever offsets the hardware includes
-    L.x = __builtin_amdgcn_raw_buffer_load_b128(r, vzero + 8192u, 0, 0);
+    for (int b = 0; b < 8; b++) L[b] = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16u * b, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
   };
 
   // Half-tile values parked one tile per lane (slot k & 63), finished every 64 tiles.
   u32 H0 = 0, H1 = 0, AF = 0, MG = 0;  // half 0, half 1, after | kFirstTile, message (DESC false)
 
-  auto process = [&](const LineState& cur, const TileDesc& dcur, u32 dm, u64 k) {
+  auto process = [&](const u32x4 (&cur)[8], const TileDesc& dcur, u32 dm, u64 k) {
     const bool first = (dcur.after & kFirstTile) != 0;  // wave-uniform, like everything below
-    const u32 mis = (u32)(dcur.tile_start & 15);
-    u32x4 d[9];
+    const u32 len = dcur.len & 0xFFFFu, mis = dcur.len >> 16;
+    u32x4 d[8];
 #pragma unroll
-    for (int b = 0; b < 8; b++) d[b] = cur.d[b];
-    if (mis) {  // lane l's 9th block is lane l+1's first, lane 63's the shared one
-#pragma unroll
-      for (int x = 0; x < 4; x++)
-        d[8][x] = (u32)__builtin_amdgcn_update_dpp((int)cur.x[x], (int)cur.d[0][x], 0x130, 0xF, 0xF, false);
-    } else {
-      d[8] = u32x4{0u, 0u, 0u, 0u};
+    for (int b = 0; b < 8; b++) d[b] = cur[b];
+    // Head: the first tile's first mis bytes precede the message (lane 0's first block).
+    // Tail: a short tile whose end is not 16-B aligned also holds bytes past the message in
+    // its last loaded block. Each lane keeps only its line's message bytes.
+    const bool head = first && mis != 0u, tail = len < 8192u && (len & 15u) != 0u;
+    if (head || tail) {
+      const int v0 = (int)len - 128 * lane;
+      const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
+      const u32 lo = (head && lane == 0) ? mis : 0u;
+      keep_bytes(d, lo, hi);
     }
-    // A short last tile whose end is not 16-B aligned: its last loaded block also holds
-    // bytes past the message; zero every byte of each lane's 144-B window from the
-    // message end on (the lane's line is window bytes [mis, mis + 128), and its first
-    // `valid` bytes are message bytes), so the tile reads as zero-padded.
-    if (dcur.len < 8192u && ((u32)(dcur.tile_start + dcur.len) & 15u)) {
-      const int v0 = (int)dcur.len - 128 * lane;
-      const u32 zb = mis + (v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0));  // keep window bytes < zb
+    u32 crc = (first && lane == 0) ? seeds.v[mis] : 0u;
 #pragma unroll
-      for (int b = 0; b < 9; b++) {
+    for (int b = 0; b < 8; b++)
 #pragma unroll
-        for (int x = 0; x < 4; x++) {
-          const u32 p = 16u * b + 4u * x;
-          u32 keep = 0u;
-          if (p + 4u <= zb) keep = 0xFFFFFFFFu;
-          else if (p < zb) keep = 0xFFFFFFFFu >> (8u * (p + 4u - zb));
-          d[b][x] &= keep;
-        }
-      }
-    }
-    u32 crc = (first && lane == 0) ? init : 0u;
-    const u32 m3 = mis & 3;
-    switch (mis >> 2) {
-      case 0: crc = mis ? crc_line<0, true>(d, crc, m3, lc0, lc1) : crc_line<0, false>(d, crc, m3, lc0, lc1); break;
-      case 1: crc = crc_line<1, true>(d, crc, m3, lc0, lc1); break;
-      case 2: crc = crc_line<2, true>(d, crc, m3, lc0, lc1); break;
-      default: crc = crc_line<3, true>(d, crc, m3, lc0, lc1); break;
-    }
+      for (int q = 0; q < 4; q++) crc = step4(crc ^ d[b][q], lc0, lc1);
 
     // line l of half h -> Z_{128*(31-l)}(line): 8 conflict-free nibble lookups; then XOR
     // over each half with DPP (lane 31: lines 0..31, lane 63: lines 32..63)
@@ -305,7 +274,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   fetch_desc(1, dB, mB);
   TileDesc dcur = unpack(dA);
   u32 mcur = mA;
-  LineState A, B;
+  u32x4 A[8], B[8];
   load_line(dcur, A, nk != 0);
   fill.store(sbase);
   __syncthreads();
@@ -352,38 +321,38 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
                                                           const TileDesc* __restrict__ desc,
                                                           const u32* __restrict__ overflow,
                                                           const u32* __restrict__ gtab, const u32* __restrict__ gops,
-                                                          u32 init, u32* __restrict__ out,
+                                                          HeadSeeds seeds, u32* __restrict__ out,
                                                           u32* __restrict__ tilecrc, u64 nkmax) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
   // Precomputed descriptors unless the batch had more tiles than the workspace holds
   // (overlapping messages); then every tile is located by binary search.
   if (*overflow == 0u)
-    ragged_body<WG, true>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, init, out,
+    ragged_body<WG, true>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, seeds, out,
                           tilecrc, nkmax, sbase);
   else
-    ragged_body<WG, false>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, init, out,
+    ragged_body<WG, false>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, seeds, out,
                            tilecrc, nkmax, sbase);
 }
 
 template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
-                                                  const TileDesc*, const u32*, const u32*, const u32*, u32, u32*,
-                                                  u32*, u64);
+                                                  const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds,
+                                                  u32*, u32*, u64);
 
 // Per message with tiles: its padded CRC = XOR of its tiles' values = px[last] ^
-// px[first - 1] (px = inclusive XOR-scan of tilecrc), or the XOR the overflow path
-// accumulated in out[m]; then the padding undone -- Z_p^{-1} for p = (-L) mod 8192, as
-// p's bits over the inverse operators Z_{2^b}^{-1} -- and the final XOR applied.
-__global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, const u64* __restrict__ lengths,
-                                          u32 lstride, u64 count, const u32* __restrict__ px,
-                                          const u32* __restrict__ overflow, const u32* __restrict__ gops,
-                                          u32 final_xor, u32* __restrict__ out) {
+// px[first - 1] (px = inclusive XOR-scan of the tile values), or the XOR the overflow path
+// accumulated in out[m]; then the padding undone -- Z_p^{-1} for p = -(L + mis) mod 8192,
+// as p's bits over the inverse operators Z_{2^b}^{-1} -- and the final XOR applied.
+__global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, const u64* __restrict__ offsets,
+                                          u32 ostride, const u64* __restrict__ lengths, u32 lstride, u64 count,
+                                          const u32* __restrict__ px, const u32* __restrict__ overflow,
+                                          const u32* __restrict__ gops, u32 final_xor, u32* __restrict__ out) {
   const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= count) return;
   const u64 t0 = tile_base[m], t1 = tile_base[m + 1];
   if (t1 == t0) return;  // empty message: written by the count kernel
   u32 v = *overflow ? out[m] : px[t1 - 1] ^ (t0 ? px[t0 - 1] : 0u);
-  const u32 pad = (u32)(0 - lengths[m * lstride]) & 8191u;
+  const u32 pad = (u32)(0 - (lengths[m * lstride] + (offsets[m * ostride] & 15))) & 8191u;
 #pragma unroll 1
   for (int b = 0; b < kNumInvOps; b++)
     if ((pad >> b) & 1u) v = opmul_global(gops + kRagInvOps + 128 * b, v);

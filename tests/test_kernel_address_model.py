@@ -1,5 +1,5 @@
 """CPU models of the kernels' load addresses and tile indexing (subspace_amd/csrc/
-crc_ragged.hip make_desc + load_line + the 9th-block wave shift, crc_uniform.hip tile_rsrc / load_tile, and the sweep
+crc_ragged.hip make_desc + load_line, crc_uniform.hip load_tile, and the sweep
 front mapping): every byte any load can read lies inside the caller's messages, every
 message byte is read, every tile is visited exactly once. Runs without a GPU."""
 import numpy as np
@@ -14,38 +14,24 @@ def tiles_for_length(n):
 
 def ragged_loads(s, e):
     """For message [s, e): (tile j, lane, block, address or None) for every load of
-    load_line. Tiles are aligned to the message start (tile j starts at ts = s + 8192j and
-    holds min(8192, e - ts) bytes); loads are buffer loads against the range [t0a, rend) =
-    [ts rounded down, tile end rounded up to 16 B), and an offset >= the range size reads
-    zeros without a memory access (None). Blocks 0..7 are the lane's own (offsets 128*lane
-    + 16*b); block 8 is the load shared by the wave, at offset 8192."""
-    n = e - s
-    nt = tiles_for_length(n)
+    load_line. Tiles cover the extended message [s0, e), s0 = s rounded down to 16 B: tile
+    j starts at ts = s0 + 8192j and holds min(8192, e - ts) bytes; loads are buffer loads
+    against the range [ts, tile end rounded up to 16 B), and an offset >= the range size
+    reads zeros without a memory access (None). Lane l loads the 8 blocks at 128*l + 16*b."""
+    s0 = s & ~15
+    nt = tiles_for_length(e - s0)
     for j in range(nt):
-        ts = s + (j << 13)
-        ln = min(8192, e - ts)
-        t0a = ts & ~15
-        nrec = ((ts + ln + 15) & ~15) - t0a
+        ts = s0 + (j << 13)
+        nrec = (min(8192, e - ts) + 15) & ~15
         for lane in range(64):
             for b in range(8):
                 off = lane * 128 + 16 * b
-                yield j, lane, b, (t0a + off if off < nrec else None)
-            yield j, lane, 8, (t0a + 8192 if 8192 < nrec else None)
+                yield j, lane, b, (ts + off if off < nrec else None)
 
 
 def ragged_line_window(s, e, j, lane):
-    """The 9 blocks process() realigns for (tile j, lane): its own 8, then lane+1's block
-    0 (DPP wave_shl:1) or, for lane 63, the shared block (zeros when the message start is
-    16-B aligned) -- as addresses (None = zeros)."""
-    loads = {}
-    for jj, ln, b, addr in ragged_loads(s, e):
-        if jj == j:
-            loads[(ln, b)] = addr
-    own = [loads[(lane, b)] for b in range(8)]
-    if (s & 15) == 0:
-        return own + [None]  # aligned start: the 9th block is not used (zeros)
-    nxt = loads[(lane + 1, 0)] if lane < 63 else loads[(63, 8)]
-    return own + [nxt]
+    """The 8 blocks process() reads for (tile j, lane) -- as addresses (None = zeros)."""
+    return [addr for jj, ln, b, addr in ragged_loads(s, e) if jj == j and ln == lane]
 
 
 @pytest.mark.parametrize("seed", range(6))
@@ -67,24 +53,22 @@ def test_every_ragged_load_stays_in_its_message_blocks(seed):
 @pytest.mark.parametrize("s,n", [(0, 1), (3, 100), (17, 8192), (5, 8193), (0, 4096), (1, 65536 + 7), (15, 24577),
                                  (64, 16384 + 9), (7, 8192 * 3)])
 def test_ragged_line_windows_hold_each_line(s, n):
-    """Every lane's realigned 128-B line [ts + 128l, +128) is read from its 9-block window:
-    blocks at consecutive 16-B steps from the aligned start, the 9th through the wave
-    shift -- and every message byte of the line comes from a real load."""
+    """Every lane's 128-B line [ts + 128l, +128) is its 8 consecutive aligned blocks, and
+    every message byte of the line comes from a real load."""
     e = s + n
-    nt = tiles_for_length(n)
+    s0 = s & ~15
+    nt = tiles_for_length(e - s0)
     for j in range(nt):
-        ts = s + (j << 13)
+        ts = s0 + (j << 13)
         for lane in range(64):
             win = ragged_line_window(s, e, j, lane)
-            base = (ts & ~15) + 128 * lane
-            line = range(ts + 128 * lane, ts + 128 * lane + 128)
+            base = ts + 128 * lane
             for b, addr in enumerate(win):
                 if addr is not None:
                     assert addr == base + 16 * b, (s, n, j, lane, b)
-            for x in line:
+            for x in range(base, base + 128):
                 if s <= x < e:
-                    b = (x - base) // 16
-                    assert 0 <= b < 9 and win[b] is not None, (s, n, j, lane, x)
+                    assert win[(x - base) // 16] is not None, (s, n, j, lane, x)
 
 
 def test_ragged_loads_cover_every_message_byte():

@@ -1,5 +1,6 @@
 """CPU model of the kernels' CRC decomposition (the algebra, not the HIP code):
-the ragged kernel's start-aligned tiles with a zero-padded last tile, per-lane line-shift
+the ragged kernel's 16-B aligned tiles (head bytes masked, first line seeded with
+Z_mis^{-1}(init)) with a zero-padded last tile, per-lane line-shift
 operators + DPP half reduction, Z_4096 join, Z_{8192*T} shift, XOR combine and the
 padding undone with Z_{2^b}^{-1}; the uniform kernel's per-line
 CRCs and transposed tree. Each must equal the reference CRC (zlib) bit for bit."""
@@ -78,18 +79,26 @@ def ragged_model(buf: bytes, s: int, L: int, init: int) -> int:
     e = s + L
     if L == 0:
         return init
-    nt = (L + 8191) >> 13
+    mis = s & 15
+    s0 = s - mis  # the extended message [s0, e): its first mis bytes are masked to zero
+    nt = (L + mis + 8191) >> 13
     out = 0
     for j in range(nt):
-        ts = s + (j << 13)  # tiles are aligned to the message start
+        ts = s0 + (j << 13)
         lines = []
         for lane in range(64):
             ls = ts + 128 * lane
-            data = bytearray(128)  # bytes past the message end stay zero (padded last tile)
+            data = bytearray(128)  # bytes outside [s, e) stay zero (head mask, padded last tile)
             for i in range(128):
-                if ls + i < e:
+                if s <= ls + i < e:
                     data[i] = buf[ls + i]
-            lines.append(crc_raw(init if (j == 0 and lane == 0) else 0, bytes(data)))
+            seed = 0
+            if j == 0 and lane == 0:
+                seed = init
+                for b in range(4):  # Z_mis^{-1}(init): after the mis zero bytes the state is init
+                    if (mis >> b) & 1:
+                        seed = apply(ZINV_POW2[b], seed)
+            lines.append(crc_raw(seed, bytes(data)))
         # per lane: Z_{128*(31 - l%32)} on its line; XOR over each half (DPP); the halves
         # joined with Z_4096; then the shift to the padded message end, Z_{8192*T}
         shifted = [apply(LANE_OPS[31 - (lane & 31)], lines[lane]) for lane in range(64)]
@@ -103,8 +112,8 @@ def ragged_model(buf: bytes, s: int, L: int, init: int) -> int:
             after >>= 1
             k += 1
         out ^= t
-    # out = crc_raw(init, D || 0^p) = Z_p(crc_raw(init, D)), p = 8192*nt - L: undo the padding
-    pad = (-L) % 8192
+    # out = Z_p(crc_raw(init, D)), p = 8192*nt - (L + mis): undo the padding
+    pad = (-(L + mis)) % 8192
     for b in range(13):
         if (pad >> b) & 1:
             out = apply(ZINV_POW2[b], out)
