@@ -48,7 +48,7 @@ for s in $STEPS; do
         stop_if_fault $? "pmc_$ctr"
       done ;;
     configs)
-      timeout -k 10 600 python tools/bench_configs.py --configs C,Cu,D,E > "$OUT/configs.log" 2>&1
+      timeout -k 10 600 python tools/bench_configs.py --configs C,Cu,D,E,S > "$OUT/configs.log" 2>&1
       rc=$?
       if [ $rc -ne 0 ]; then echo "step configs rc=$rc (stop)" >> "$OUT/status.txt"; exit $rc; fi ;;
     *)
