@@ -17,10 +17,10 @@
 namespace subspace_amd {
 
 template <int WG>
-__global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int);
+__global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int, u32*);
 
 struct TileDesc;
-__global__ void crc32_ragged_count_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*);
+__global__ void crc32_ragged_count_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*);
 __global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, u64, u64, TileDesc*, u32*);
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
@@ -111,6 +111,7 @@ struct subspace_crc_ctx {
   int uniform_blocks = 0;  // 0 = one workgroup per CU
   int uniform_order = 0;   // tile order: 0 XCD-spread sweep, 1 per-workgroup region, 2 plain sweep, 3 XCD-grouped
   bool long_path = true;   // whole-8 KiB-piece uniform batches take crc32_long_kernel
+  u32* zero_word = nullptr;  // zeroed by the next uniform or ragged launch (slot mismatch count)
   u64* d_uoff = nullptr;  // offsets/lengths materialised for non-4K uniform batches
   u64* d_ulen = nullptr;
   u64 u_capacity = 0;
@@ -198,7 +199,9 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   if (rc) return rc;
   const u64 n1 = count + 1;
   crc32_ragged_count_kernel<<<(unsigned)((n1 + 255) / 256), 256, 0, st>>>(offsets, ostride, lengths, lstride, count,
-                                                                           init, final_xor, c->d_ntiles, out);
+                                                                           init, final_xor, c->d_ntiles, out,
+                                                                           c->zero_word);
+  c->zero_word = nullptr;
   HIP_TRY(hipGetLastError());
   size_t tmp = c->scan_tmp_bytes;
   HIP_TRY(ragged_scan(c->d_scan_tmp, tmp, c->d_ntiles, c->d_tbase, n1, st));
@@ -247,10 +250,19 @@ int check_slot_args(int32_t checksum_size, int32_t metadata_size, uint32_t mode)
   return SUBSPACE_CRC_OK;
 }
 
+// Payload kernels of a slot batch: the uniform or ragged launch zeroes the mismatch count
+// (c->zero_word) on the way; slot_finish memsets it only if neither ran.
+void want_zeroed(subspace_crc_ctx* c, u32* err) { c->zero_word = err; }
+bool was_zeroed(subspace_crc_ctx* c, u32* err) {
+  const bool z = err && c->zero_word == nullptr;
+  c->zero_word = nullptr;
+  return z;
+}
+
 int slot_finish(subspace_crc_ctx* c, const u64* slots, uint8_t* buf, u64 stride, const u64* sizes, u64 usize,
                 u64 count, int32_t cs, int32_t ms, u32 mode, u32* status, u32* err, hipStream_t st,
-                u32* crc_out = nullptr) {
-  if (err) HIP_TRY(hipMemsetAsync(err, 0, sizeof(u32), st));
+                u32* crc_out = nullptr, bool err_zeroed = false) {
+  if (err && !err_zeroed) HIP_TRY(hipMemsetAsync(err, 0, sizeof(u32), st));
   crc32_slot_finish_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(
       slots, buf, stride, sizes, usize, count, cs, ms, mode, c->d_crc0, c->d_tab, c->d_pow2, status, err, crc_out);
   HIP_TRY(hipGetLastError());
@@ -432,7 +444,8 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     const int ord = c->uniform_order;
 #define LAUNCH(WGV)                                                                                    \
   crc32_uniform4k_kernel<WGV><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(b, stride, count, c->d_tab,         \
-                                                                                c->d_laneops, init, final_xor, dev_out, ord)
+                                                                                c->d_laneops, init, final_xor, dev_out, ord,  \
+                                                                                c->zero_word)
     switch (wg) {
       case 256: LAUNCH(256); break;
       case 768: LAUNCH(768); break;
@@ -440,6 +453,7 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
       default: LAUNCH(512); break;
     }
 #undef LAUNCH
+    c->zero_word = nullptr;
     HIP_TRY(hipGetLastError());
     return SUBSPACE_CRC_OK;
   }
@@ -502,10 +516,12 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
   // payload CRCs from init 0 at absolute addresses (base 0; fields 1 and 2 of each record)
   const u64* rec = reinterpret_cast<const u64*>(dev_slots);
   const u64 cap = count * ((max_message_size + 15 + 8191) / 8192) + 1;
+  want_zeroed(c, dev_error_count);
   rc = ragged_run(c, nullptr, cap, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st);
+  const bool zeroed = was_zeroed(c, dev_error_count);
   if (rc) return rc;
   return slot_finish(c, rec, nullptr, 0, nullptr, 0, count, checksum_size, metadata_size, mode, dev_status,
-                     dev_error_count, st);
+                     dev_error_count, st, nullptr, zeroed);
 }
 
 }  // extern "C"
@@ -538,6 +554,7 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
   rc = ensure_slot_ws(c, count);
   if (rc) return rc;
   auto* buf = static_cast<uint8_t*>(dev_buffer);
+  want_zeroed(c, dev_error_count);
   if (dev_message_sizes) {
     slot_payload_offsets_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(slot_stride, prefix_size, count,
                                                                                 c->d_soff);
@@ -548,9 +565,10 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
     rc = subspace_crc32_batch_uniform(c, buf + prefix_size, slot_stride, message_size, count, 0u, 0u, c->d_crc0,
                                       st);
   }
+  const bool zeroed = was_zeroed(c, dev_error_count);
   if (rc) return rc;
   return slot_finish(c, nullptr, buf, slot_stride, dev_message_sizes, message_size, count, checksum_size,
-                     metadata_size, mode, dev_status, dev_error_count, st, dev_crc_out);
+                     metadata_size, mode, dev_status, dev_error_count, st, dev_crc_out, zeroed);
 }
 
 }  // namespace

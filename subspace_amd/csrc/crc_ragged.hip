@@ -61,11 +61,13 @@ __host__ __device__ inline u64 tiles_for(u64 s, u64 len) { return len ? (len + (
 // payload/size fields of subspace_crc_slot records).
 __global__ void crc32_ragged_count_kernel(const u64* __restrict__ offsets, u32 ostride,
                                           const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
-                                          u32 final_xor, u64* __restrict__ ntiles, u32* __restrict__ out) {
+                                          u32 final_xor, u64* __restrict__ ntiles, u32* __restrict__ out,
+                                          u32* __restrict__ zero_word) {
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (i > count) return;
   if (i == count) {
     ntiles[i] = 0;  // scan sentinel: tile_base[count] = total tiles
+    if (zero_word) *zero_word = 0u;  // a slot batch's mismatch count (no separate memset)
     return;
   }
   const u64 nt = tiles_for(offsets[i * ostride], lengths[i * lstride]);

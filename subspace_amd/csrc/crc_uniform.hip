@@ -29,9 +29,12 @@ template <int WG>
 __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __restrict__ base, u64 stride, u64 count,
                                                              const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                              u32 init, u32 final_xor, u32* __restrict__ out,
-                                                             int order) {
+                                                             int order, u32* __restrict__ zero_word) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
+  // a word the caller's next kernel accumulates into (a slot batch's mismatch count): zeroed
+  // here so the call needs no separate memset
+  if (zero_word != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0u;
 
   const int lane = threadIdx.x & 63;
   // wave-uniform (SGPR) wave index: keeps the tile loop a scalar loop, so hipcc's waitcnt
@@ -181,12 +184,12 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
 }
 
 template __global__ void crc32_uniform4k_kernel<256>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                     int);
+                                                     int, u32*);
 template __global__ void crc32_uniform4k_kernel<512>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                     int);
+                                                     int, u32*);
 template __global__ void crc32_uniform4k_kernel<768>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                     int);
+                                                     int, u32*);
 template __global__ void crc32_uniform4k_kernel<1024>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                     int);
+                                                     int, u32*);
 
 }  // namespace subspace_amd
