@@ -7,9 +7,20 @@
 // (publisher.cc:673, subscriber.h:274, user callbacks such as client_test.cc:5234)
 // keep calling, because a kernel launch per 4 KiB message would cost more than
 // the CRC itself. SubspaceCRC32C is the same function for the CRC-32C polynomial.
+//
+// On x86-64 CPUs with PCLMULQDQ (every current server part; checked at run time) the
+// 16-B-multiple body of an IEEE CRC of 64 bytes or more is folded with carry-less
+// multiplies (4 x 128-bit lanes, then one, then a Barrett reduction to 32 bits; the
+// published folding scheme for reflected CRCs, with the constants below derived for
+// 0xEDB88320), the remaining bytes by slice-by-16. tests/test_host_api.py checks every
+// boundary of the split against zlib.
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 
 #include "crc_math.h"
 
@@ -62,9 +73,66 @@ uint32_t crc_slice16(const Slice16& s, uint32_t crc, const uint8_t* data, size_t
   return crc;
 }
 
+#if defined(__x86_64__)
+// Raw-state IEEE CRC of len bytes (len >= 64, len % 16 == 0) by carry-less folding.
+// Folding constants, bit-reflected and shifted left by one (reflected-domain products):
+//   k1, k2 = x^(4*128+32), x^(4*128-32) mod P   (fold 4 x 128 bits by 512 bits)
+//   k3, k4 = x^(128+32),   x^(128-32)   mod P   (fold by 128 bits)
+//   k5     = x^64 mod P                          (128 -> 64 -> 32 bits)
+//   mu, p  = x^64 div P and P, reflected (33 bits), for the Barrett reduction.
+#define SUBSPACE_PCLMUL __attribute__((target("pclmul,sse4.1")))
+SUBSPACE_PCLMUL inline __m128i ld128(const uint8_t* q) { return _mm_loadu_si128(reinterpret_cast<const __m128i*>(q)); }
+SUBSPACE_PCLMUL inline __m128i fold128(__m128i x, __m128i k, __m128i next) {  // x * k (both halves) + next
+  return _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(x, k, 0x00), _mm_clmulepi64_si128(x, k, 0x11)), next);
+}
+
+SUBSPACE_PCLMUL uint32_t crc_pclmul(uint32_t crc, const uint8_t* p, size_t len) {
+  const __m128i k12 = _mm_set_epi64x(0x1c6e41596ll, 0x154442bd4ll);
+  const __m128i k34 = _mm_set_epi64x(0x0ccaa009ell, 0x1751997d0ll);
+  const __m128i k5 = _mm_set_epi64x(0, 0x163cd6124ll);
+  const __m128i mup = _mm_set_epi64x(0x1f7011641ll, 0x1db710641ll);
+  const __m128i mask32 = _mm_set_epi32(0, 0, 0, -1);
+  __m128i x1 = _mm_xor_si128(ld128(p), _mm_cvtsi32_si128((int)crc));
+  __m128i x2 = ld128(p + 16), x3 = ld128(p + 32), x4 = ld128(p + 48);
+  p += 64;
+  len -= 64;
+  for (; len >= 64; p += 64, len -= 64) {
+    x1 = fold128(x1, k12, ld128(p));
+    x2 = fold128(x2, k12, ld128(p + 16));
+    x3 = fold128(x3, k12, ld128(p + 32));
+    x4 = fold128(x4, k12, ld128(p + 48));
+  }
+  x1 = fold128(x1, k34, x2);
+  x1 = fold128(x1, k34, x3);
+  x1 = fold128(x1, k34, x4);
+  for (; len >= 16; p += 16, len -= 16) x1 = fold128(x1, k34, ld128(p));
+  // 128 -> 64 bits
+  x1 = _mm_xor_si128(_mm_clmulepi64_si128(x1, k34, 0x10), _mm_srli_si128(x1, 8));
+  // 64 -> 32 bits
+  x1 = _mm_xor_si128(_mm_clmulepi64_si128(_mm_and_si128(x1, mask32), k5, 0x00), _mm_srli_si128(x1, 4));
+  // Barrett reduction
+  __m128i t = _mm_clmulepi64_si128(_mm_and_si128(x1, mask32), mup, 0x10);
+  t = _mm_clmulepi64_si128(_mm_and_si128(t, mask32), mup, 0x00);
+  return (uint32_t)_mm_extract_epi32(_mm_xor_si128(x1, t), 1);
+}
+
+bool have_pclmul() {
+  static const bool ok = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+  return ok;
+}
+#endif
+
 }  // namespace
 
 extern "C" uint32_t SubspaceCRC32(uint32_t crc, const uint8_t* data, size_t length) {
+#if defined(__x86_64__)
+  if (length >= 64 && have_pclmul()) {
+    const size_t body = length & ~(size_t)15;
+    crc = crc_pclmul(crc, data, body);
+    data += body;
+    length -= body;
+  }
+#endif
   return crc_slice16(slice16(), crc, data, length);
 }
 

@@ -209,3 +209,22 @@ def test_drain_helper_builds_and_reports_no_device(lib):
         assert d["device"] is False and d["error"]
     else:
         assert r.returncode == 0 and d["failures"] == 0, r.stdout + r.stderr
+
+
+def test_host_crc_pclmul_boundaries(lib):
+    """SubspaceCRC32's carry-less-multiply body (inputs >= 64 B; 16-B multiples folded, the
+    rest by tables) against zlib around every boundary it has: 63/64/65 bytes, multiples of
+    16 and 64 +- 1, with raw input states, unaligned starts, and chained calls."""
+    import zlib
+    rng = np.random.default_rng(1664)
+    buf = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    lengths = sorted({n + d for n in (64, 80, 128, 192, 256, 1024, 4096, 65536) for d in (-17, -16, -1, 0, 1, 15, 16)})
+    for n in lengths:
+        for off in (0, 1, 7, 13):
+            s = int(rng.integers(0, 1 << 32))
+            d = buf[off:off + n]
+            want = (~zlib.crc32(d, (~s) & 0xFFFFFFFF)) & 0xFFFFFFFF
+            assert lib.SubspaceCRC32(s, d, n) == want, (n, off)
+    a, b = buf[:1000], buf[1000:5000]  # chaining: body, tail, body
+    st = lib.SubspaceCRC32(lib.SubspaceCRC32(0xFFFFFFFF, a, len(a)), b, len(b))
+    assert st == (~zlib.crc32(a + b)) & 0xFFFFFFFF
