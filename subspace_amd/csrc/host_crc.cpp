@@ -6,7 +6,8 @@
 // lives in crc_kernels.hip; this host function is what per-message callers
 // (publisher.cc:673, subscriber.h:274, user callbacks such as client_test.cc:5234)
 // keep calling, because a kernel launch per 4 KiB message would cost more than
-// the CRC itself. SubspaceCRC32C is the same function for the CRC-32C polynomial.
+// the CRC itself. SubspaceCRC32C is the same function for the CRC-32C polynomial (the
+// SSE4.2 crc32 instruction where the CPU has it, slice-by-16 otherwise).
 //
 // On x86-64 CPUs with PCLMULQDQ (every current server part; checked at run time) the
 // 16-B-multiple body of an IEEE CRC of 64 bytes or more is folded with carry-less
@@ -116,6 +117,25 @@ SUBSPACE_PCLMUL uint32_t crc_pclmul(uint32_t crc, const uint8_t* p, size_t len) 
   return (uint32_t)_mm_extract_epi32(_mm_xor_si128(x1, t), 1);
 }
 
+// CRC-32C with the SSE4.2 crc32 instruction (the same instruction the reference's
+// -msse4.2 build uses, client/checksum.cc:56-76): 8 bytes per step, raw state in and out.
+__attribute__((target("sse4.2"))) uint32_t crc32c_sse42(uint32_t crc, const uint8_t* p, size_t len) {
+  uint64_t c = crc;
+  for (; len >= 8; p += 8, len -= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    c = _mm_crc32_u64(c, v);
+  }
+  uint32_t c32 = (uint32_t)c;
+  for (; len; p++, len--) c32 = _mm_crc32_u8(c32, *p);
+  return c32;
+}
+
+bool have_sse42() {
+  static const bool ok = __builtin_cpu_supports("sse4.2");
+  return ok;
+}
+
 bool have_pclmul() {
   static const bool ok = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
   return ok;
@@ -139,5 +159,8 @@ extern "C" uint32_t SubspaceCRC32(uint32_t crc, const uint8_t* data, size_t leng
 // CRC-32C (Castagnoli), raw state in and out: the value a -msse4.2 / -march=native x86
 // build of the reference computes with _mm_crc32_u64/u32/u8 (client/checksum.cc:56-76).
 extern "C" uint32_t SubspaceCRC32C(uint32_t crc, const uint8_t* data, size_t length) {
+#if defined(__x86_64__)
+  if (have_sse42()) return crc32c_sse42(crc, data, length);
+#endif
   return crc_slice16(slice16c(), crc, data, length);
 }
