@@ -100,6 +100,15 @@ def cpu_baseline(batches_host: list[np.ndarray], seconds: float) -> dict:
             done += BATCH_BYTES
             i += 1
         sse = round(done / (time.perf_counter() - t0) / 2**30, 3)
+    # informational: the library's own host SubspaceCRC32 (PCLMULQDQ body) on one core, over
+    # whole 256 MiB batches (per-message calls would time Python's call overhead instead)
+    from subspace_amd import checksum
+    done, t0, i = 0, time.perf_counter(), 0
+    while time.perf_counter() - t0 < min(1.0, seconds / 4):
+        checksum.subspace_crc32(0xFFFFFFFF, batches_host[i % len(batches_host)])
+        done += BATCH_BYTES
+        i += 1
+    dropin = round(done / (time.perf_counter() - t0) / 2**30, 3)
     config_a = None  # BASELINE configs[0]: the per-message CPU path (tools/config_a.cpp)
     exe = ROOT / "tools" / "config_a"
     if exe.exists():
@@ -121,6 +130,9 @@ def cpu_baseline(batches_host: list[np.ndarray], seconds: float) -> dict:
     return {"value": round(rn, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "value_1core": round(r1, 3),
             "sse42_crc32c_value": sse,
+            "dropin_host_1core_value": dropin,
+            "dropin_host_note": "libsubspace_crc.so's host SubspaceCRC32 (bit-exact IEEE; PCLMULQDQ folding) on one "
+                                "core over the same batches; informational",
             "config_a": config_a,
             "sse42_crc32c_note": "client/checksum.cc:56-76 (-msse4.2 builds) restated on the same batches and "
                                  "threads: CRC-32C, NOT bit-exact with the IEEE parity path; informational",
