@@ -44,7 +44,8 @@ def main():
     for _ in range(3):
         ctx.crc32_ragged(buf[: int(total) + 64], d_off, d_len, cout)
     torch.cuda.synchronize()
-    print("ok", int(out[0].item()) & 0xFFFFFFFF, int(rout[0].item()) & 0xFFFFFFFF, int(total))
+    print("ok", int(out[0].item()) & 0xFFFFFFFF, int(rout[0].item()) & 0xFFFFFFFF, int(total), "C payload bytes",
+          int(lens.sum()))
     ctx.close()
 
 
