@@ -27,7 +27,7 @@ __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*,
                                     const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds, u32*, u32*, u64);
 __global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, const u64*, u32, u64, const u32*, const u32*,
                                           const u32*, u32, u32*);
-hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u64 nw, u64 nkmax, u32* out, u64 n,
+hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u64 nw, u64 nkmax, u32* tord, u32* out, u64 n,
                     hipStream_t stream);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, int, int, u32, const u32*,
                                          const u32*, const u32*, u32*, u32*, u32*);
@@ -102,6 +102,7 @@ struct subspace_crc_ctx {
   u64 ws_messages = 0;
   uint8_t* d_desc = nullptr;
   u32* d_tilecrc = nullptr;  // per-tile values, wave-major (desc_capacity + one tile per wave)
+  u32* d_tord = nullptr;     // the same values in tile order (the scan's input)
   u32* d_px = nullptr;       // their inclusive XOR-scan
   void* d_xscan_tmp = nullptr;
   size_t xscan_tmp_bytes = 0;
@@ -164,17 +165,19 @@ int ensure_ragged_ws(subspace_crc_ctx* c, u64 messages, u64 tiles) {
     (void)hipFree(c->d_desc);
     (void)hipFree(c->d_tilecrc);
     (void)hipFree(c->d_px);
+    (void)hipFree(c->d_tord);
     (void)hipFree(c->d_xscan_tmp);
     c->d_desc = nullptr;
-    c->d_tilecrc = c->d_px = nullptr;
+    c->d_tilecrc = c->d_px = c->d_tord = nullptr;
     c->d_xscan_tmp = nullptr;
     c->desc_capacity = 0;
     HIP_TRY(hipMalloc(&c->d_desc, tiles * kTileDescBytes));
     // wave-major: nw * ceil(tiles / nw) < tiles + nw entries (nw = waves of a persistent grid)
     HIP_TRY(hipMalloc(&c->d_tilecrc, (tiles + (u64)c->num_cus * (kRaggedWG / 64)) * sizeof(u32)));
     HIP_TRY(hipMalloc(&c->d_px, tiles * sizeof(u32)));
+    HIP_TRY(hipMalloc(&c->d_tord, tiles * sizeof(u32)));
     size_t tmp = 0;
-    HIP_TRY(xor_scan(nullptr, tmp, c->d_tilecrc, 1, tiles, c->d_px, tiles, nullptr));
+    HIP_TRY(xor_scan(nullptr, tmp, c->d_tilecrc, 1, tiles, c->d_tord, c->d_px, tiles, nullptr));
     HIP_TRY(hipMalloc(&c->d_xscan_tmp, tmp));
     c->xscan_tmp_bytes = tmp;
     c->desc_capacity = tiles;
@@ -205,7 +208,8 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   HIP_TRY(hipGetLastError());
   size_t tmp = c->scan_tmp_bytes;
   HIP_TRY(ragged_scan(c->d_scan_tmp, tmp, c->d_ntiles, c->d_tbase, n1, st));
-  crc32_ragged_desc_kernel<<<(unsigned)((cap + 255) / 256), 256, 0, st>>>(
+  // one wave per 1,024 tiles (kDescTilesPerWave), four waves per block
+  crc32_ragged_desc_kernel<<<(unsigned)((cap + 4095) / 4096), 256, 0, st>>>(
       offsets, ostride, lengths, lstride, c->d_tbase, count, cap, reinterpret_cast<TileDesc*>(c->d_desc),
       c->d_overflow);
   HIP_TRY(hipGetLastError());
@@ -222,7 +226,7 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   // (entries past the batch's real tile count are scanned but never read); the final
   // kernel undoes the last tile's zero padding and applies the final XOR
   size_t xtmp = c->xscan_tmp_bytes;
-  HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, nw, nkmax, c->d_px, cap, st));
+  HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, nw, nkmax, c->d_tord, c->d_px, cap, st));
   crc32_ragged_final_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(
       c->d_tbase, offsets, ostride, lengths, lstride, count, c->d_px, c->d_overflow, c->d_rops, final_xor, out);
   HIP_TRY(hipGetLastError());
@@ -387,6 +391,7 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_desc);
   (void)hipFree(c->d_tilecrc);
   (void)hipFree(c->d_px);
+  (void)hipFree(c->d_tord);
   (void)hipFree(c->d_xscan_tmp);
   (void)hipFree(c->d_overflow);
   (void)hipFree(c->d_uoff);
@@ -473,7 +478,7 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
         c->d_tilecrc, (u32)nkmax);
     HIP_TRY(hipGetLastError());
     size_t xtmp = c->xscan_tmp_bytes;
-    HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, nw, nkmax, c->d_px, tiles, st));
+    HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, nw, nkmax, c->d_tord, c->d_px, tiles, st));
     crc32_long_final_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(c->d_px, (u32)pieces, (u32)count,
                                                                               dev_out);
     HIP_TRY(hipGetLastError());

@@ -101,15 +101,44 @@ __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, u32 ostrid
 }
 
 // Per tile (up to `capacity`): its descriptor. Sets *overflow if the batch has more tiles.
-__global__ void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, u32 ostride,
-                                         const u64* __restrict__ lengths, u32 lstride,
-                                         const u64* __restrict__ tile_base, u64 count, u64 capacity,
-                                         TileDesc* __restrict__ desc, u32* __restrict__ overflow) {
+// Wave g covers tiles [g*kDescTilesPerWave, +kDescTilesPerWave): ONE binary search (the
+// same address in every lane) finds the message of its first tile; then per 64-tile window
+// lane l holds tile_base[m0 + l] (one coalesced load) and each lane finds its tile's message
+// with a 6-step shuffle search over those 64 bases. Only a window whose 64 candidates do not
+// reach a lane's tile (runs of zero-length messages) searches globally for that lane. A
+// search per tile (the previous form) cost 20 dependent loads per tile (0.25 ms on config C).
+constexpr u64 kDescTilesPerWave = 1024;
+__global__ __launch_bounds__(256) void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, u32 ostride,
+                                                                const u64* __restrict__ lengths, u32 lstride,
+                                                                const u64* __restrict__ tile_base, u64 count,
+                                                                u64 capacity, TileDesc* __restrict__ desc,
+                                                                u32* __restrict__ overflow) {
   const u64 total = tile_base[count];
-  const u64 tau = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tau == 0) *overflow = total > capacity ? 1u : 0u;
-  if (tau >= total || tau >= capacity) return;
-  desc[tau] = make_desc(offsets, ostride, lengths, lstride, tile_base, find_msg(tile_base, count, tau), tau);
+  const u64 limit = total < capacity ? total : capacity;
+  const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *overflow = total > capacity ? 1u : 0u;
+  const u64 t_begin = (((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * kDescTilesPerWave;
+  if (t_begin >= limit) return;  // wave-uniform
+  const u64 t_end = t_begin + kDescTilesPerWave < limit ? t_begin + kDescTilesPerWave : limit;
+  u64 m0 = find_msg(tile_base, count, t_begin);  // tile_base[m0] <= t_begin < tile_base[m0 + 1]
+  for (u64 t0 = t_begin; t0 < t_end; t0 += 64) {
+    const u64 tau = t0 + (u64)lane;
+    const u64 mc = m0 + (u64)lane;
+    // nondecreasing over lanes; tile_base[count] = total > every tile, past it: +inf
+    const u64 cand = mc <= count ? tile_base[mc] : ~(u64)0;
+    int lo = 0;  // last lane with cand <= tau (lane 0 always: cand_0 <= t0 <= tau)
+#pragma unroll
+    for (int step = 32; step; step >>= 1) {
+      const u64 v = __shfl(cand, lo + step, 64);
+      if (v <= tau) lo += step;
+    }
+    // lo < 63: cand_{lo+1} > tau, so m0 + lo is tau's message. lo = 63: not known whether
+    // message m0 + 64 starts at or before tau; search for it (mc <= count for all lanes here).
+    u64 m = m0 + (u64)lo;
+    if (lo == 63 && tau < t_end) m = find_msg(tile_base, count, tau);
+    if (tau < t_end) desc[tau] = make_desc(offsets, ostride, lengths, lstride, tile_base, m, tau);
+    m0 = __shfl(m, 63, 64);  // message of tile t0 + 63, the next window's first candidate
+  }
 }
 
 // ------------------------------------------------------------------ main kernel
@@ -362,11 +391,11 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
 }
 
 // hipcub scan wrappers: exclusive prefix sum of per-message tile counts; inclusive XOR
-// scan of per-tile values in tile order tau, gathered from the kernels' wave-major array
+// scan of per-tile values in tile order tau, transposed from the kernels' wave-major array
 // (tile tau = k*nw + w sits at w*nkmax + k). The flush stores are the reason for that
 // layout: 64 lanes storing tilecrc[tau] directly hit 64 lines 4*nw bytes apart, each
 // shared by waves of every XCD, and cost 8 % of the long kernel's time at config D
-// (r01aw); the gather costs the scan a few microseconds.
+// (r01aw); the transpose reads and writes 8 B per tile.
 hipError_t ragged_scan(void* temp, size_t& temp_bytes, const u64* in, u64* out, u64 n, hipStream_t stream) {
   return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, stream);
 }
@@ -375,18 +404,40 @@ struct XorOp {
   __host__ __device__ u32 operator()(u32 a, u32 b) const { return a ^ b; }
 };
 
-struct TileGather {
-  const u32* v;
-  u64 nw, nkmax;
-  __host__ __device__ u32 operator()(u64 tau) const { return v[(tau % nw) * nkmax + tau / nw]; }
-};
+// Wave-major tile values -> tile order: out[k*nw + w] = in[w*nkmax + k] for tau < n, through
+// 64 x 64 LDS tiles (reads along k and writes along w both coalesced). Gathering inside the
+// scan instead (a transform iterator, 64-bit div/mod per element and 4-B reads nkmax*4 B apart)
+// cost 185 us at config C's 15.4 M tiles (r01bt).
+__global__ __launch_bounds__(256) void tile_values_to_tau_order(const u32* __restrict__ in, u32 nw, u32 nkmax,
+                                                                u32* __restrict__ out, u64 n) {
+  __shared__ u32 t[64][65];
+  const u32 k0 = blockIdx.x * 64u, w0 = blockIdx.y * 64u;
+  const u32 x = threadIdx.x & 63u, y0 = threadIdx.x >> 6;
+#pragma unroll
+  for (u32 i = 0; i < 16u; i++) {  // row w0 + y, column k0 + x
+    const u32 y = y0 + 4u * i, w = w0 + y, k = k0 + x;
+    t[y][x] = (w < nw && k < nkmax) ? in[(u64)w * nkmax + k] : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (u32 i = 0; i < 16u; i++) {  // tau = (k0 + y)*nw + w0 + x
+    const u32 y = y0 + 4u * i, w = w0 + x, k = k0 + y;
+    const u64 tau = (u64)k * nw + w;
+    if (w < nw && k < nkmax && tau < n) out[tau] = t[x][y];
+  }
+}
 
-hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u64 nw, u64 nkmax, u32* out, u64 n,
+// Inclusive XOR-scan of the first n tile values in tile order. `tord` (n words) holds the
+// transposed values; a size query (temp == nullptr) launches nothing.
+hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u64 nw, u64 nkmax, u32* tord, u32* out, u64 n,
                     hipStream_t stream) {
-  hipcub::CountingInputIterator<u64> tau(0);
-  hipcub::TransformInputIterator<u32, TileGather, hipcub::CountingInputIterator<u64>> it(tau,
-                                                                                       TileGather{in, nw, nkmax});
-  return hipcub::DeviceScan::InclusiveScan(temp, temp_bytes, it, out, XorOp(), (int)n, stream);
+  if (temp != nullptr && n > 0) {
+    const dim3 grid((unsigned)((nkmax + 63) / 64), (unsigned)((nw + 63) / 64));
+    tile_values_to_tau_order<<<grid, 256, 0, stream>>>(in, (u32)nw, (u32)nkmax, tord, n);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipcub::DeviceScan::InclusiveScan(temp, temp_bytes, tord, out, XorOp(), (int)n, stream);
 }
 
 }  // namespace subspace_amd

@@ -194,3 +194,56 @@ def test_xcd_group_slot_is_a_bijection(wg, grid):
     xcd = {xcd_group_slot(b, grid, wid, wpb): b & 7 for b in range(grid) for wid in range(wpb)}
     for g in range(grid * wpb // 16):
         assert len({xcd[16 * g + i] for i in range(16)}) == 1
+
+
+def desc_kernel_messages(ntiles, capacity, per_wave=1024):
+    """Replays crc32_ragged_desc_kernel's message lookup: per wave, one search for its first
+    tile, then per 64-tile window a search over the 64 candidate bases tile_base[m0 + l]
+    (+inf past tile_base[count]), the global search when the last candidate is reached, and
+    the next window's m0 = lane 63's message. Returns {tile: message}."""
+    count = len(ntiles)
+    tb = np.concatenate([[0], np.cumsum(ntiles, dtype=np.int64)])  # tile_base, count + 1 entries
+    total = int(tb[count])
+    limit = min(total, capacity)
+
+    def find_msg(tau):  # last m < count with tb[m] <= tau
+        return int(np.searchsorted(tb[:count], tau, side="right")) - 1
+
+    got = {}
+    for t_begin in range(0, limit, per_wave):
+        t_end = min(t_begin + per_wave, limit)
+        m0 = find_msg(t_begin)
+        for t0 in range(t_begin, t_end, 64):
+            cand = [int(tb[m0 + l]) if m0 + l <= count else 1 << 62 for l in range(64)]
+            ms = []
+            for lane in range(64):
+                tau = t0 + lane
+                lo = 0
+                for step in (32, 16, 8, 4, 2, 1):
+                    if cand[lo + step] <= tau:
+                        lo += step
+                m = m0 + lo
+                if lo == 63 and tau < t_end:
+                    m = find_msg(tau)
+                if tau < t_end:
+                    got[tau] = m
+                ms.append(m)
+            m0 = ms[63]
+    return got, tb
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_desc_window_search_matches_binary_search(seed):
+    rng = np.random.default_rng(seed)
+    parts = []
+    for _ in range(40):
+        parts.append(np.zeros(int(rng.integers(0, 150)), dtype=np.int64))  # zero-tile runs
+        parts.append(rng.integers(1, 3, int(rng.integers(1, 100))))        # one/two-tile messages
+        parts.append(rng.integers(3, 300, int(rng.integers(0, 3))))        # multi-tile messages
+    ntiles = np.concatenate(parts).astype(np.int64)
+    total = int(ntiles.sum())
+    for capacity in (total, total - 37, 64 * 5 + 3):
+        got, tb = desc_kernel_messages(ntiles, capacity)
+        assert sorted(got) == list(range(min(total, capacity)))
+        for tau, m in got.items():
+            assert tb[m] <= tau < tb[m + 1], (capacity, tau, m)

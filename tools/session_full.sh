@@ -19,7 +19,7 @@ run configs 600 python tools/bench_configs.py --configs C,Cu,D,E
 run bench 400 python bench.py
 run bench_ev10 300 python bench.py --event-every 10 --no-cpu-baseline --no-e2e
 run bench_E 300 python bench.py --workload E --steps 20 --warmup 3
-run delaypat 300 ./tools/ubench/delaypat
+[ -x ./tools/ubench/delaypat ] && run delaypat 300 ./tools/ubench/delaypat
 cd /tmp
 run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-e2e
 run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_FETCH_SIZE -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-e2e
