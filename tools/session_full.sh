@@ -1,5 +1,6 @@
 #!/bin/bash
-# Full round session: tests -> configs -> bench variants -> design probe -> rocprof.
+# Full round session: tests -> bench -> rocprof -> configs -> bench E.
+# bench.py runs before the heavy configs: right after them it reads ~4 % low (r01bx).
 # Stops at the first failure / fault (no GPU work after a fault).
 set -u
 TAG=${1:-r01d}
@@ -15,13 +16,14 @@ run() {  # name, timeout, command...
 }
 run pytest 900 python -m pytest tests/ -x -q -m gpu -p no:cacheprovider --timeout 600 -rf
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-run configs 600 python tools/bench_configs.py --configs C,Cu,D,E
 run bench 400 python bench.py
 run bench_ev10 300 python bench.py --event-every 10 --no-cpu-baseline --no-e2e
-run bench_E 300 python bench.py --workload E --steps 20 --warmup 3
 [ -x ./tools/ubench/delaypat ] && run delaypat 300 ./tools/ubench/delaypat
 cd /tmp
-run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-e2e
+run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-e2e
 run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_FETCH_SIZE -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-e2e
 run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_WRITE_SIZE -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-e2e
+cd $GRAFT_REPO_ROOT
+run configs 600 python tools/bench_configs.py --configs C,Cu,D,E
+run bench_E 300 python bench.py --workload E --steps 20 --warmup 3
 echo done >> $OUT/status.txt
