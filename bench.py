@@ -64,8 +64,10 @@ def parse():
                     help="0 (default): one HIP event pair around the whole timed region, launch duration = "
                          "region / K (an event record between launches costs ~9 us per step on MI355X); "
                          "N > 0: also bracket every N-th launch (perturbs the timed region)")
-    ap.add_argument("--workload", default="B", choices=["B", "E"],
+    ap.add_argument("--workload", default="B", choices=["B", "C", "E"],
                     help="B: 65,536 x 4 KiB per GPU per step (weak scaling, default); "
+                         "C: 1 Mi ragged messages 64 B - 1 MiB (117.8 GB) in contiguous shards balanced by "
+                         "bytes (strong scaling) + RCCL gather; "
                          "E: 8 Mi x 4 KiB sharded round-robin over the GPUs (strong scaling) + RCCL gather")
     return ap.parse_args()
 
@@ -221,6 +223,24 @@ def main():
                              id_stride=world)
             bufs.append(b)
             outs.append(torch.empty(nmsg, dtype=torch.int32, device=dev))
+    elif args.workload == "C":
+        # this rank's contiguous, byte-balanced range of config C (one ragged call per step)
+        from subspace_amd import synth
+        goldens_c = json.loads((ROOT / "tests" / "golden" / "configs.json").read_text())["C"]
+        lengths_c = synth.ragged_lengths(synth.SEED_C, goldens_c["count"])
+        bounds_c = shard.ragged_ranges(lengths_c, world)
+        lo, hi = int(bounds_c[rank]), int(bounds_c[rank + 1])
+        local_len = lengths_c[lo:hi]
+        offs_c, arena_c = synth.packed_offsets(local_len, 64)
+        nmsg, nbuf = hi - lo, 1
+        b = torch.empty(int(arena_c) + 64, dtype=torch.uint8, device=dev)
+        d_off_c = torch.from_numpy(offs_c.astype(np.int64)).to(dev)
+        d_len_c = torch.from_numpy(local_len.astype(np.int64)).to(dev)
+        if nmsg:
+            gpu.fill_ragged(b, d_off_c, d_len_c, seed=synth.SEED_C, first_id=lo)
+        bufs.append(b)
+        outs.append(torch.empty(max(nmsg, 1), dtype=torch.int32, device=dev))
+        c_total_bytes = int(lengths_c.sum())
     else:
         total_e = 8 << 20
         nmsg, nbuf = shard.shard_count(total_e, rank, world), 1
@@ -228,7 +248,7 @@ def main():
         gpu.fill_uniform(b, MSG_BYTES, MSG_BYTES, nmsg, seed=0x5EED000E, first_id=rank, id_stride=world)
         bufs.append(b)
         outs.append(torch.empty(nmsg, dtype=torch.int32, device=dev))
-    step_bytes = nmsg * MSG_BYTES
+    step_bytes = int(local_len.sum()) if args.workload == "C" else nmsg * MSG_BYTES
     torch.cuda.synchronize()
 
     if nbuf % args.streams:  # workload E has one buffer: its steps stay on one stream
@@ -241,6 +261,10 @@ def main():
         # batch i % nbuf always runs on stream i % len(streams): nbuf is a multiple of the
         # stream count, so a batch's buffers are only ever used in order on one stream
         k = i % nbuf
+        if args.workload == "C":
+            if nmsg:
+                ctx.crc32_ragged(bufs[0], d_off_c, d_len_c, outs[0], stream=streams[0])
+            return
         ctx.crc32_uniform(bufs[k], MSG_BYTES, MSG_BYTES, nmsg, outs[k], stream=streams[i % len(streams)])
 
     settle = max(0, args.settle - args.warmup)
@@ -296,6 +320,19 @@ def main():
     if args.workload == "B" and world == 1:
         crc0 = outs[0].cpu().numpy().view(np.uint32)
         bitexact = hashlib.sha256(crc0.astype("<u4").tobytes()).hexdigest() == goldens["B"]["sha256_le_u32"]
+    if args.workload == "C":
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        if world > 1:
+            full = shard.gather_ragged_crcs(outs[0][:nmsg], bounds_c, rank, world, dist)
+        else:
+            full = outs[0][:nmsg].cpu().numpy().view(np.uint32)
+        gather_ms = (time.perf_counter() - tg) * 1e3
+        if rank == 0:
+            bitexact = hashlib.sha256(np.asarray(full, dtype="<u4").tobytes()).hexdigest() == \
+                goldens["C"]["sha256_le_u32"]
     if args.workload == "E":
         if world > 1:
             dist.barrier()
@@ -339,6 +376,15 @@ def main():
                         "message_bytes": MSG_BYTES, "batches_rotated": ROTATE,
                         "parallelism": f"independent message shards x{world}", "streams": args.streams}
             scaling = "weak"
+        elif args.workload == "C":
+            total_bytes = c_total_bytes * args.steps  # the whole 1 Mi-message batch per step
+            workload = {"workload": "C: 1 Mi messages, 64 B - 1 MiB log-uniform (117.8 GB), one CRC32 each, "
+                                    "contiguous shards balanced by bytes", "messages_total": int(bounds_c[-1]),
+                        "messages_rank0": nmsg, "bytes_total": c_total_bytes,
+                        "parallelism": f"contiguous byte-balanced shards x{world}, RCCL all_gather of CRCs "
+                                       "(untimed)",
+                        "gather_ms": round(gather_ms, 3) if gather_ms is not None else None}
+            scaling = "strong"
         else:
             total_bytes = (8 << 20) * MSG_BYTES * args.steps  # the whole 8 Mi batch per step
             workload = {"workload": "E: 8 Mi x 4 KiB payloads per step, round-robin over the GPUs, one CRC32 each",
@@ -371,7 +417,8 @@ def main():
             "bitexact_vs_golden": bitexact,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "subspace_amd::crc32_uniform4k_kernel<512>", "avg_launch_ms": round(avg_kern_ms, 4),
+                         "kernel": "subspace_amd::crc32_ragged_kernel<512> + prep (whole call)" if args.workload == "C"
+                         else "subspace_amd::crc32_uniform4k_kernel<512>", "avg_launch_ms": round(avg_kern_ms, 4),
                          "launch_ms_source": f"HIP event span of the timed region / K ({args.streams} stream(s), "
                                              "consecutive launches overlap when 2)",
                          "sampled_launch_ms": round(sampled_ms, 4) if sampled_ms else None},
