@@ -186,8 +186,9 @@ int ensure_ragged_ws(subspace_crc_ctx* c, u64 messages, u64 tiles) {
   return SUBSPACE_CRC_OK;
 }
 
+// Persistent grid: enough blocks for one wave per work unit, at most one block per CU.
 int grid_for(subspace_crc_ctx* c, u64 work_units, int waves_per_block) {
-  const u64 waves = (work_units + 0) ? work_units : 1;
+  const u64 waves = work_units ? work_units : 1;
   u64 blocks = (waves + waves_per_block - 1) / waves_per_block;
   if (blocks > (u64)c->num_cus) blocks = c->num_cus;
   return (int)(blocks ? blocks : 1);
