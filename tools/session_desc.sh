@@ -15,7 +15,9 @@ run() {  # name, timeout, command...
 run pytest 600 python -u -m pytest tests/ -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread -rf
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run configs 600 python tools/bench_configs.py --configs C,Cu,D,S
-for i in 1 2; do  # interleaved A/B on config C: previous (per-tile search) vs new descriptor kernel
+# interleaved A/B on config C: tools/ubench/probes/lib_olddesc.so = a build of the commit before
+# the descriptor change (git worktree + make; not kept)
+for i in 1 2; do
   SUBSPACE_CRC_PROBE_LIB=$PWD/tools/ubench/probes/lib_olddesc.so run C_old$i 300 python tools/bench_configs.py --configs C,Cu,D
   run C_new$i 300 python tools/bench_configs.py --configs C,Cu,D
 done
