@@ -13,6 +13,13 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "config: full-size BASELINE config parity (runs first)")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    """Full-size BASELINE config tests (tests/test_gpu_configs.py) run before everything
+    else, so that under `-x` a failure elsewhere cannot leave a config unexercised."""
+    items.sort(key=lambda it: 0 if it.get_closest_marker("config") else 1)  # stable
 
 
 @pytest.fixture(scope="session")
