@@ -1,24 +1,39 @@
 #!/usr/bin/env python3
 """Headline benchmark: device-resident batched CRC32 on MI355X.
 
-Workload (BASELINE.json configs[1], "config B"): 65,536 independent 4 KiB payloads,
-one CRC32 each, bit-exact with the reference's client/checksum.cc. One step = one
-launch of the batched kernel over one 256 MiB batch already resident in HBM. Four
-distinct batches are rotated so the 256 MiB Infinity Cache cannot serve re-reads
-(every step reads HBM). The payloads are synthetic (SURVEY.md 8d generator),
-generated on device before timing.
+Workload at N = 1 (BASELINE.json configs[1], "config B"): 65,536 independent 4 KiB
+payloads, one CRC32 each, bit-exact with the reference's client/checksum.cc. One step =
+one launch of the batched kernel over one 256 MiB batch already resident in HBM. Four
+distinct batches are rotated so the 256 MiB Infinity Cache cannot serve re-reads (every
+step reads HBM). Payloads are synthetic (SURVEY.md 8d generator), generated on device
+before timing. The same run also times configs C (1 Mi ragged messages), D (256 x 64 MiB,
+ragged and uniform API) and S (config B in the reference's slot layout: publish and
+verify), each checked bit-exact, under "configs".
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...    (one rank per GPU, weak scaling:
-                                                        every rank checksums its own
-                                                        65,536-message shard per step)
+Workload at N > 1 (BASELINE.json configs[4], "config E"): 8 Mi x 4 KiB payloads sharded
+round-robin over the GPUs (strong scaling), one RCCL all_gather of the 4-byte CRCs after
+the timed region (timed separately), the whole list checked against the fixture; rank 0
+then times the same 8 Mi batch alone on its GPU, and the line reports per-GPU value and
+efficiency = value / (N x that single-GPU rate).
 
-Prints ONE JSON line (rank 0). `value` = aggregate GiB/s over all ranks (bytes of all
-ranks / max-over-ranks time). `roofline` is for the CRC kernel itself (one HIP event
-pair around the K launches on their stream, / K; algorithmic bytes = 65,536 x 4,096 per
-launch).
-`cpu_baseline` times the oracle (a C restatement of the reference table path) on this
-host's cores over a bounded sample of the same batches.
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload B|C|E]
+      With N > 1 and no WORLD_SIZE in the environment, this process only spawns N ranks
+      (python -m torch.distributed.run, one process per GPU, RCCL) and exits with their
+      status; it never touches a GPU itself.
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+      The driver's form: WORLD_SIZE must equal --gpus (exit 2 otherwise).
+  python bench.py --gpus N --dry-run-cpu [--workload E|C|B]
+      The same spawn, shard, time and gather code on the CPU (gloo; each rank checksums its
+      shard with the library's host SubspaceCRC32 instead of the kernel) over small fixture
+      batches (E -> config B's 65,536 messages round-robin, C -> the first 2,048 messages
+      of C in byte-balanced ranges), checked against the fixture hash. For tests.
+
+Prints ONE JSON line (rank 0). `value` = aggregate GiB/s over all ranks (bytes of all ranks
+/ max-over-ranks time between barriers). `roofline` is for the dominant kernel (one HIP
+event pair around the K launches on their stream, / K). `cpu_baseline` times the oracle
+(a C restatement of the reference table path) on this host's cores over bounded samples
+of configs B, C, D and E (median of 5 runs each, 1 core and all cores available to the
+job).
 """
 from __future__ import annotations
 
@@ -26,6 +41,8 @@ import argparse
 import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -40,6 +57,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md chip table
 MSGS, MSG_BYTES = 65536, 4096
 BATCH_BYTES = MSGS * MSG_BYTES
 ROTATE = 4  # 4 x 256 MiB > the 256 MiB Infinity Cache: every step reads HBM
+E_COUNT = 8 << 20
+GOLD = json.loads((ROOT / "tests" / "golden" / "configs.json").read_text())
 
 
 def parse():
@@ -59,68 +78,64 @@ def parse():
     ap.add_argument("--streams", type=int, default=1, choices=[1, 2])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="budget for the CPU baseline legs")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="CPU baseline: runs per sample (median reported)")
     ap.add_argument("--event-every", type=int, default=0,
                     help="0 (default): one HIP event pair around the whole timed region, launch duration = "
                          "region / K (an event record between launches costs ~9 us per step on MI355X); "
                          "N > 0: also bracket every N-th launch (perturbs the timed region)")
-    ap.add_argument("--workload", default="B", choices=["B", "C", "E"],
-                    help="B: 65,536 x 4 KiB per GPU per step (weak scaling, default); "
+    ap.add_argument("--workload", default=None, choices=["B", "C", "E"],
+                    help="default B at 1 GPU, E at N > 1. "
+                         "B: 65,536 x 4 KiB per GPU per step (weak scaling); "
                          "C: 1 Mi ragged messages 64 B - 1 MiB (117.8 GB) in contiguous shards balanced by "
                          "bytes (strong scaling) + RCCL gather; "
                          "E: 8 Mi x 4 KiB sharded round-robin over the GPUs (strong scaling) + RCCL gather")
+    ap.add_argument("--configs", default=None,
+                    help="secondary configs timed after the headline at N = 1 (comma list of C, Cu, D, Du, S; "
+                         "default C,D,Du,S with workload B, none otherwise; 'none' disables)")
+    ap.add_argument("--config-iters", type=int, default=20)
+    ap.add_argument("--no-solo", action="store_true", help="N > 1: skip rank 0's single-GPU reference leg")
+    ap.add_argument("--dry-run-cpu", action="store_true",
+                    help="CPU + gloo rehearsal of the spawn/shard/gather path (host SubspaceCRC32), for tests")
     return ap.parse_args()
 
 
-def cpu_baseline(batches_host: list[np.ndarray], seconds: float) -> dict:
-    """Oracle (reference table path restated in C) on this host's cores."""
-    sys.path.insert(0, str(ROOT / "tests"))
-    import _oracle
-    orc = _oracle.load()
-    offs = np.arange(MSGS, dtype=np.uint64) * np.uint64(MSG_BYTES)
-    lens = np.full(MSGS, MSG_BYTES, dtype=np.uint64)
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+def die(msg: str, code: int = 2):
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+    sys.exit(code)
 
-    def rate(nthreads, budget):
-        done, t0 = 0, time.perf_counter()
-        i = 0
-        while True:
-            orc.crc32_batch(batches_host[i % len(batches_host)], offs, lens, threads=nthreads)
-            done += BATCH_BYTES
-            i += 1
-            if time.perf_counter() - t0 >= budget:
-                break
-        return done / (time.perf_counter() - t0) / 2**30, done
 
-    r1, b1 = rate(1, seconds / 2)
-    rn, bn = rate(threads, seconds / 2)
-    sse = None
-    if orc.has_sse42():  # informational: the reference's -msse4.2 path computes CRC-32C
-        done, t0, i = 0, time.perf_counter(), 0
-        while time.perf_counter() - t0 < min(1.0, seconds / 4):
-            orc.crc32c_sse42_batch(batches_host[i % len(batches_host)], offs, lens, threads=threads)
-            done += BATCH_BYTES
-            i += 1
-        sse = round(done / (time.perf_counter() - t0) / 2**30, 3)
-    # informational: the library's own host SubspaceCRC32 (PCLMULQDQ body) on one core, over
-    # whole 256 MiB batches (per-message calls would time Python's call overhead instead)
-    from subspace_amd import checksum
-    done, t0, i = 0, time.perf_counter(), 0
-    while time.perf_counter() - t0 < min(1.0, seconds / 4):
-        checksum.subspace_crc32(0xFFFFFFFF, batches_host[i % len(batches_host)])
-        done += BATCH_BYTES
-        i += 1
-    dropin = round(done / (time.perf_counter() - t0) / 2**30, 3)
-    config_a = None  # BASELINE configs[0]: the per-message CPU path (tools/config_a.cpp)
-    exe = ROOT / "tools" / "config_a"
-    if exe.exists():
-        import subprocess
-        try:
-            r = subprocess.run([str(exe), "20000", str(ROOT / "oracle" / "liboracle_crc.so")], capture_output=True,
-                               text=True, timeout=120)
-            config_a = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None
-        except (subprocess.SubprocessError, ValueError, IndexError):
-            config_a = None
+# ------------------------------------------------------------------------------ launch
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: start N rank processes (one per GPU) through
+    torch.distributed.run as a child and return its exit status. This process never
+    initialises a GPU (no exec from a GPU-initialised process)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def digest(crcs) -> str:
+    return hashlib.sha256(np.asarray(crcs, dtype="<u4").tobytes()).hexdigest()
+
+
+# ------------------------------------------------------------------------------ CPU baseline
+def cpu_share() -> dict:
+    """Cores this job may use: the process affinity set, limited to the job's CPU share
+    where the environment states one (OMP_NUM_THREADS: 16 per GPU on the gpurun boxes,
+    whose nproc shows the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    share = int(omp) if omp and omp.isdigit() and int(omp) > 0 else aff
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -129,21 +144,124 @@ def cpu_baseline(batches_host: list[np.ndarray], seconds: float) -> dict:
                 break
     except OSError:
         pass
-    return {"value": round(rn, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "value_1core": round(r1, 3),
+    return {"cores": max(1, min(aff, share)), "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": omp, "cpu_model": cpu_model}
+
+
+def cpu_samples(dev, bufs_b) -> dict:
+    """Host copies of bounded samples of configs B, C, D and E (the same generator as the
+    device batches): name -> (arena, offsets, lengths, description)."""
+    import torch
+    from subspace_amd import gpu, synth
+    out = {}
+    offs = np.arange(MSGS, dtype=np.uint64) * np.uint64(MSG_BYTES)
+    lens = np.full(MSGS, MSG_BYTES, dtype=np.uint64)
+    out["B"] = (bufs_b[0].cpu().numpy(), offs, lens, "config B's batch 0 (65,536 x 4 KiB, 256 MiB)")
+    # C: the first messages of config C up to 256 MiB, 64-B aligned packing as in the GPU run
+    lc = synth.ragged_lengths(synth.SEED_C, 4096)
+    k = int(np.searchsorted(np.cumsum(lc, dtype=np.uint64), np.uint64(256 << 20), side="right"))
+    lc = lc[:k]
+    oc, tot = synth.packed_offsets(lc, 64)
+    b = torch.empty(tot + 64, dtype=torch.uint8, device=dev)
+    gpu.fill_ragged(b, torch.from_numpy(oc.view(np.int64)).to(dev), torch.from_numpy(lc.view(np.int64)).to(dev),
+                    seed=synth.SEED_C)
+    out["C"] = (b.cpu().numpy(), oc, lc, f"config C's first {k:,} messages ({int(lc.sum()) / 2**20:.0f} MiB)")
+    # D: 16 of the 256 x 64 MiB messages (one CRC per message is serial on a CPU, so the
+    # all-core leg needs >= one message per worker; the 1-core leg times the first 4)
+    b = torch.empty(16 << 26, dtype=torch.uint8, device=dev)
+    gpu.fill_uniform(b, 64 << 20, 64 << 20, 16, seed=synth.SEED_D)
+    out["D"] = (b.cpu().numpy(), np.arange(16, dtype=np.uint64) << np.uint64(26), np.full(16, 64 << 20, np.uint64),
+                "config D's first 16 x 64 MiB messages (1-core leg: the first 4)")
+    # E: 65,536 messages of shard 0 of 8 (ids 0, 8, 16, ...)
+    b = torch.empty(BATCH_BYTES, dtype=torch.uint8, device=dev)
+    gpu.fill_uniform(b, MSG_BYTES, MSG_BYTES, MSGS, seed=synth.SEED_E, first_id=0, id_stride=8)
+    out["E"] = (b.cpu().numpy(), offs, lens, "65,536 messages of config E's shard 0 of 8 (256 MiB)")
+    del b
+    torch.cuda.empty_cache()
+    return out
+
+
+def cpu_baseline(samples: dict, runs: int) -> dict:
+    """The oracle (reference table path restated in C) on this host's cores: per sample,
+    the median of `runs` runs on 1 core and on all cores of the job's share (one pinned
+    worker per core, round-robin message partition, sample pages first touched by their
+    worker; BASELINE.md "CPU-baseline plan")."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _oracle
+    orc = _oracle.load()
+    share = cpu_share()
+    threads = share["cores"]
+    per, pinned = {}, 0
+    for name, (arena, offs, lens, desc) in samples.items():
+        nbytes = int(lens.sum())
+        ref = orc.crc32_batch(arena, offs, lens, threads=threads)
+        k1 = min(len(offs), 4) if name == "D" else len(offs)  # 1-core leg: ~256 MiB
+        bytes_1 = int(lens[:k1].sum())
+        orc.crc32_batch_pinned(arena, offs[:k1], lens[:k1], threads=1)  # warm (page faults, clocks)
+        t1 = []
+        for _ in range(runs):
+            t = time.perf_counter()
+            got, _ = orc.crc32_batch_pinned(arena, offs[:k1], lens[:k1], threads=1)
+            t1.append(time.perf_counter() - t)
+        touched = orc.first_touch_copy(arena, offs, lens, threads)
+        tn = []
+        for _ in range(runs):
+            t = time.perf_counter()
+            got_n, pinned = orc.crc32_batch_pinned(touched, offs, lens, threads=threads)
+            tn.append(time.perf_counter() - t)
+        assert np.array_equal(got, ref[:k1]) and np.array_equal(got_n, ref)
+        per[name] = {"bytes": nbytes, "sample": desc,
+                     "value_1core": round(bytes_1 / float(np.median(t1)) / 2**30, 3),
+                     "value_all_cores": round(nbytes / float(np.median(tn)) / 2**30, 3)}
+        del touched
+    arena_b, offs_b, lens_b, _ = samples["B"]
+    sse = None
+    if orc.has_sse42():  # informational: the reference's -msse4.2 path computes CRC-32C
+        ts = []
+        for _ in range(runs):
+            t = time.perf_counter()
+            orc.crc32c_sse42_batch(arena_b, offs_b, lens_b, threads=threads)
+            ts.append(time.perf_counter() - t)
+        sse = round(BATCH_BYTES / float(np.median(ts)) / 2**30, 3)
+    # informational: the library's own host SubspaceCRC32 (PCLMULQDQ body) on one core, over
+    # the whole 256 MiB batch (per-message calls would time Python's call overhead instead)
+    from subspace_amd import checksum
+    ts = []
+    for _ in range(runs):
+        t = time.perf_counter()
+        checksum.subspace_crc32(0xFFFFFFFF, arena_b)
+        ts.append(time.perf_counter() - t)
+    dropin = round(BATCH_BYTES / float(np.median(ts)) / 2**30, 3)
+    config_a = None  # BASELINE configs[0]: the per-message CPU path (tools/config_a.cpp)
+    exe = ROOT / "tools" / "config_a"
+    if exe.exists():
+        try:
+            r = subprocess.run([str(exe), "20000", str(ROOT / "oracle" / "liboracle_crc.so")], capture_output=True,
+                               text=True, timeout=120)
+            config_a = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None
+        except (subprocess.SubprocessError, ValueError, IndexError):
+            config_a = None
+    return {"value": per["B"]["value_all_cores"], "unit": "GiB/s", "cores": threads, "kind": "port",
+            "value_1core": per["B"]["value_1core"],
+            "nproc": share["nproc"], "affinity_cpus": share["affinity_cpus"],
+            "omp_num_threads": share["omp_num_threads"], "workers_pinned": pinned,
+            "cores_note": "cores = the job's CPU share: the affinity set, limited by OMP_NUM_THREADS where set "
+                          "(16 per GPU on the gpurun boxes, where nproc counts the whole machine)",
+            "configs": per,
             "sse42_crc32c_value": sse,
+            "sse42_crc32c_note": "client/checksum.cc:56-76 (-msse4.2 builds) restated on config B's sample and "
+                                 "the same threads: CRC-32C, NOT bit-exact with the IEEE parity path; informational",
             "dropin_host_1core_value": dropin,
             "dropin_host_note": "libsubspace_crc.so's host SubspaceCRC32 (bit-exact IEEE; PCLMULQDQ folding) on one "
-                                "core over the same batches; informational",
+                                "core over config B's sample; informational",
             "config_a": config_a,
-            "sse42_crc32c_note": "client/checksum.cc:56-76 (-msse4.2 builds) restated on the same batches and "
-                                 "threads: CRC-32C, NOT bit-exact with the IEEE parity path; informational",
-            "sample": f"config-B batches (65,536 x 4 KiB, host copies of the device batches): "
-                      f"{bn / 2**30:.2f} GiB on {threads} threads, {b1 / 2**30:.2f} GiB on 1 thread; "
-                      f"oracle/crc32_oracle.c byte-table loop (reference client/checksum.cc:125-130), "
-                      f"gcc -O2, CPU: {cpu_model}"}
+            "sample": f"bounded samples of configs B, C, D, E (~256 MiB each, host copies of device-generated "
+                      f"batches), median of {runs} runs each on 1 core and on {threads} pinned cores; "
+                      f"oracle/crc32_oracle.c byte-table loop (reference client/checksum.cc:125-130), gcc -O2, "
+                      f"CPU: {share['cpu_model']}; value = config B on all cores"}
 
 
+# ------------------------------------------------------------------------------ end to end
 def end_to_end(ctx, gpu) -> dict:
     from subspace_amd import slots
     stride = slots.slot_stride(MSG_BYTES)  # PrefixSize(64) + Aligned64(4096) = 4160
@@ -190,94 +308,105 @@ def end_to_end(ctx, gpu) -> dict:
                     "zero-copy over PCIe"}
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-    from subspace_amd import gpu
+# ------------------------------------------------------------------------------ workloads
+class Workload:
+    """One rank's share of a headline workload on its GPU: buffers, one step, the
+    bit-exactness check. world/rank may differ from the job's (rank 0's solo leg)."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    if world > 1:
-        torch.cuda.set_device(local)
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    ctx = gpu.CrcContext(local)
-    stream = torch.cuda.current_stream()
+    def __init__(self, name, ctx, dev, world, rank):
+        import torch
+        from subspace_amd import gpu, shard, synth
+        self.name, self.ctx, self.world, self.rank = name, ctx, world, rank
+        self.bufs, self.outs = [], []
+        if name == "B":  # ROTATE distinct 256 MiB batches per rank (message ids r, r + world, ...)
+            self.nmsg = MSGS
+            for k in range(ROTATE):
+                b = torch.empty(MSGS * MSG_BYTES, dtype=torch.uint8, device=dev)
+                gpu.fill_uniform(b, MSG_BYTES, MSG_BYTES, MSGS, seed=synth.SEED_B, first_id=rank + k * MSGS * world,
+                                 id_stride=world)
+                self.bufs.append(b)
+                self.outs.append(torch.empty(MSGS, dtype=torch.int32, device=dev))
+            self.step_bytes = MSGS * MSG_BYTES
+            self.total_bytes = self.step_bytes * world  # weak scaling: every rank its own batch
+        elif name == "C":  # this rank's contiguous, byte-balanced range (one ragged call per step)
+            lengths = synth.ragged_lengths(synth.SEED_C, GOLD["C"]["count"])
+            self.bounds = shard.ragged_ranges(lengths, world)
+            lo, hi = int(self.bounds[rank]), int(self.bounds[rank + 1])
+            local = lengths[lo:hi]
+            offs, arena = synth.packed_offsets(local, 64)
+            self.nmsg = hi - lo
+            b = torch.empty(int(arena) + 64, dtype=torch.uint8, device=dev)
+            self.d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+            self.d_len = torch.from_numpy(local.astype(np.int64)).to(dev)
+            if self.nmsg:
+                gpu.fill_ragged(b, self.d_off, self.d_len, seed=synth.SEED_C, first_id=lo)
+            self.bufs.append(b)
+            self.outs.append(torch.empty(max(self.nmsg, 1), dtype=torch.int32, device=dev))
+            self.step_bytes = int(local.sum())
+            self.total_bytes = int(lengths.sum())
+        else:  # E: this rank's round-robin shard of the 8 Mi-message batch, one buffer
+            self.nmsg = shard.shard_count(E_COUNT, rank, world)
+            b = torch.empty(self.nmsg * MSG_BYTES, dtype=torch.uint8, device=dev)
+            gpu.fill_uniform(b, MSG_BYTES, MSG_BYTES, self.nmsg, seed=synth.SEED_E, first_id=rank, id_stride=world)
+            self.bufs.append(b)
+            self.outs.append(torch.empty(self.nmsg, dtype=torch.int32, device=dev))
+            self.step_bytes = self.nmsg * MSG_BYTES
+            self.total_bytes = E_COUNT * MSG_BYTES
+        self.nbuf = len(self.bufs)
 
-    from subspace_amd import shard
-
-    # ---- inputs. B: ROTATE distinct 256 MiB batches per rank (message ids r, r+world, ...).
-    #      E: this rank's round-robin shard of the 8 Mi-message batch, one buffer.
-    bufs, outs = [], []
-    if args.workload == "B":
-        nmsg, nbuf = MSGS, ROTATE
-        for k in range(nbuf):
-            b = torch.empty(nmsg * MSG_BYTES, dtype=torch.uint8, device=dev)
-            gpu.fill_uniform(b, MSG_BYTES, MSG_BYTES, nmsg, seed=0x5EED000B, first_id=rank + k * nmsg * world,
-                             id_stride=world)
-            bufs.append(b)
-            outs.append(torch.empty(nmsg, dtype=torch.int32, device=dev))
-    elif args.workload == "C":
-        # this rank's contiguous, byte-balanced range of config C (one ragged call per step)
-        from subspace_amd import synth
-        goldens_c = json.loads((ROOT / "tests" / "golden" / "configs.json").read_text())["C"]
-        lengths_c = synth.ragged_lengths(synth.SEED_C, goldens_c["count"])
-        bounds_c = shard.ragged_ranges(lengths_c, world)
-        lo, hi = int(bounds_c[rank]), int(bounds_c[rank + 1])
-        local_len = lengths_c[lo:hi]
-        offs_c, arena_c = synth.packed_offsets(local_len, 64)
-        nmsg, nbuf = hi - lo, 1
-        b = torch.empty(int(arena_c) + 64, dtype=torch.uint8, device=dev)
-        d_off_c = torch.from_numpy(offs_c.astype(np.int64)).to(dev)
-        d_len_c = torch.from_numpy(local_len.astype(np.int64)).to(dev)
-        if nmsg:
-            gpu.fill_ragged(b, d_off_c, d_len_c, seed=synth.SEED_C, first_id=lo)
-        bufs.append(b)
-        outs.append(torch.empty(max(nmsg, 1), dtype=torch.int32, device=dev))
-        c_total_bytes = int(lengths_c.sum())
-    else:
-        total_e = 8 << 20
-        nmsg, nbuf = shard.shard_count(total_e, rank, world), 1
-        b = torch.empty(nmsg * MSG_BYTES, dtype=torch.uint8, device=dev)
-        gpu.fill_uniform(b, MSG_BYTES, MSG_BYTES, nmsg, seed=0x5EED000E, first_id=rank, id_stride=world)
-        bufs.append(b)
-        outs.append(torch.empty(nmsg, dtype=torch.int32, device=dev))
-    step_bytes = int(local_len.sum()) if args.workload == "C" else nmsg * MSG_BYTES
-    torch.cuda.synchronize()
-
-    if nbuf % args.streams:  # workload E has one buffer: its steps stay on one stream
-        args.streams = 1
-    streams = [stream] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
-    for s2 in streams[1:]:
-        s2.wait_stream(stream)
-
-    def step(i):
+    def step(self, i, streams):
         # batch i % nbuf always runs on stream i % len(streams): nbuf is a multiple of the
         # stream count, so a batch's buffers are only ever used in order on one stream
-        k = i % nbuf
-        if args.workload == "C":
-            if nmsg:
-                ctx.crc32_ragged(bufs[0], d_off_c, d_len_c, outs[0], stream=streams[0])
+        k = i % self.nbuf
+        if self.name == "C":
+            if self.nmsg:
+                self.ctx.crc32_ragged(self.bufs[0], self.d_off, self.d_len, self.outs[0], stream=streams[0])
             return
-        ctx.crc32_uniform(bufs[k], MSG_BYTES, MSG_BYTES, nmsg, outs[k], stream=streams[i % len(streams)])
+        self.ctx.crc32_uniform(self.bufs[k], MSG_BYTES, MSG_BYTES, self.nmsg, self.outs[k],
+                               stream=streams[i % len(streams)])
 
-    settle = max(0, args.settle - args.warmup)
-    for i in range(settle):
-        step(i)
-    for i in range(args.warmup):
-        step(i)
+    def check(self, dist):
+        """(bit-exact vs the fixture on rank 0, gather ms). Collective when world > 1: the
+        4-byte CRCs of every rank are all_gathered to global order and the whole list is
+        compared with the fixture (B: each rank's batch 0 is a distinct id set, so at
+        world 1 it is exactly config B)."""
+        import torch
+        from subspace_amd import shard
+        if self.name == "B":
+            if self.world > 1:
+                return None, None
+            return digest(self.outs[0].cpu().numpy().view(np.uint32)) == GOLD["B"]["sha256_le_u32"], None
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        if self.world > 1 and self.name == "C":
+            full = shard.gather_ragged_crcs(self.outs[0][:self.nmsg], self.bounds, self.rank, self.world, dist)
+        elif self.world > 1:
+            full = shard.gather_crcs(self.outs[0], E_COUNT, self.rank, self.world, dist)
+        else:
+            full = self.outs[0][:self.nmsg].cpu().numpy().view(np.uint32)
+        gather_ms = (time.perf_counter() - tg) * 1e3
+        ok = digest(full) == GOLD[self.name]["sha256_le_u32"] if full is not None else None
+        return ok, gather_ms
+
+    def free(self):
+        self.bufs, self.outs = [], []
+
+
+def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0):
+    """W untimed warm-up steps (after settle launches), then EXACTLY `steps` steps between
+    barrier + synchronize on both sides. Returns (max-over-ranks seconds, HIP-event span of
+    the region / steps in ms, sampled per-launch ms or None)."""
+    import torch
+    stream = streams[0]
+    for i in range(max(0, settle - warmup)):
+        wl.step(i, streams)
+    for i in range(warmup):
+        wl.step(i, streams)
     torch.cuda.synchronize()
-
-    # ---- timed region: K steps, barrier + sync on both sides, max over ranks
-    every = args.event_every
     ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for i in range(0, args.steps, every)} if every > 0 else {}
+          for i in range(0, steps, event_every)} if event_every > 0 else {}
     region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     if world > 1:
         dist.barrier()
@@ -286,11 +415,11 @@ def main():
     region[0].record(stream)
     for s2 in streams[1:]:
         s2.wait_stream(stream)  # every stream starts after the region's first event
-    for i in range(args.steps):
+    for i in range(steps):
         e = ev.get(i)
         if e:
             e[0].record(stream)
-        step(i)
+        wl.step(i, streams)
         if e:
             e[1].record(stream)
     for s2 in streams[1:]:
@@ -301,62 +430,308 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=stream.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # Launch interval of the CRC kernel: the HIP-event span of the K back-to-back launches /
-    # K (events on the first stream, joined with the second). With two streams consecutive
-    # launches overlap, so this effective interval is shorter than rocprofv3's per-dispatch
-    # duration (which then counts the overlapped part twice); with one stream it includes
-    # the inter-launch gaps.
-    avg_kern_ms = region[0].elapsed_time(region[1]) / args.steps
-    sampled_ms = float(np.mean([a.elapsed_time(b) for a, b in ev.values()])) if ev else None
+    avg_ms = region[0].elapsed_time(region[1]) / steps
+    sampled = float(np.mean([a.elapsed_time(b) for a, b in ev.values()])) if ev else None
+    return elapsed, avg_ms, sampled
 
-    # ---- bit-exactness of what was timed. B at world 1: batch 0 is exactly config B.
-    #      E: gather every rank's CRCs to rank 0 over RCCL (timed separately) and compare the
-    #      whole 8 Mi list with the fixture.
-    goldens = json.loads((ROOT / "tests" / "golden" / "configs.json").read_text())
-    bitexact, gather_ms = None, None
-    if args.workload == "B" and world == 1:
-        crc0 = outs[0].cpu().numpy().view(np.uint32)
-        bitexact = hashlib.sha256(crc0.astype("<u4").tobytes()).hexdigest() == goldens["B"]["sha256_le_u32"]
-    if args.workload == "C":
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        if world > 1:
-            full = shard.gather_ragged_crcs(outs[0][:nmsg], bounds_c, rank, world, dist)
-        else:
-            full = outs[0][:nmsg].cpu().numpy().view(np.uint32)
-        gather_ms = (time.perf_counter() - tg) * 1e3
-        if rank == 0:
-            bitexact = hashlib.sha256(np.asarray(full, dtype="<u4").tobytes()).hexdigest() == \
-                goldens["C"]["sha256_le_u32"]
-    if args.workload == "E":
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        if world > 1:
-            full = shard.gather_crcs(outs[0], 8 << 20, rank, world, dist)
-        else:
-            full = outs[0].cpu().numpy().view(np.uint32)
-        gather_ms = (time.perf_counter() - tg) * 1e3
-        if rank == 0:
-            bitexact = hashlib.sha256(np.asarray(full, dtype="<u4").tobytes()).hexdigest() == \
-                goldens["E"]["sha256_le_u32"]
 
-    # ---- end-to-end from host shared-memory slots (not `value`): config B in the reference's
-    #      channel layout (65,536 slots of PrefixSize 64 + 4 KiB, stride 4,160) in pinned host
-    #      memory; subspace_crc32_host_slots streams it to the GPU in ~32 MiB chunks (copies
-    #      overlap kernels) and writes flag + checksum back into every host prefix.
+# ------------------------------------------------------------------------------ secondary configs
+def time_calls(fn, iters, warm_ms=60.0):
+    """ms per call: one HIP event pair around `iters` back-to-back calls (after >= warm_ms of
+    warm-up calls), / iters -- the headline's timing rule."""
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < warm_ms:
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def config_line(nbytes, ms, bitexact, kernel, extra=None):
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    line = {"value": round(nbytes / (ms * 1e-3) / 2**30, 1), "unit": "GiB/s", "bytes": int(nbytes),
+            "ms_per_call": round(ms, 4), "pct_of_hbm_peak": round(100 * gbs / HBM_PEAK_GBS, 2),
+            "bitexact_vs_golden": bitexact,
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kernel,
+                         "launch_ms_source": "HIP event span of back-to-back calls / calls (the whole C-ABI call: "
+                                             "prep kernels + CRC kernel + combine)"}}
+    if extra:
+        line.update(extra)
+    return line
+
+
+def secondary_configs(ctx, dev, names, iters) -> dict:
+    """Configs C, C unaligned, D (ragged API), D (uniform API: long-message kernel) and S
+    (slot publish / verify) through the production C ABI, each checked bit-exact."""
+    import torch
+    from subspace_amd import gpu, slots, synth
+    res = {}
+
+    def u64t(a):
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(dev)
+
+    for name in names:
+        if name in ("C", "Cu"):
+            lengths = synth.ragged_lengths(synth.SEED_C, GOLD["C"]["count"])
+            offsets, total = synth.packed_offsets(lengths, 1 if name == "Cu" else 64)
+            buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+            d_off, d_len = u64t(offsets), u64t(lengths)
+            gpu.fill_ragged(buf, d_off, d_len, seed=synth.SEED_C)
+            out = torch.empty(len(lengths), dtype=torch.int32, device=dev)
+            ms = time_calls(lambda: ctx.crc32_ragged(buf, d_off, d_len, out), iters)
+            ok = digest(out.cpu().numpy().view(np.uint32)) == GOLD["C"]["sha256_le_u32"]
+            res[name] = config_line(int(lengths.sum()), ms, ok, "subspace_crc32_batch (ragged kernel)", {
+                "workload": "C: 1 Mi messages, 64 B - 1 MiB log-uniform, " +
+                            ("packed unaligned" if name == "Cu" else "64-B aligned offsets"),
+                "messages": len(lengths)})
+            del buf, d_off, d_len, out
+        elif name in ("D", "Du"):
+            n, L = GOLD["D"]["count"], 64 << 20
+            buf = torch.empty(n * L, dtype=torch.uint8, device=dev)
+            gpu.fill_uniform(buf, L, L, n, seed=synth.SEED_D)
+            out = torch.empty(n, dtype=torch.int32, device=dev)
+            if name == "D":
+                d_off = u64t(np.arange(n, dtype=np.uint64) * np.uint64(L))
+                d_len = u64t(np.full(n, L, dtype=np.uint64))
+                ms = time_calls(lambda: ctx.crc32_ragged(buf, d_off, d_len, out), iters)
+                kern = "subspace_crc32_batch (ragged kernel)"
+            else:
+                ms = time_calls(lambda: ctx.crc32_uniform(buf, L, L, n, out), iters)
+                kern = "subspace_crc32_batch_uniform (long-message kernel)"
+            ok = digest(out.cpu().numpy().view(np.uint32)) == GOLD["D"]["sha256_le_u32"]
+            res[name] = config_line(n * L, ms, ok, kern, {"workload": "D: 256 x 64 MiB", "messages": n})
+            del buf, out
+        elif name == "S":
+            res.update(slot_configs(ctx, dev, iters))
+        torch.cuda.empty_cache()
+    return res
+
+
+def slot_configs(ctx, dev, iters) -> dict:
+    """Config S: config B in the reference's slot layout on the device (65,536 slots of
+    PrefixSize 64 + 4 KiB payload, stride 4,160, 4 rotated channel buffers), the full 3-span
+    checksum. Publish (CALCULATE) must leave every prefix equal to the host drop-in's
+    CalculateCRC32Checksum<3> over GetMessageChecksumData (64 sampled slots); verify
+    (VERIFY) must pass every slot."""
+    import torch
+    from subspace_amd import checksum, gpu, slots
+    n, size, cs, ms_, nbuf = MSGS, MSG_BYTES, 4, 0, 4
+    ps, stride = slots.compute_prefix_size(cs, ms_), slots.slot_stride(size, cs, ms_)
+    rng = np.random.default_rng(0x5EED0005)
+    host = rng.integers(0, 256, stride * n, dtype=np.uint8)
+    host.reshape(n, stride)[:, :ps] = slots.make_prefixes(n, np.full(n, size, dtype=np.uint64), checksum_size=cs,
+                                                          metadata_size=ms_, seed=5)
+    bufs = [torch.from_numpy(host).to(dev) for _ in range(nbuf)]
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    errs = torch.zeros(1, dtype=torch.int32, device=dev)
+    nbytes = n * (size + 44)  # checksummed bytes: span 0 (44 B) + payload
+    res = {}
+    for mode, key in ((gpu.SLOT_CALCULATE, "S_publish"), (gpu.SLOT_VERIFY, "S_verify")):
+        i = [0]
+
+        def call():
+            b = bufs[i[0] % nbuf]
+            i[0] += 1
+            ctx.crc32_slots_strided(b, stride, n, message_size=size, checksum_size=cs, metadata_size=ms_, mode=mode,
+                                    status=status if mode == gpu.SLOT_VERIFY else None,
+                                    error_count=errs if mode == gpu.SLOT_VERIFY else None)
+        ms = time_calls(call, 100)
+        ok = None
+        if mode == gpu.SLOT_VERIFY:
+            torch.cuda.synchronize()
+            ok = int(errs.item()) == 0 and bool((status == 0).all().item())
+            chan = bufs[0].cpu().numpy()
+            for k in rng.choice(n, 64, replace=False):
+                pre = chan[k * stride:k * stride + ps]
+                pay = chan[k * stride + ps:k * stride + ps + size]
+                want = checksum.calculate_crc32_checksum(checksum.get_message_checksum_data(pre, pay, size, cs, ms_))
+                ok = ok and bytes(pre[48:52]) == want
+        res[key] = config_line(nbytes, ms, ok, "subspace_crc32_slots_strided", {
+            "workload": "S: 65,536 slots (prefix 64 B + 4 KiB payload, stride 4,160), 3-span checksum, " +
+                        ("publish: flag + checksum stored" if mode == gpu.SLOT_CALCULATE else
+                         "verify: per-slot status + mismatch count"),
+            "check": "verify passes all slots and 64 sampled stored checksums equal the host drop-in's"})
+    del bufs
+    return res
+
+
+# ------------------------------------------------------------------------------ CPU dry run
+def dry_run_cpu(args, world, rank) -> int:
+    """The multi-rank path on the CPU (gloo): same spawn, shard, barrier/max timing and
+    gather code as the GPU run; each rank checksums its shard with the library's host
+    SubspaceCRC32 (libsubspace_crc.so), and rank 0 checks the gathered list against the
+    fixture. E -> config B's 65,536 messages round-robin ("B" fixture); C -> the first
+    2,048 messages of config C in byte-balanced contiguous ranges ("C_2k"); B -> every rank
+    the 4,096-message "B_small" batch (weak)."""
+    import torch
+    import torch.distributed as dist
+    from subspace_amd import checksum, shard, synth
+    if world > 1:
+        dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            die(f"ranks joined {dist.get_world_size()} != --gpus {args.gpus}")
+    wl = args.workload
+    if wl == "E":
+        key, count = "B", GOLD["B"]["count"]
+        ids = shard.shard_ids(count, rank, world)
+        data = synth.host_uniform(GOLD["B"]["seed"], ids, MSG_BYTES)
+        msgs = [data[j] for j in range(len(ids))]
+    elif wl == "C":
+        key, count = "C_2k", GOLD["C_2k"]["count"]
+        lengths = synth.ragged_lengths(synth.SEED_C, count)
+        bounds = shard.ragged_ranges(lengths, world)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        offs, arena = synth.packed_offsets(lengths[lo:hi], 64)
+        data = synth.host_ragged(synth.SEED_C, np.arange(lo, hi), lengths[lo:hi], offs, arena)
+        msgs = [data[int(o):int(o) + int(n)] for o, n in zip(offs, lengths[lo:hi])]
+    else:
+        key, count = "B_small", GOLD["B_small"]["count"]
+        data = synth.host_uniform(GOLD["B_small"]["seed"], np.arange(count, dtype=np.uint64), MSG_BYTES)
+        msgs = [data[j] for j in range(count)]
+    local = np.zeros(max(len(msgs), 1), dtype=np.uint32)
+    step_bytes = sum(int(m.nbytes) for m in msgs)
+
+    def step():
+        for j, m in enumerate(msgs):
+            local[j] = checksum.subspace_crc32(0xFFFFFFFF, m)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    tl = torch.from_numpy(local[:len(msgs)].view(np.int32).copy())
+    tg = time.perf_counter()
+    if world > 1 and wl == "C":
+        full = shard.gather_ragged_crcs(tl, bounds, rank, world, dist)
+    elif world > 1 and wl == "E":
+        full = shard.gather_crcs(tl, count, rank, world, dist)
+    else:
+        full = local[:len(msgs)]
+    gather_ms = (time.perf_counter() - tg) * 1e3
+    if rank == 0:
+        total = (step_bytes * world if wl == "B" else GOLD[key]["total_bytes"]) * args.steps
+        value = total / elapsed / 2**30
+        print(json.dumps({
+            "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak" if wl == "B" else "strong", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (host twin of the device generator)",
+            "dry_run_cpu": True, "device": "cpu: host SubspaceCRC32 (libsubspace_crc.so) per rank, gloo",
+            "config": {"workload": f"dry run of {wl} over fixture {key} ({count} messages)",
+                       "parallelism": f"{'round-robin' if wl == 'E' else 'byte-balanced contiguous' if wl == 'C' else 'replicated'} "
+                                      f"shards x{world}, gloo all_gather of CRCs",
+                       "gather_ms": round(gather_ms, 3)},
+            "per_gpu_value": round(value / world, 3),
+            "bitexact_vs_golden": digest(full) == GOLD[key]["sha256_le_u32"] if full is not None else None,
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+# ------------------------------------------------------------------------------ main
+def main():
+    args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args))  # this process never touches a GPU
+    world = int(world_env or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        die(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch with --nproc-per-node equal to --gpus")
+    if args.workload is None:
+        args.workload = "B" if world == 1 else "E"
+    if args.dry_run_cpu:
+        sys.exit(dry_run_cpu(args, world, rank))
+
+    import torch
+    import torch.distributed as dist
+    from subspace_amd import gpu
+    if torch.cuda.device_count() <= local:
+        die(f"LOCAL_RANK {local} but only {torch.cuda.device_count()} visible GPU(s)")
+    if world > 1:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            die(f"RCCL sees {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    ctx = gpu.CrcContext(local)
+    stream = torch.cuda.current_stream()
+
+    wl = Workload(args.workload, ctx, dev, world, rank)
+    torch.cuda.synchronize()
+    if wl.nbuf % args.streams:  # workloads C and E have one buffer: their steps stay on one stream
+        args.streams = 1
+    streams = [stream] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
+    for s2 in streams[1:]:
+        s2.wait_stream(stream)
+    settle = max(0, args.settle - args.warmup)
+    elapsed, avg_kern_ms, sampled_ms = run_timed(wl, args.steps, args.warmup, args.settle, streams, world, dist,
+                                                 args.event_every)
+    bitexact, gather_ms = wl.check(dist)
+    step_bytes, total_step_bytes, nmsg = wl.step_bytes, wl.total_bytes, wl.nmsg
+    bounds = getattr(wl, "bounds", None)
+
+    # ---- N > 1: the same workload alone on rank 0's GPU (the N = 1 configuration), for the
+    #      per-GPU efficiency; the other ranks wait at the barrier
+    solo = None
+    if world > 1 and not args.no_solo:
+        if rank == 0:
+            wl.free()
+            torch.cuda.empty_cache()
+            one = Workload(args.workload, ctx, dev, 1, 0)
+            torch.cuda.synchronize()
+            solo_steps = max(1, min(args.steps, 200 if args.workload == "B" else 20))
+            el1, avg1, _ = run_timed(one, solo_steps, min(args.warmup, 3), 0, [stream], 1, None)
+            ok1, _ = one.check(None)
+            solo = {"value": round(one.total_bytes * solo_steps / el1 / 2**30, 2), "steps": solo_steps,
+                    "ms_per_step": round(el1 / solo_steps * 1e3, 4), "bitexact_vs_golden": ok1,
+                    "what": f"workload {args.workload} at N = 1 (the whole batch) on rank 0's GPU, timed after the "
+                            "N-rank region while the other ranks wait"}
+            one.free()
+        dist.barrier()
+    wl.free()
+    torch.cuda.empty_cache()
+
+    # ---- N = 1 extras (rank 0 only): secondary configs, end-to-end, CPU baseline
+    configs = None
+    cfg_names = args.configs if args.configs is not None else ("C,D,Du,S" if args.workload == "B" else "none")
+    if world == 1 and cfg_names != "none":
+        configs = secondary_configs(ctx, dev, [c for c in cfg_names.split(",") if c], args.config_iters)
     e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e and args.workload == "B":
+    if world == 1 and not args.no_e2e and args.workload == "B":
         e2e = end_to_end(ctx, gpu)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "B":
-        cpu = cpu_baseline([b.cpu().numpy() for b in bufs], args.cpu_seconds)
+    if world == 1 and not args.no_cpu_baseline and args.workload == "B":
+        wl_b = Workload("B", ctx, dev, 1, 0)
+        cpu = cpu_baseline(cpu_samples(dev, wl_b.bufs), args.cpu_runs)
+        wl_b.free()
 
     traffic = None
     # PMC-measured HBM bytes per config-B launch (tools/summarize_profile.py); other
@@ -365,31 +740,30 @@ def main():
     if tfile.exists() and args.workload == "B":
         try:
             traffic = json.loads(tfile.read_text()).get("hbm_bytes_per_launch")
-        except Exception:
+        except (OSError, ValueError):
             traffic = None
 
     if rank == 0:
+        total_bytes = total_step_bytes * args.steps
         if args.workload == "B":
-            total_bytes = step_bytes * args.steps * world  # every rank: its own 65,536-message batch
             workload = {"workload": "B: 65,536 x 4 KiB payloads per GPU per step, one CRC32 (IEEE, "
                                     "client/checksum.cc default build) each", "messages_per_gpu": nmsg,
                         "message_bytes": MSG_BYTES, "batches_rotated": ROTATE,
                         "parallelism": f"independent message shards x{world}", "streams": args.streams}
             scaling = "weak"
         elif args.workload == "C":
-            total_bytes = c_total_bytes * args.steps  # the whole 1 Mi-message batch per step
             workload = {"workload": "C: 1 Mi messages, 64 B - 1 MiB log-uniform (117.8 GB), one CRC32 each, "
-                                    "contiguous shards balanced by bytes", "messages_total": int(bounds_c[-1]),
-                        "messages_rank0": nmsg, "bytes_total": c_total_bytes,
+                                    "contiguous shards balanced by bytes", "messages_total": int(bounds[-1]),
+                        "messages_rank0": nmsg, "bytes_total": total_step_bytes,
                         "parallelism": f"contiguous byte-balanced shards x{world}, RCCL all_gather of CRCs "
-                                       "(untimed)",
+                                       "(timed separately)",
                         "gather_ms": round(gather_ms, 3) if gather_ms is not None else None}
             scaling = "strong"
         else:
-            total_bytes = (8 << 20) * MSG_BYTES * args.steps  # the whole 8 Mi batch per step
             workload = {"workload": "E: 8 Mi x 4 KiB payloads per step, round-robin over the GPUs, one CRC32 each",
-                        "messages_total": 8 << 20, "messages_per_gpu": nmsg, "message_bytes": MSG_BYTES,
-                        "parallelism": f"round-robin message shards x{world}, RCCL all_gather of CRCs (untimed)",
+                        "messages_total": E_COUNT, "messages_per_gpu": nmsg, "message_bytes": MSG_BYTES,
+                        "parallelism": f"round-robin message shards x{world}, RCCL all_gather of CRCs "
+                                       "(timed separately)",
                         "gather_ms": round(gather_ms, 3) if gather_ms is not None else None,
                         # the same rate with one gather of every step's CRCs to rank 0 added per step
                         "value_incl_gather": round(total_bytes / (elapsed + args.steps * gather_ms * 1e-3) / 2**30, 2)
@@ -397,6 +771,9 @@ def main():
             scaling = "strong"
         value = total_bytes / elapsed / 2**30
         achieved = step_bytes / (avg_kern_ms * 1e-3) / 1e9
+        kernel = {"B": "subspace_amd::crc32_uniform4k_kernel<512>",
+                  "E": "subspace_amd::crc32_uniform4k_kernel<512>",
+                  "C": "subspace_amd::crc32_ragged_kernel<512> + prep (whole call)"}[args.workload]
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -414,17 +791,21 @@ def main():
                     + ("; 4 rotated 256 MiB batches per GPU)" if args.workload == "B" else ")"),
             "config": workload,
             "pct_of_hbm_peak": round(100.0 * value * 2**30 / 1e9 / (HBM_PEAK_GBS * world), 2),
+            "per_gpu_value": round(value / world, 2),
             "bitexact_vs_golden": bitexact,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "subspace_amd::crc32_ragged_kernel<512> + prep (whole call)" if args.workload == "C"
-                         else "subspace_amd::crc32_uniform4k_kernel<512>", "avg_launch_ms": round(avg_kern_ms, 4),
-                         "launch_ms_source": f"HIP event span of the timed region / K ({args.streams} stream(s), "
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
+                         "avg_launch_ms": round(avg_kern_ms, 4),
+                         "launch_ms_source": f"HIP event span of rank 0's timed region / K ({args.streams} stream(s), "
                                              "consecutive launches overlap when 2)",
                          "sampled_launch_ms": round(sampled_ms, 4) if sampled_ms else None},
-            "cpu_baseline": cpu,
-            "e2e_pcie": e2e,
         }
+        if solo is not None:
+            line["single_gpu"] = solo
+            line["efficiency"] = round(value / (world * solo["value"]), 4)
+        line["configs"] = configs
+        line["cpu_baseline"] = cpu
+        line["e2e_pcie"] = e2e
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

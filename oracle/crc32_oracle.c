@@ -39,9 +39,11 @@
  * and the reference's own -msse4.2 outputs recorded in SURVEY.md 8c ("hello" ->
  * 0x9A71BB4C), tests/golden/crc32c_kat.json.
  */
+#define _GNU_SOURCE /* pthread_setaffinity_np, CPU_* (the pinned CPU-baseline workers) */
 #include "crc32_oracle.h"
 
 #include <pthread.h>
+#include <sched.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -233,6 +235,82 @@ void oracle_crc32_batch(const uint8_t* base, const uint64_t* offsets, const uint
   for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
   free(jobs);
   free(th);
+}
+
+/* The CPU-baseline plan's threading (BASELINE.md "CPU-baseline plan" 2): one worker thread
+ * per core, worker t pinned to the t-th CPU of the calling process's affinity set (the
+ * calling thread itself is left alone and only joins), messages partitioned round-robin.
+ * oracle_first_touch_copy copies a sample into `dst` with the same workers and partition,
+ * so each message's pages are first touched (and, on a NUMA host, placed) by the worker
+ * that later checksums it. Both return the number of workers that could be pinned. */
+typedef struct {
+  uint8_t* dst;
+  const uint8_t* src;
+  batch_job job;
+  int cpu;
+  int pinned;
+} pinned_job;
+
+static void pin_self(pinned_job* p) {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  CPU_SET(p->cpu, &set);
+  p->pinned = pthread_setaffinity_np(pthread_self(), sizeof(set), &set) == 0;
+}
+
+static void* pinned_crc_worker(void* arg) {
+  pinned_job* p = (pinned_job*)arg;
+  pin_self(p);
+  batch_worker(&p->job);
+  return NULL;
+}
+
+static void* pinned_copy_worker(void* arg) {
+  pinned_job* p = (pinned_job*)arg;
+  pin_self(p);
+  const batch_job* j = &p->job;
+  for (size_t i = (size_t)j->tid; i < j->n; i += (size_t)j->nthreads)
+    memcpy(p->dst + j->offsets[i], p->src + j->offsets[i], (size_t)j->lengths[i]);
+  return NULL;
+}
+
+static int run_pinned(void* (*fn)(void*), uint8_t* dst, const uint8_t* src, const uint64_t* offsets,
+                      const uint64_t* lengths, size_t n, uint32_t init, uint32_t* out, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  cpu_set_t mine;
+  int cpus[CPU_SETSIZE], ncpu = 0;
+  if (sched_getaffinity(0, sizeof(mine), &mine) == 0)
+    for (int c = 0; c < CPU_SETSIZE; c++)
+      if (CPU_ISSET(c, &mine)) cpus[ncpu++] = c;
+  if (ncpu == 0) cpus[ncpu++] = 0;
+  pinned_job* jobs = (pinned_job*)calloc((size_t)nthreads, sizeof(pinned_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int t = 0; t < nthreads; t++) {
+    batch_job b = {src, offsets, lengths, n, init, out, t, nthreads};
+    jobs[t].dst = dst;
+    jobs[t].src = src;
+    jobs[t].job = b;
+    jobs[t].cpu = cpus[t % ncpu];
+    pthread_create(&th[t], NULL, fn, &jobs[t]);
+  }
+  int pinned = 0;
+  for (int t = 0; t < nthreads; t++) {
+    pthread_join(th[t], NULL);
+    pinned += jobs[t].pinned;
+  }
+  free(jobs);
+  free(th);
+  return pinned;
+}
+
+int oracle_crc32_batch_pinned(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, size_t n,
+                              uint32_t init, uint32_t* out, int nthreads) {
+  return run_pinned(pinned_crc_worker, NULL, base, offsets, lengths, n, init, out, nthreads);
+}
+
+int oracle_first_touch_copy(uint8_t* dst, const uint8_t* src, const uint64_t* offsets, const uint64_t* lengths,
+                            size_t n, int nthreads) {
+  return run_pinned(pinned_copy_worker, dst, src, offsets, lengths, n, 0, NULL, nthreads);
 }
 
 /* ------------------------------------------------------------------ synthetic inputs */

@@ -30,6 +30,12 @@ void oracle_verify_slots(const uint8_t* base, const uint64_t* prefix_off, const 
                          uint32_t* status);
 void oracle_crc32_batch(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, size_t n,
                         uint32_t init, uint32_t* out, int nthreads);
+/* The same with one pinned worker thread per CPU of the caller's affinity set (the
+ * CPU-baseline plan), and the first-touch copy of a sample by the same workers. */
+int oracle_crc32_batch_pinned(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, size_t n,
+                              uint32_t init, uint32_t* out, int nthreads);
+int oracle_first_touch_copy(uint8_t* dst, const uint8_t* src, const uint64_t* offsets, const uint64_t* lengths,
+                            size_t n, int nthreads);
 
 uint64_t oracle_splitmix64(uint64_t x);
 void oracle_synth_fill(uint64_t seed, uint64_t msg, uint64_t start, uint8_t* dst, size_t n);

@@ -54,7 +54,9 @@ def ragged_ranges(lengths, world: int) -> np.ndarray:
     lengths = np.asarray(lengths, dtype=np.uint64)
     if world < 1:
         raise ValueError("world must be >= 1")
-    starts = np.concatenate([[0], np.cumsum(lengths, dtype=np.uint64)])  # bytes before message i
+    # bytes before message i; built from a uint64 zero so it stays uint64 end to end
+    # (np.concatenate of a Python-int list with uint64 promotes to float64)
+    starts = np.concatenate([np.zeros(1, dtype=np.uint64), np.cumsum(lengths, dtype=np.uint64)])
     total = int(starts[-1])
     targets = [(total * r + world - 1) // world for r in range(world)]  # ceil(total*r/world)
     b = np.searchsorted(starts[:-1], np.array(targets, dtype=np.uint64), side="left").astype(np.int64)

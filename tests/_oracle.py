@@ -28,6 +28,10 @@ class Oracle:
         lib.oracle_verify_checksum.restype = ctypes.c_int
         lib.oracle_verify_checksum.argtypes = [vp, vp, sz, vp]
         lib.oracle_crc32_batch.argtypes = [vp, vp, vp, sz, u32, vp, ctypes.c_int]
+        lib.oracle_crc32_batch_pinned.restype = ctypes.c_int
+        lib.oracle_crc32_batch_pinned.argtypes = [vp, vp, vp, sz, u32, vp, ctypes.c_int]
+        lib.oracle_first_touch_copy.restype = ctypes.c_int
+        lib.oracle_first_touch_copy.argtypes = [vp, vp, vp, vp, sz, ctypes.c_int]
         lib.oracle_splitmix64.restype = u64
         lib.oracle_splitmix64.argtypes = [u64]
         lib.oracle_synth_fill.argtypes = [u64, u64, u64, vp, sz]
@@ -128,6 +132,29 @@ class Oracle:
         self.lib.oracle_crc32_batch(base.ctypes.data, offsets.ctypes.data, lengths.ctypes.data, len(offsets),
                                     init & 0xFFFFFFFF, out.ctypes.data, threads)
         return out
+
+    def crc32_batch_pinned(self, base: np.ndarray, offsets, lengths, init: int = 0xFFFFFFFF,
+                           threads: int = 1) -> tuple[np.ndarray, int]:
+        """crc32_batch with one worker per core, pinned (BASELINE.md CPU-baseline plan).
+        Returns (crcs, number of workers that were pinned)."""
+        assert base.dtype == np.uint8 and base.flags.c_contiguous
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+        out = np.zeros(len(offsets), dtype=np.uint32)
+        pinned = self.lib.oracle_crc32_batch_pinned(base.ctypes.data, offsets.ctypes.data, lengths.ctypes.data,
+                                                    len(offsets), init & 0xFFFFFFFF, out.ctypes.data, threads)
+        return out, int(pinned)
+
+    def first_touch_copy(self, src: np.ndarray, offsets, lengths, threads: int) -> np.ndarray:
+        """A copy of `src` whose message bytes are first touched by the pinned worker that
+        owns them under crc32_batch_pinned's round-robin partition."""
+        assert src.dtype == np.uint8 and src.flags.c_contiguous
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+        dst = np.empty_like(src)  # untouched pages
+        self.lib.oracle_first_touch_copy(dst.ctypes.data, src.ctypes.data, offsets.ctypes.data, lengths.ctypes.data,
+                                         len(offsets), threads)
+        return dst
 
     def ragged_lengths(self, seed: int, count: int) -> np.ndarray:
         return np.array([self.lib.oracle_ragged_length(seed, i) for i in range(count)], dtype=np.uint64)

@@ -3,6 +3,8 @@
 
   python tests/golden/make_golden.py            # small vectors  -> golden.json
   python tests/golden/make_golden.py --configs  # + full-size synthetic config hashes -> configs.json
+  python tests/golden/make_golden.py --small    # only the small config prefixes (B_small, C_small,
+                                                # C_2k), merged into the existing configs.json
 
 Expected values come from Python's zlib.crc32 (zlib 1.2.11), an implementation of
 the same published IEEE CRC-32 algorithm that is independent of this repository.
@@ -146,7 +148,7 @@ def list_hash(crcs: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(crcs, dtype="<u4").tobytes()).hexdigest()
 
 
-def config_hashes(oracle, threads: int) -> dict:
+def config_hashes(oracle, threads: int, small_only: bool = False) -> dict:
     res = {"generator": "tests/golden/make_golden.py --configs", "init": M32, "crc": "raw"}
     t0 = time.time()
 
@@ -162,12 +164,17 @@ def config_hashes(oracle, threads: int) -> dict:
         print(f"{name}: {len(lengths)} msgs, {res[name]['total_bytes'] / 2**30:.2f} GiB in {time.time() - t:.1f}s",
               flush=True)
 
-    add("B", synth.SEED_B, np.full(65536, 4096, dtype=np.uint64), "65,536 x 4 KiB")
+    if not small_only:
+        add("B", synth.SEED_B, np.full(65536, 4096, dtype=np.uint64), "65,536 x 4 KiB")
     add("B_small", synth.SEED_B, np.full(4096, 4096, dtype=np.uint64), "first 4,096 messages of B")
-    add("C", synth.SEED_C, synth.ragged_lengths(synth.SEED_C, 1 << 20), "1 Mi ragged 64 B - 1 MiB")
+    if not small_only:
+        add("C", synth.SEED_C, synth.ragged_lengths(synth.SEED_C, 1 << 20), "1 Mi ragged 64 B - 1 MiB")
     add("C_small", synth.SEED_C, synth.ragged_lengths(synth.SEED_C, 20000), "first 20,000 messages of C")
-    add("D", synth.SEED_D, np.full(256, 64 << 20, dtype=np.uint64), "256 x 64 MiB")
-    add("E", synth.SEED_E, np.full(8 << 20, 4096, dtype=np.uint64), "8 Mi x 4 KiB (global message ids)")
+    add("C_2k", synth.SEED_C, synth.ragged_lengths(synth.SEED_C, 2048),
+        "first 2,048 messages of C (bench.py --dry-run-cpu, contiguous shards)")
+    if not small_only:
+        add("D", synth.SEED_D, np.full(256, 64 << 20, dtype=np.uint64), "256 x 64 MiB")
+        add("E", synth.SEED_E, np.full(8 << 20, 4096, dtype=np.uint64), "8 Mi x 4 KiB (global message ids)")
     res["seconds"] = round(time.time() - t0, 1)
     return res
 
@@ -175,6 +182,7 @@ def config_hashes(oracle, threads: int) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", action="store_true")
+    ap.add_argument("--small", action="store_true")
     ap.add_argument("--threads", type=int, default=8)
     args = ap.parse_args()
     oracle = _oracle.load()
@@ -185,6 +193,13 @@ def main():
         cfg = config_hashes(oracle, args.threads)
         (HERE / "configs.json").write_text(json.dumps(cfg, indent=1) + "\n")
         print("wrote configs.json")
+    elif args.small:
+        cfg = json.loads((HERE / "configs.json").read_text())
+        small = config_hashes(oracle, args.threads, small_only=True)
+        for k in ("B_small", "C_small", "C_2k"):
+            cfg[k] = small[k]
+        (HERE / "configs.json").write_text(json.dumps(cfg, indent=1) + "\n")
+        print("updated configs.json (small prefixes)")
 
 
 if __name__ == "__main__":

@@ -1,0 +1,55 @@
+"""bench.py's multi-rank launch path on the CPU (gloo), through bench.py itself.
+
+`python bench.py --gpus N --dry-run-cpu` runs the same code as a GPU run of N ranks -- the
+parent spawns N rank processes through torch.distributed.run, each rank builds its shard
+(round-robin for E, byte-balanced contiguous ranges for C), times its steps between
+barriers with a max-over-ranks reduction and all_gathers its 4-byte CRCs -- with the
+library's host SubspaceCRC32 in place of the kernel and gloo in place of RCCL. Rank 0
+checks the gathered list against the committed fixture hash (tests/golden/configs.json).
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def run_bench(*args, env_extra=None, timeout=300):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=str(ROOT))
+
+
+def last_json(stdout: str) -> dict:
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout  # exactly one JSON line, from rank 0
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world,workload", [(2, "E"), (2, "C"), (3, "C")])
+def test_dry_run_spawns_ranks_and_matches_fixture(world, workload):
+    r = run_bench("--gpus", str(world), "--dry-run-cpu", "--workload", workload, "--steps", "2", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = last_json(r.stdout)
+    assert line["n_gpus"] == world
+    assert line["bitexact_vs_golden"] is True
+    assert line["scaling"] == "strong"
+    assert line["value"] > 0 and line["per_gpu_value"] == pytest.approx(line["value"] / world, rel=1e-2)
+
+
+def test_dry_run_single_rank_default_workload():
+    r = run_bench("--dry-run-cpu", "--steps", "1", "--warmup", "0")
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = last_json(r.stdout)
+    assert line["n_gpus"] == 1 and line["bitexact_vs_golden"] is True and line["scaling"] == "weak"
+
+
+def test_world_size_must_match_gpus():
+    r = run_bench("--gpus", "2", "--dry-run-cpu", env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert "WORLD_SIZE" in r.stderr
