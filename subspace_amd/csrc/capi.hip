@@ -20,23 +20,24 @@ template <int WG>
 __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int, u32*);
 
 struct TileDesc;
-__global__ void crc32_ragged_count_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*);
-__global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, u64, u64, TileDesc*, u32*);
+__global__ void crc32_ragged_count_scan_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
+                                               u64*, u32*, u32*, u64);
+__global__ void tile_segment_scan_kernel(const u32*, u32, u32, u32, const u64*, u64, u32*, u32*);
+__global__ void segment_prefix_kernel(u32*, u64, u32, u32, const u64*, u64, u64*, u32*);
+__global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, u64, u64, const u32*,
+                                         TileDesc*, u32*, u64*, u64, u32*);
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
                                     const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds, u32*, u32*, u64);
 __global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, const u64*, u32, u64, const u32*, const u32*,
-                                          const u32*, u32, u32*);
-hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u64 nw, u64 nkmax, u32* tord, u32* out, u64 n,
-                    hipStream_t stream);
+                                          u32, u32, const u32*, const u32*, u32, u32*, u64*, u64, u32*);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, int, int, u32, const u32*,
                                          const u32*, const u32*, u32*, u32*, u32*);
 __global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*);
-hipError_t ragged_scan(void* temp, size_t& temp_bytes, const u64* in, u64* out, u64 n, hipStream_t stream);
 __global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* offsets, u64* lengths);
 template <int WG>
 __global__ void crc32_long_kernel(const uint8_t*, u64, u32, u32, const u32*, const u32*, u32, u32, u32*, u32);
-__global__ void crc32_long_final_kernel(const u32*, u32, u32, u32*);
+__global__ void crc32_long_final_kernel(const u32*, const u32*, u32, u32, u32, u32, u32*, u64*, u64, u32*);
 
 }  // namespace subspace_amd
 
@@ -81,6 +82,9 @@ uintptr_t host_alias(uintptr_t p, uint64_t n) {
   return 0;
 }
 constexpr size_t kTileDescBytes = 16;
+constexpr u64 kScanTile = 4096;   // segments per workgroup of the segment scan (crc_combine.hip)
+constexpr u64 kCountTile = 4096;  // messages per workgroup of the tile-count scan
+constexpr u64 ceil_div(u64 a, u64 b) { return (a + b - 1) / b; }
 
 }  // namespace
 
@@ -95,18 +99,22 @@ struct subspace_crc_ctx {
   Tables host_tab;
   Mat32 zinv1;  // Z_1^{-1}: the ragged kernel's head seeds Z_r^{-1}(init)
   // ragged workspace
-  u64* d_ntiles = nullptr;   // count + 1
-  u64* d_tbase = nullptr;    // count + 1
-  void* d_scan_tmp = nullptr;
-  size_t scan_tmp_bytes = 0;
+  u64* d_tbase = nullptr;    // count + 1: tiles before each message (exclusive scan)
   u64 ws_messages = 0;
   uint8_t* d_desc = nullptr;
   u32* d_tilecrc = nullptr;  // per-tile values, wave-major (desc_capacity + one tile per wave)
-  u32* d_tord = nullptr;     // the same values in tile order (the scan's input)
-  u32* d_px = nullptr;       // their inclusive XOR-scan
-  void* d_xscan_tmp = nullptr;
-  size_t xscan_tmp_bytes = 0;
+  u32* d_local = nullptr;    // per-segment inclusive XOR prefixes of the values, tile order
+  u32* d_segx = nullptr;     // per-segment XORs, then their exclusive XOR prefixes
+  u32* d_chunk = nullptr;    // message of every kDescTilesPerWave-th tile (tile-count scan)
   u64 desc_capacity = 0;
+  // look-back scan state: word 0 = the two workgroup tickets (u32 each), then the
+  // tile-count scan's status words (scan_a_words), then the segment scan's (scan_b_words).
+  // Zeroed at allocation; each call's later kernels zero what its scans used
+  // (crc_device.h reset_scan_state). scan_dirty: a call failed between a scan and its reset.
+  u64* d_scan_state = nullptr;
+  u64 scan_a_words = 0, scan_b_words = 0;
+  bool scan_dirty = false;
+  u64 mem_tiles = 0;  // device memory / 8 KiB: bounds the descriptor workspace
   u32* d_overflow = nullptr;
   int uniform_wg = 512;    // workgroup size of the uniform kernel (256/512/640/768/1024)
   int uniform_blocks = 0;  // 0 = one workgroup per CU
@@ -144,45 +152,91 @@ struct subspace_crc_ctx {
 
 namespace {
 
+// Geometry of the wave-major tile values of the persistent ragged / long kernels: nw waves,
+// nkmax values per wave, segments of 64 tiles of one sweep row (crc_combine.hip).
+struct TileGeom {
+  u64 nw, nkmax, nwb, nseg;
+};
+TileGeom tile_geom(const subspace_crc_ctx* c, u64 tiles) {
+  TileGeom g;
+  g.nw = (u64)c->num_cus * (kRaggedWG / 64);
+  g.nkmax = ceil_div(tiles ? tiles : 1, g.nw);
+  g.nwb = ceil_div(g.nw, 64);
+  g.nseg = g.nkmax * g.nwb;
+  return g;
+}
+
 int ensure_ragged_ws(subspace_crc_ctx* c, u64 messages, u64 tiles) {
+  bool state = false;
   if (messages > c->ws_messages) {
-    (void)hipFree(c->d_ntiles);
     (void)hipFree(c->d_tbase);
-    (void)hipFree(c->d_scan_tmp);
-    c->d_ntiles = c->d_tbase = nullptr;
-    c->d_scan_tmp = nullptr;
+    c->d_tbase = nullptr;
     c->ws_messages = 0;
-    const u64 n = messages + 1;
-    HIP_TRY(hipMalloc(&c->d_ntiles, n * sizeof(u64)));
-    HIP_TRY(hipMalloc(&c->d_tbase, n * sizeof(u64)));
-    size_t tmp = 0;
-    HIP_TRY(ragged_scan(nullptr, tmp, c->d_ntiles, c->d_tbase, n, nullptr));
-    HIP_TRY(hipMalloc(&c->d_scan_tmp, tmp));
-    c->scan_tmp_bytes = tmp;
+    HIP_TRY(hipMalloc(&c->d_tbase, (messages + 1) * sizeof(u64)));
     c->ws_messages = messages;
+    state = true;
   }
   if (tiles > c->desc_capacity) {
     (void)hipFree(c->d_desc);
     (void)hipFree(c->d_tilecrc);
-    (void)hipFree(c->d_px);
-    (void)hipFree(c->d_tord);
-    (void)hipFree(c->d_xscan_tmp);
+    (void)hipFree(c->d_local);
+    (void)hipFree(c->d_segx);
+    (void)hipFree(c->d_chunk);
     c->d_desc = nullptr;
-    c->d_tilecrc = c->d_px = c->d_tord = nullptr;
-    c->d_xscan_tmp = nullptr;
+    c->d_tilecrc = c->d_local = c->d_segx = c->d_chunk = nullptr;
     c->desc_capacity = 0;
+    const TileGeom g = tile_geom(c, tiles);
     HIP_TRY(hipMalloc(&c->d_desc, tiles * kTileDescBytes));
-    // wave-major: nw * ceil(tiles / nw) < tiles + nw entries (nw = waves of a persistent grid)
-    HIP_TRY(hipMalloc(&c->d_tilecrc, (tiles + (u64)c->num_cus * (kRaggedWG / 64)) * sizeof(u32)));
-    HIP_TRY(hipMalloc(&c->d_px, tiles * sizeof(u32)));
-    HIP_TRY(hipMalloc(&c->d_tord, tiles * sizeof(u32)));
-    size_t tmp = 0;
-    HIP_TRY(xor_scan(nullptr, tmp, c->d_tilecrc, 1, tiles, c->d_tord, c->d_px, tiles, nullptr));
-    HIP_TRY(hipMalloc(&c->d_xscan_tmp, tmp));
-    c->xscan_tmp_bytes = tmp;
+    // wave-major: nw * nkmax < tiles + nw entries
+    HIP_TRY(hipMalloc(&c->d_tilecrc, g.nw * g.nkmax * sizeof(u32)));
+    HIP_TRY(hipMalloc(&c->d_local, tiles * sizeof(u32)));
+    HIP_TRY(hipMalloc(&c->d_segx, g.nseg * sizeof(u32)));
+    HIP_TRY(hipMalloc(&c->d_chunk, ceil_div(tiles, kDescTilesPerWave) * sizeof(u32)));
     c->desc_capacity = tiles;
+    state = true;
+  }
+  if (state || !c->d_scan_state) {
+    (void)hipFree(c->d_scan_state);
+    c->d_scan_state = nullptr;
+    c->scan_a_words = ceil_div(c->ws_messages + 1, kCountTile);
+    c->scan_b_words = ceil_div(tile_geom(c, c->desc_capacity).nseg, kScanTile);
+    HIP_TRY(hipMalloc(&c->d_scan_state, (1 + c->scan_a_words + c->scan_b_words) * sizeof(u64)));
+    HIP_TRY(hipMemset(c->d_scan_state, 0, (1 + c->scan_a_words + c->scan_b_words) * sizeof(u64)));
+    c->scan_dirty = false;
   }
   if (!c->d_overflow) HIP_TRY(hipMalloc(&c->d_overflow, 16));
+  return SUBSPACE_CRC_OK;
+}
+
+// Before a call's first scan: a call that failed after a scan may have left state behind.
+int scan_state_clean(subspace_crc_ctx* c, hipStream_t st) {
+  if (c->scan_dirty) {
+    HIP_TRY(hipMemsetAsync(c->d_scan_state, 0, (1 + c->scan_a_words + c->scan_b_words) * sizeof(u64), st));
+    c->scan_dirty = false;
+  }
+  return SUBSPACE_CRC_OK;
+}
+
+// Descriptor capacity of a call: the caller's bound (exact for non-overlapping messages),
+// limited to what device memory can hold plus a tile per message, and below 2^32 (tile
+// indices are u32 in the combine). A batch with more tiles takes the overflow path.
+u64 clamp_capacity(const subspace_crc_ctx* c, u64 cap, u64 count) {
+  const u64 lim = std::min<u64>(c->mem_tiles + count + 1, (1ull << 32) - (1ull << 20));
+  return std::min(cap, lim);
+}
+
+// The tile-value combine after a ragged or long kernel: segment scans of the wave-major
+// values, then the look-back over the segment XORs. total_ptr: the device's tile count
+// (ragged) or null (long: `tiles` exact).
+int combine_tiles(subspace_crc_ctx* c, const TileGeom& g, const u64* total_ptr, u64 tiles, hipStream_t st) {
+  const dim3 grid((unsigned)ceil_div(g.nkmax, 64), (unsigned)g.nwb);
+  tile_segment_scan_kernel<<<grid, 256, 0, st>>>(c->d_tilecrc, (u32)g.nw, (u32)g.nkmax, (u32)g.nwb, total_ptr, tiles,
+                                                  c->d_local, c->d_segx);
+  HIP_TRY(hipGetLastError());
+  u32* tickets = reinterpret_cast<u32*>(c->d_scan_state);
+  segment_prefix_kernel<<<(unsigned)ceil_div(g.nseg, kScanTile), 256, 0, st>>>(
+      c->d_segx, g.nseg, (u32)g.nw, (u32)g.nwb, total_ptr, tiles, c->d_scan_state + 1 + c->scan_a_words, tickets + 1);
+  HIP_TRY(hipGetLastError());
   return SUBSPACE_CRC_OK;
 }
 
@@ -199,38 +253,44 @@ int grid_for(subspace_crc_ctx* c, u64 work_units, int waves_per_block) {
 // `cap` sizes the descriptor workspace; a batch with more tiles takes the search path.
 int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* offsets, u32 ostride, const u64* lengths,
                u32 lstride, u64 count, u32 init, u32 final_xor, u32* out, hipStream_t st) {
+  cap = clamp_capacity(c, cap, count);
   int rc = ensure_ragged_ws(c, count, cap);
   if (rc) return rc;
+  const TileGeom g = tile_geom(c, cap);
   const u64 n1 = count + 1;
-  crc32_ragged_count_kernel<<<(unsigned)((n1 + 255) / 256), 256, 0, st>>>(offsets, ostride, lengths, lstride, count,
-                                                                           init, final_xor, c->d_ntiles, out,
-                                                                           c->zero_word);
+  rc = scan_state_clean(c, st);
+  if (rc) return rc;
+  c->scan_dirty = true;  // until the final kernel is launched
+  u32* tickets = reinterpret_cast<u32*>(c->d_scan_state);
+  crc32_ragged_count_scan_kernel<<<(unsigned)ceil_div(n1, kCountTile), 256, 0, st>>>(
+      offsets, ostride, lengths, lstride, count, init, final_xor, c->d_tbase, out, c->zero_word, c->d_scan_state + 1,
+      reinterpret_cast<u32*>(c->d_scan_state), c->d_chunk, ceil_div(cap, kDescTilesPerWave));
   c->zero_word = nullptr;
   HIP_TRY(hipGetLastError());
-  size_t tmp = c->scan_tmp_bytes;
-  HIP_TRY(ragged_scan(c->d_scan_tmp, tmp, c->d_ntiles, c->d_tbase, n1, st));
-  // one wave per 1,024 tiles (kDescTilesPerWave), four waves per block
-  crc32_ragged_desc_kernel<<<(unsigned)((cap + 4095) / 4096), 256, 0, st>>>(
-      offsets, ostride, lengths, lstride, c->d_tbase, count, cap, reinterpret_cast<TileDesc*>(c->d_desc),
-      c->d_overflow);
+  // one wave per kDescTilesPerWave tiles, four waves per block
+  crc32_ragged_desc_kernel<<<(unsigned)ceil_div(cap, 4 * kDescTilesPerWave), 256, 0, st>>>(
+      offsets, ostride, lengths, lstride, c->d_tbase, count, cap, c->d_chunk, reinterpret_cast<TileDesc*>(c->d_desc),
+      c->d_overflow, c->d_scan_state + 1, ceil_div(n1, kCountTile), tickets);
   HIP_TRY(hipGetLastError());
   const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU
   HeadSeeds seeds;  // Z_r^{-1}(init), r = 0..15: the seed of a message's first line, mis = r
   seeds.v[0] = init;
   for (int r = 1; r < 16; r++) seeds.v[r] = apply(c->zinv1, seeds.v[r - 1]);
-  const u64 nw = (u64)blocks * (kRaggedWG / 64), nkmax = (cap + nw - 1) / nw;  // wave-major tile values
   crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, ragged_lds_bytes(), st>>>(
       base, offsets, ostride, lengths, lstride, c->d_tbase, count, reinterpret_cast<const TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_tab, c->d_rops, seeds, out, c->d_tilecrc, nkmax);
+      c->d_overflow, c->d_tab, c->d_rops, seeds, out, c->d_tilecrc, g.nkmax);
   HIP_TRY(hipGetLastError());
-  // padded message CRC = XOR of its tiles' values = difference of two XOR-scan entries
-  // (entries past the batch's real tile count are scanned but never read); the final
-  // kernel undoes the last tile's zero padding and applies the final XOR
-  size_t xtmp = c->xscan_tmp_bytes;
-  HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, nw, nkmax, c->d_tord, c->d_px, cap, st));
-  crc32_ragged_final_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(
-      c->d_tbase, offsets, ostride, lengths, lstride, count, c->d_px, c->d_overflow, c->d_rops, final_xor, out);
+  // padded message CRC = XOR of its tiles' values = difference of two entries of their
+  // XOR prefix (only the batch's real tiles are combined); the final kernel undoes the last
+  // tile's zero padding and applies the final XOR
+  rc = combine_tiles(c, g, c->d_tbase + count, cap, st);
+  if (rc) return rc;
+  crc32_ragged_final_kernel<<<(unsigned)ceil_div(count, 256), 256, 0, st>>>(
+      c->d_tbase, offsets, ostride, lengths, lstride, count, c->d_local, c->d_segx, (u32)g.nw, (u32)g.nwb,
+      c->d_overflow, c->d_rops, final_xor, out, c->d_scan_state + 1 + c->scan_a_words, ceil_div(g.nseg, kScanTile),
+      tickets + 1);
   HIP_TRY(hipGetLastError());
+  c->scan_dirty = false;
   return SUBSPACE_CRC_OK;
 }
 
@@ -305,6 +365,7 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   auto* c = new subspace_crc_ctx();
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
+  c->mem_tiles = (u64)prop.totalGlobalMem / 8192;
   c->poly = poly;
   c->host_tab = make_tables(poly);
   c->zinv1 = inverse(z_one(c->host_tab));
@@ -386,14 +447,13 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_laneops);
   (void)hipFree(c->d_crc0);
   (void)hipFree(c->d_soff);
-  (void)hipFree(c->d_ntiles);
   (void)hipFree(c->d_tbase);
-  (void)hipFree(c->d_scan_tmp);
   (void)hipFree(c->d_desc);
   (void)hipFree(c->d_tilecrc);
-  (void)hipFree(c->d_px);
-  (void)hipFree(c->d_tord);
-  (void)hipFree(c->d_xscan_tmp);
+  (void)hipFree(c->d_local);
+  (void)hipFree(c->d_segx);
+  (void)hipFree(c->d_chunk);
+  (void)hipFree(c->d_scan_state);
   (void)hipFree(c->d_overflow);
   (void)hipFree(c->d_uoff);
   (void)hipFree(c->d_ulen);
@@ -404,7 +464,7 @@ int subspace_crc_ctx_reserve(subspace_crc_ctx* c, uint64_t max_messages, uint64_
   g_err[0] = 0;
   if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
   HIP_TRY(hipSetDevice(c->device));
-  return ensure_ragged_ws(c, max_messages, max_tiles);
+  return ensure_ragged_ws(c, max_messages, clamp_capacity(c, max_tiles, max_messages));
 }
 
 int subspace_crc32_batch(subspace_crc_ctx* c, const void* dev_base, uint64_t arena_bytes, const uint64_t* dev_offsets,
@@ -473,16 +533,21 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     const u64 tiles = pieces * count;
     int rc = ensure_ragged_ws(c, 0, tiles);
     if (rc) return rc;
-    const u64 nw = (u64)c->num_cus * (kRaggedWG / 64), nkmax = (tiles + nw - 1) / nw;
+    const TileGeom g = tile_geom(c, tiles);
+    rc = scan_state_clean(c, st);
+    if (rc) return rc;
+    c->scan_dirty = true;  // until the final kernel is launched
     crc32_long_kernel<kRaggedWG><<<c->num_cus, kRaggedWG, ragged_lds_bytes(), st>>>(
         static_cast<const uint8_t*>(dev_base), stride, (u32)pieces, (u32)count, c->d_tab, c->d_rops, init, final_xor,
-        c->d_tilecrc, (u32)nkmax);
+        c->d_tilecrc, (u32)g.nkmax);
     HIP_TRY(hipGetLastError());
-    size_t xtmp = c->xscan_tmp_bytes;
-    HIP_TRY(xor_scan(c->d_xscan_tmp, xtmp, c->d_tilecrc, nw, nkmax, c->d_tord, c->d_px, tiles, st));
-    crc32_long_final_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(c->d_px, (u32)pieces, (u32)count,
-                                                                              dev_out);
+    rc = combine_tiles(c, g, nullptr, tiles, st);
+    if (rc) return rc;
+    crc32_long_final_kernel<<<(unsigned)ceil_div(count, 256), 256, 0, st>>>(
+        c->d_local, c->d_segx, (u32)g.nw, (u32)g.nwb, (u32)pieces, (u32)count, dev_out,
+        c->d_scan_state + 1 + c->scan_a_words, ceil_div(g.nseg, kScanTile), reinterpret_cast<u32*>(c->d_scan_state) + 1);
     HIP_TRY(hipGetLastError());
+    c->scan_dirty = false;
     return SUBSPACE_CRC_OK;
   }
   // Any other shape: materialise offsets/lengths and take the ragged path.

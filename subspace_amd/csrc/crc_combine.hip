@@ -1,0 +1,293 @@
+// Scans and the tile-value combine of the ragged and long-message paths, hand-written for
+// gfx950 (no library scan): one single-pass scan per call for the per-message tile counts,
+// and a transpose + segment scan for the per-tile CRC values.
+//
+//  * Tile bases. crc32_ragged_count_scan_kernel computes every message's tile count and
+//    its exclusive prefix sum in ONE pass (decoupled look-back): tile_base[m] = tiles before
+//    message m, tile_base[count] = the batch's total. It also writes the (constant) result
+//    of zero-length messages, zeroes every other output word (the overflow path XORs tile
+//    values into it) and a slot batch's mismatch count, and the descriptor kernel's chunk
+//    hints: chunk_msg[c] = the message holding tile c * kDescTilesPerWave, for up to
+//    kChunkHints chunks per message (the descriptor kernel checks a hint against tile_base
+//    and searches when it does not hold -- a stale entry of an earlier call included).
+//  * Tile values. The main kernels store one value per tile wave-major, tilecrc[w*nkmax + k]
+//    for tile tau = k*nw + w (contiguous per flush: crc_ragged.hip). A message's CRC is the
+//    XOR of its tiles' values, i.e. P(t1 - 1) ^ P(t0 - 1) for the inclusive XOR prefix P in
+//    tile order. P is kept in two levels instead of as a full scan:
+//      segment s = 64 consecutive tiles of one sweep row k (tau = k*nw + 64*b + x, x < 64;
+//                  s = k*nwb + b, nwb = ceil(nw / 64)), ordered like tau;
+//      local[tau] = XOR of the values of tau's segment up to tau (inclusive),
+//      segx[s]    = XOR of all tile values before segment s (exclusive),
+//      P(tau)     = segx[s(tau)] ^ local[tau]                          (tile_prefix below).
+//    tile_segment_scan_kernel reads 64 x 64 blocks of the wave-major array through LDS (both
+//    the reads along k and the writes along w coalesced), scans each 64-tile row segment with
+//    a wave-wide XOR scan, writes local[] in tile order and each segment's XOR; the segment
+//    XORs (1/64 of the tiles) get a single-pass exclusive look-back scan in place. (Storing
+//    local[] only at message-last tiles, the only ones the final kernels read, from a
+//    per-tile end mask written by the descriptor kernel, was slower: 36 -> 43 us at config
+//    C, r02f -- the masked partial-line stores cost as much as full ones.)
+//
+// Look-back scans (Merrill & Garland's decoupled look-back): a workgroup takes a ticket (its
+// position in the scan, so every workgroup it waits for was started before it), scans its
+// 4,096 elements, publishes its aggregate, then wave 0 reads its predecessors' status words
+// 64 at a time -- an inclusive prefix ends the walk -- and publishes its own inclusive
+// prefix. A status word is one 64-bit agent-scope atomic (flag and value together), so no
+// other ordering is needed. The status words and tickets are zeroed at allocation and then
+// by the next kernel of the call that runs after the scan (reset_scan_state, crc_device.h:
+// the descriptor kernel for the tile-count scan, the final kernels for the segment scan),
+// so every call -- and every replay of a captured hipGraph -- starts from a zeroed state.
+#include "crc_device.h"
+
+namespace subspace_amd {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 16;
+constexpr u64 kScanTile = (u64)kScanThreads * kScanItems;  // segment scan: elements per workgroup
+constexpr int kCountItems = 16;
+constexpr u64 kCountTile = (u64)kScanThreads * kCountItems;  // tile-count scan: messages per workgroup
+constexpr u64 kFlagAggregate = 1, kFlagInclusive = 2;
+constexpr u64 kChunkHints = 4;  // chunk-index entries written per message (crc32_ragged_count_scan_kernel)
+
+// Sum of u64 values below 2^62 (tile counts): flag in the top two bits.
+struct SumOp {
+  using T = u64;
+  static __device__ __forceinline__ T identity() { return 0; }
+  static __device__ __forceinline__ T op(T a, T b) { return a + b; }
+  static __device__ __forceinline__ u64 pack(u64 flag, T v) { return (flag << 62) | v; }
+  static __device__ __forceinline__ u64 flag(u64 s) { return s >> 62; }
+  static __device__ __forceinline__ T value(u64 s) { return s & ((1ull << 62) - 1); }
+};
+
+// XOR of u32 values (tile CRC values): flag in the high word.
+struct XorOp {
+  using T = u32;
+  static __device__ __forceinline__ T identity() { return 0; }
+  static __device__ __forceinline__ T op(T a, T b) { return a ^ b; }
+  static __device__ __forceinline__ u64 pack(u64 flag, T v) { return (flag << 32) | v; }
+  static __device__ __forceinline__ u64 flag(u64 s) { return s >> 32; }
+  static __device__ __forceinline__ T value(u64 s) { return (u32)s; }
+};
+
+template <class Op>
+__device__ __forceinline__ typename Op::T shfl_up_t(typename Op::T v, int d) {
+  if constexpr (sizeof(typename Op::T) == 8) {
+    const u32 lo = (u32)__shfl_up((int)(u32)v, d, 64), hi = (u32)__shfl_up((int)(u32)(v >> 32), d, 64);
+    return ((u64)hi << 32) | lo;
+  } else {
+    return (typename Op::T)__shfl_up((int)v, d, 64);
+  }
+}
+
+template <class Op>
+__device__ __forceinline__ typename Op::T shfl_xor_t(typename Op::T v, int m) {
+  if constexpr (sizeof(typename Op::T) == 8) {
+    const u32 lo = (u32)__shfl_xor((int)(u32)v, m, 64), hi = (u32)__shfl_xor((int)(u32)(v >> 32), m, 64);
+    return ((u64)hi << 32) | lo;
+  } else {
+    return (typename Op::T)__shfl_xor((int)v, m, 64);
+  }
+}
+
+// Workgroup ticket: the scan position of this workgroup (0, 1, ... in start order).
+__device__ __forceinline__ u64 scan_ticket(u32* ticket) {
+  __shared__ u32 s_tile;
+  if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+  __syncthreads();
+  return s_tile;
+}
+
+// Exclusive scan of the workgroup's kScanThreads * ITEMS elements x (thread t holds elements
+// t*ITEMS .. +ITEMS-1 of tile `tile`), in place, continued from every earlier tile's
+// elements through the look-back on `status`.
+template <class Op, int ITEMS>
+__device__ __forceinline__ void scan_tile_lookback(typename Op::T (&x)[ITEMS], u64 tile, u64* status) {
+  using T = typename Op::T;
+  __shared__ T s_wave[kScanThreads / 64];
+  __shared__ T s_prefix;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T agg = Op::identity();
+#pragma unroll
+  for (int j = 0; j < ITEMS; j++) agg = Op::op(agg, x[j]);
+  T inc = agg;  // inclusive scan of the thread aggregates over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T o = shfl_up_t<Op>(inc, d);
+    if (lane >= d) inc = Op::op(o, inc);
+  }
+  T excl = shfl_up_t<Op>(inc, 1);
+  if (lane == 0) excl = Op::identity();
+  if (lane == 63) s_wave[wid] = inc;
+  __syncthreads();
+  T wpre = Op::identity(), total = Op::identity();
+#pragma unroll
+  for (int q = 0; q < kScanThreads / 64; q++) {
+    if (q < wid) wpre = Op::op(wpre, s_wave[q]);
+    total = Op::op(total, s_wave[q]);
+  }
+  if (wid == 0) {
+    T prefix = Op::identity();
+    if (tile == 0) {
+      if (lane == 0) __hip_atomic_store(&status[0], Op::pack(kFlagInclusive, total), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(&status[tile], Op::pack(kFlagAggregate, total), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+      i64 base = (i64)tile - 1;
+      while (true) {
+        const i64 idx = base - lane;  // lane 0: the nearest predecessor
+        u64 s = Op::pack(kFlagInclusive, Op::identity());
+        if (idx >= 0) {
+          // every predecessor holds an earlier ticket and publishes; the bound only turns a
+          // broken invariant (stale state) into wrong results instead of a hung GPU
+          u32 spins = 0;
+          do {
+            s = __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } while (Op::flag(s) == 0 && ++spins < (1u << 22));
+          if (Op::flag(s) == 0) s = Op::pack(kFlagInclusive, Op::identity());
+        }
+        const u64 incl = __ballot(Op::flag(s) == kFlagInclusive);
+        const int first = incl ? __ffsll((unsigned long long)incl) - 1 : 63;
+        T v = lane <= first ? Op::value(s) : Op::identity();
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) v = Op::op(v, shfl_xor_t<Op>(v, m));
+        prefix = Op::op(v, prefix);
+        if (incl) break;
+        base -= 64;
+      }
+      if (lane == 0) __hip_atomic_store(&status[tile], Op::pack(kFlagInclusive, Op::op(prefix, total)),
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) s_prefix = prefix;
+  }
+  __syncthreads();
+  T run = Op::op(s_prefix, Op::op(wpre, excl));
+#pragma unroll
+  for (int j = 0; j < ITEMS; j++) {
+    const T v = x[j];
+    x[j] = run;
+    run = Op::op(run, v);
+  }
+}
+
+// Tiles of message (s, L): its extended length L + (s & 15) in 8 KiB tiles (0 if L = 0)
+// (crc_ragged.hip: a message is read from the 16-B block holding its first byte).
+__device__ __forceinline__ u64 msg_tiles(u64 s, u64 len) { return len ? (len + (s & 15) + 8191) >> 13 : 0; }
+
+// Per message: tile count, scanned into tile_base (count + 1 entries); zero-length messages
+// get their result, every other output word is zeroed. `offsets`/`lengths` are read with an
+// element stride (1 for plain arrays, 3 for the payload/size fields of subspace_crc_slot).
+__global__ __launch_bounds__(kScanThreads) void crc32_ragged_count_scan_kernel(
+    const u64* __restrict__ offsets, u32 ostride, const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
+    u32 final_xor, u64* __restrict__ tile_base, u32* __restrict__ out, u32* __restrict__ zero_word,
+    u64* __restrict__ status, u32* __restrict__ ticket, u32* __restrict__ chunk_msg, u64 nchunks) {
+  __shared__ u64 sx[kCountTile];  // striped (coalesced) global order <-> per-thread runs
+  const u64 tile = scan_ticket(ticket);
+  const u64 base = tile * kCountTile;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < kCountItems; j++) {
+    const u64 i = base + (u64)(j * kScanThreads + tid);
+    u64 nt = 0;
+    if (i < count) {
+      nt = msg_tiles(offsets[i * ostride], lengths[i * lstride]);
+      out[i] = nt == 0 ? init ^ final_xor : 0u;
+    } else if (i == count && zero_word) {
+      *zero_word = 0u;  // a slot batch's mismatch count (no separate memset)
+    }
+    sx[j * kScanThreads + tid] = nt;
+  }
+  __syncthreads();
+  u64 x[kCountItems], nt[kCountItems];
+#pragma unroll
+  for (int j = 0; j < kCountItems; j++) x[j] = nt[j] = sx[tid * kCountItems + j];
+  scan_tile_lookback<SumOp, kCountItems>(x, tile, status);  // synchronises before returning
+#pragma unroll
+  for (int j = 0; j < kCountItems; j++) {
+    sx[tid * kCountItems + j] = x[j];
+    // chunk hints: chunks whose first tile lies in this message, [ceil(tb / C), (tb + nt - 1) / C],
+    // at most kChunkHints of them (a longer message's later chunks are found by search)
+    if (nt[j]) {
+      const u64 m = base + (u64)(tid * kCountItems + j);
+      const u64 c0 = (x[j] + kDescTilesPerWave - 1) / kDescTilesPerWave, c1 = (x[j] + nt[j] - 1) / kDescTilesPerWave;
+      for (u64 c = c0; c <= c1 && c < c0 + kChunkHints && c < nchunks; c++) chunk_msg[c] = (u32)m;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kCountItems; j++) {
+    const u64 i = base + (u64)(j * kScanThreads + tid);
+    if (i <= count) tile_base[i] = sx[j * kScanThreads + tid];
+  }
+}
+
+// Tiles present: the batch's total (device value, ragged path) or a host count (long path),
+// bounded by the workspace capacity.
+__device__ __forceinline__ u64 tiles_present(const u64* total_ptr, u64 n) {
+  if (total_ptr) {
+    const u64 t = *total_ptr;
+    return t < n ? t : n;
+  }
+  return n;
+}
+
+// Wave-major tile values -> per-segment inclusive XOR scans in tile order (local) and the
+// XOR of every segment (segx, before its scan). Block (a, b) covers k in [64a, +64) and
+// w in [64b, +64); wave q scans the rows k = 64a + q + 4i.
+__global__ __launch_bounds__(256) void tile_segment_scan_kernel(const u32* __restrict__ in, u32 nw, u32 nkmax,
+                                                                u32 nwb, const u64* __restrict__ total_ptr, u64 n_cap,
+                                                                u32* __restrict__ local, u32* __restrict__ segx) {
+  __shared__ u32 t[64][65];
+  const u64 n = tiles_present(total_ptr, n_cap);
+  const u32 k0 = blockIdx.x * 64u, w0 = blockIdx.y * 64u;
+  if ((u64)k0 * nw + w0 >= n) return;  // every tile of the block is past the batch
+  const u32 x = threadIdx.x & 63u, y0 = threadIdx.x >> 6;
+#pragma unroll
+  for (u32 i = 0; i < 16u; i++) {  // row w0 + y, column k0 + x
+    const u32 y = y0 + 4u * i, w = w0 + y, k = k0 + x;
+    t[y][x] = (w < nw && k < nkmax) ? in[(u64)w * nkmax + k] : 0u;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (u32 i = 0; i < 16u; i++) {  // row k = k0 + y: tiles tau = k*nw + w0 + x
+    const u32 y = y0 + 4u * i, w = w0 + x, k = k0 + y;
+    u32 v = t[x][y];  // 0 past nw
+    // inclusive XOR scan over the 64 lanes: DPP row shifts within each 16-lane row (source
+    // lanes out of the row read as 0), then rows 1, 3 take lane 15 of rows 0, 2 and rows
+    // 2, 3 take lane 31 (VALU only, no LDS round trip)
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    const u64 tau = (u64)k * nw + w;
+    if (k < nkmax) {
+      if (w < nw && tau < n) local[tau] = v;
+      if (x == 63u) segx[(u64)k * nwb + blockIdx.y] = v;
+    }
+  }
+}
+
+// Exclusive XOR scan of the segment values, in place (look-back, one pass). Workgroups past
+// the last segment that holds a tile of the batch leave at once (nothing later reads them).
+__global__ __launch_bounds__(kScanThreads) void segment_prefix_kernel(u32* __restrict__ segx, u64 nseg, u32 nw,
+                                                                      u32 nwb, const u64* __restrict__ total_ptr,
+                                                                      u64 n_cap, u64* __restrict__ status,
+                                                                      u32* __restrict__ ticket) {
+  const u64 tile = scan_ticket(ticket);
+  const u64 n = tiles_present(total_ptr, n_cap);
+  if (n == 0) return;
+  const u64 last = n - 1, need = (last / nw) * nwb + (last % nw) / 64u + 1;  // segments up to the last tile
+  const u64 lim = need < nseg ? need : nseg;
+  if (tile * kScanTile >= lim) return;  // workgroup-uniform
+  const u64 i0 = tile * kScanTile + (u64)threadIdx.x * kScanItems;
+  u32 x[kScanItems];
+#pragma unroll
+  for (int j = 0; j < kScanItems; j++) x[j] = i0 + j < lim ? segx[i0 + j] : 0u;
+  scan_tile_lookback<XorOp, kScanItems>(x, tile, status);
+#pragma unroll
+  for (int j = 0; j < kScanItems; j++)
+    if (i0 + j < lim) segx[i0 + j] = x[j];
+}
+
+}  // namespace subspace_amd

@@ -50,6 +50,11 @@ constexpr int kRagOpWords = kRagInvOps + kNumInvOps * 128;
 constexpr size_t ragged_lds_bytes() { return kLdsOps + (size_t)kRagLdsOpWords * 4u; }
 static_assert(ragged_lds_bytes() <= 160u * 1024u, "ragged kernel LDS exceeds 160 KiB");
 
+// Ragged path: tiles per wave of the descriptor kernel, = the chunk of the tile-count scan's
+// chunk index (chunk_msg[c] = the message holding tile c * kDescTilesPerWave).
+constexpr u64 kDescTilesPerWave = 256;
+static_assert(kDescTilesPerWave % 64 == 0, "descriptor windows are 64-tile aligned");
+
 // Ragged kernel head seeds of one call: v[r] = Z_r^{-1}(init), r = 0..15 (a kernel argument).
 struct HeadSeeds {
   u32 v[16];
@@ -162,6 +167,25 @@ __device__ __forceinline__ u32 step1(u32 crc, u32 b, u32 lc1) {
 // tile's loads, so a wave never has more than one tile of loads outstanding. Inline asm
 // is invisible to hipcc's waitcnt pass, which keeps its own (weaker) waits.
 __device__ __forceinline__ void drain_before_issue() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Inclusive XOR prefix, in tile order tau = k*nw + w, of the per-tile values at tile tau:
+// the XOR of every segment before tau's (segx, exclusive) and of tau's segment up to tau
+// (local). A segment is 64 consecutive tiles of one sweep row, s = k*nwb + w/64
+// (crc_combine.hip). tau < 2^32 (workspace capacities are bounded on the host).
+__device__ __forceinline__ u32 tile_prefix(const u32* __restrict__ local, const u32* __restrict__ segx, u32 nw,
+                                           u32 nwb, u64 tau) {
+  const u32 t = (u32)tau, k = t / nw, w = t - k * nw;
+  return segx[(u64)k * nwb + (w >> 6)] ^ local[t];
+}
+
+// Zero a look-back scan's status words and ticket (grid-stride) from a kernel that runs
+// after that scan in the same call, leaving the state ready for the next call (or graph
+// replay) without a memset (crc_combine.hip).
+__device__ __forceinline__ void reset_scan_state(u64* status, u64 nwords, u32* ticket) {
+  const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x, stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = g; i < nwords; i += stride) __hip_atomic_store(&status[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (g == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

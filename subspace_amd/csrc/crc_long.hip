@@ -15,8 +15,8 @@
 //    DPP reduction give the two 4 KiB halves in lanes 31 and 63; tiles are parked one per
 //    lane and finished every 64 tiles: Z_{8192 * (P-1-j)}( Z_4096(h0) ^ h1 ), final XOR on
 //    the message's first piece, stored to tilecrc wave-major (w * nkmax + k);
-//  * message m's CRC = XOR of its P values = px[(m+1)P - 1] ^ px[mP - 1] over the inclusive
-//    XOR-scan px of the values in tile order (crc_ragged.hip xor_scan; crc32_long_final_kernel).
+//  * message m's CRC = XOR of its P values = P((m+1)P - 1) ^ P(mP - 1) over the inclusive
+//    XOR prefix of the values in tile order (crc_combine.hip; crc32_long_final_kernel).
 #include "crc_device.h"
 
 namespace subspace_amd {
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
       rem >>= 1;
     }
     if (AF >> 31) c ^= final_xor;
-    if (valid) tilecrc[(u64)w * nkmax + kf + (u32)lane] = c;  // wave-major (crc_ragged.hip xor_scan)
+    if (valid) tilecrc[(u64)w * nkmax + kf + (u32)lane] = c;  // wave-major (crc_combine.hip)
   };
 
   LdsFill<WG, kRagLdsOpWords / 128> fill;
@@ -134,12 +134,15 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
 template __global__ void crc32_long_kernel<512>(const uint8_t*, u64, u32, u32, const u32*, const u32*, u32, u32,
                                                 u32*, u32);
 
-// out[m] = XOR of message m's pieces = px[(m+1)P - 1] ^ px[mP - 1].
-__global__ void crc32_long_final_kernel(const u32* __restrict__ px, u32 pieces, u32 count, u32* __restrict__ out) {
+// out[m] = XOR of message m's pieces = P((m+1)P - 1) ^ P(mP - 1).
+__global__ void crc32_long_final_kernel(const u32* __restrict__ local, const u32* __restrict__ segx, u32 nw, u32 nwb,
+                                        u32 pieces, u32 count, u32* __restrict__ out, u64* scan_status,
+                                        u64 scan_words, u32* scan_ticket) {
+  reset_scan_state(scan_status, scan_words, scan_ticket);  // the segment scan is done
   const u32 m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= count) return;
   const u64 last = (u64)(m + 1) * pieces - 1;
-  out[m] = px[last] ^ (m ? px[(u64)m * pieces - 1] : 0u);
+  out[m] = tile_prefix(local, segx, nw, nwb, last) ^ (m ? tile_prefix(local, segx, nw, nwb, (u64)m * pieces - 1) : 0u);
 }
 
 }  // namespace subspace_amd

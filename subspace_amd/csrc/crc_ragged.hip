@@ -30,15 +30,13 @@
 //    with a per-lane binary decomposition of T over nibble operators -- one wave pass
 //    shifts 64 tiles -- and stores them to tilecrc, wave-major ([w][k]: one wave's 64
 //    values are 256 contiguous bytes). A message's padded CRC is the XOR of its tiles'
-//    values, i.e. the difference of two entries of the inclusive XOR-scan of the values in
-//    tile order tau (gathered from the wave-major array; crc32_ragged_final_kernel). No
-//    atomics: huge messages (config D: 8192 tiles each, all in flight at once) would
-//    otherwise serialise every tile on one output word.
+//    values, i.e. the difference of two entries of the inclusive XOR prefix of the values
+//    in tile order tau (crc_combine.hip: tile_segment_scan_kernel, segment_prefix_kernel;
+//    crc32_ragged_final_kernel). No atomics: huge messages (config D: 8192 tiles each, all
+//    in flight at once) would otherwise serialise every tile on one output word.
 //    (Batches whose tiles overflow the workspace -- overlapping messages -- fall back to
 //    atomicXor into pre-zeroed words.)
 //  * Loads never touch a 16-B block that holds no byte of the message.
-#include <hipcub/hipcub.hpp>
-
 #include "crc_device.h"
 
 namespace subspace_amd {
@@ -51,29 +49,6 @@ struct TileDesc {
 };
 static_assert(sizeof(TileDesc) == 16, "TileDesc is 16 B");
 constexpr u32 kFirstTile = 0x80000000u;
-
-// Tiles of message (s, L): its extended length L + (s & 15) in 8 KiB tiles (0 if L = 0).
-__host__ __device__ inline u64 tiles_for(u64 s, u64 len) { return len ? (len + (s & 15) + 8191) >> 13 : 0; }
-
-// Per message: tile count; zero-length messages get their (constant) result here, every
-// other output word is zeroed (the overflow path XORs tile values into it).
-// `offsets` and `lengths` are read with an element stride (1 for plain arrays, 3 for the
-// payload/size fields of subspace_crc_slot records).
-__global__ void crc32_ragged_count_kernel(const u64* __restrict__ offsets, u32 ostride,
-                                          const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
-                                          u32 final_xor, u64* __restrict__ ntiles, u32* __restrict__ out,
-                                          u32* __restrict__ zero_word) {
-  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > count) return;
-  if (i == count) {
-    ntiles[i] = 0;  // scan sentinel: tile_base[count] = total tiles
-    if (zero_word) *zero_word = 0u;  // a slot batch's mismatch count (no separate memset)
-    return;
-  }
-  const u64 nt = tiles_for(offsets[i * ostride], lengths[i * lstride]);
-  ntiles[i] = nt;
-  out[i] = nt == 0 ? init ^ final_xor : 0u;
-}
 
 __device__ inline u64 find_msg(const u64* __restrict__ tile_base, u64 count, u64 tau) {
   // last m with tile_base[m] <= tau (skips zero-tile messages, whose base equals the next one's)
@@ -101,31 +76,45 @@ __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, u32 ostrid
 }
 
 // Per tile (up to `capacity`): its descriptor. Sets *overflow if the batch has more tiles.
-// Wave g covers tiles [g*kDescTilesPerWave, +kDescTilesPerWave): ONE binary search (the
-// same address in every lane) finds the message of its first tile; then per 64-tile window
-// lane l holds tile_base[m0 + l] (one coalesced load) and each lane finds its tile's message
-// with a 6-step shuffle search over those 64 bases. Only a window whose 64 candidates do not
-// reach a lane's tile (runs of zero-length messages) searches globally for that lane. A
-// search per tile (the previous form) cost 20 dependent loads per tile (0.25 ms on config C).
-constexpr u64 kDescTilesPerWave = 1024;
+// Wave g covers tiles [g*kDescTilesPerWave, +kDescTilesPerWave). The message of its first
+// tile comes from the tile-count scan's chunk hint (chunk_msg[g], crc_combine.hip: one load
+// instead of a 20-step binary search), checked with the first window's candidates and
+// replaced by a search where it does not hold (chunks deep inside a long message get no
+// hint); then per 64-tile window lane l holds tile_base[m0 + l]
+// (one coalesced load) and each lane finds its tile's message with a 6-step shuffle search
+// over those 64 bases. Only a window whose 64 candidates do not reach a lane's tile (runs of
+// zero-length messages) searches globally for that lane. A search per tile (the first form)
+// cost 20 dependent loads per tile (0.25 ms on config C); a binary search per wave for its
+// first tile's message (before the chunk index) 14 us more per config-C call (r02f).
 __global__ __launch_bounds__(256) void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, u32 ostride,
                                                                 const u64* __restrict__ lengths, u32 lstride,
                                                                 const u64* __restrict__ tile_base, u64 count,
-                                                                u64 capacity, TileDesc* __restrict__ desc,
-                                                                u32* __restrict__ overflow) {
+                                                                u64 capacity, const u32* __restrict__ chunk_msg,
+                                                                TileDesc* __restrict__ desc, u32* __restrict__ overflow, u64* scan_status,
+                                                                u64 scan_words, u32* scan_ticket) {
+  reset_scan_state(scan_status, scan_words, scan_ticket);  // the tile-count scan is done
   const u64 total = tile_base[count];
   const u64 limit = total < capacity ? total : capacity;
   const int lane = threadIdx.x & 63;
   if (blockIdx.x == 0 && threadIdx.x == 0) *overflow = total > capacity ? 1u : 0u;
-  const u64 t_begin = (((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * kDescTilesPerWave;
+  const u64 g = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const u64 t_begin = g * kDescTilesPerWave;
   if (t_begin >= limit) return;  // wave-uniform
   const u64 t_end = t_begin + kDescTilesPerWave < limit ? t_begin + kDescTilesPerWave : limit;
-  u64 m0 = find_msg(tile_base, count, t_begin);  // tile_base[m0] <= t_begin < tile_base[m0 + 1]
+  u64 m0 = chunk_msg[g];  // a hint: tile_base[m0] <= t_begin < tile_base[m0 + 1] if it holds
   for (u64 t0 = t_begin; t0 < t_end; t0 += 64) {
     const u64 tau = t0 + (u64)lane;
-    const u64 mc = m0 + (u64)lane;
+    u64 mc = m0 + (u64)lane;
     // nondecreasing over lanes; tile_base[count] = total > every tile, past it: +inf
-    const u64 cand = mc <= count ? tile_base[mc] : ~(u64)0;
+    u64 cand = mc <= count ? tile_base[mc] : ~(u64)0;
+    if (t0 == t_begin) {  // check the hint (lanes 0, 1 hold tile_base[m0], tile_base[m0 + 1])
+      const u64 b0 = __shfl(cand, 0, 64), b1 = __shfl(cand, 1, 64);
+      if (!(m0 < count && b0 <= t_begin && t_begin < b1)) {
+        m0 = find_msg(tile_base, count, t_begin);
+        mc = m0 + (u64)lane;
+        cand = mc <= count ? tile_base[mc] : ~(u64)0;
+      }
+    }
     int lo = 0;  // last lane with cand <= tau (lane 0 always: cand_0 <= t0 <= tau)
 #pragma unroll
     for (int step = 32; step; step >>= 1) {
@@ -370,14 +359,18 @@ template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u3
                                                   const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds,
                                                   u32*, u32*, u64);
 
-// Per message with tiles: its padded CRC = XOR of its tiles' values = px[last] ^
-// px[first - 1] (px = inclusive XOR-scan of the tile values), or the XOR the overflow path
-// accumulated in out[m]; then the padding undone -- Z_p^{-1} for p = -(L + mis) mod 8192,
-// as p's bits over the inverse operators Z_{2^b}^{-1} -- and the final XOR applied.
+// Per message with tiles: its padded CRC = XOR of its tiles' values = P(t1 - 1) ^ P(t0 - 1)
+// (P = inclusive XOR prefix of the tile values in tile order, crc_combine.hip), or the XOR
+// the overflow path accumulated in out[m]; then the padding undone -- Z_p^{-1} for
+// p = -(L + mis) mod 8192, as p's bits over the inverse operators Z_{2^b}^{-1} -- and the
+// final XOR applied.
 __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, const u64* __restrict__ offsets,
                                           u32 ostride, const u64* __restrict__ lengths, u32 lstride, u64 count,
-                                          const u32* __restrict__ px, const u32* __restrict__ overflow,
-                                          const u32* __restrict__ gops, u32 final_xor, u32* __restrict__ out) {
+                                          const u32* __restrict__ local, const u32* __restrict__ segx, u32 nw, u32 nwb,
+                                          const u32* __restrict__ overflow, const u32* __restrict__ gops,
+                                          u32 final_xor, u32* __restrict__ out, u64* scan_status, u64 scan_words,
+                                          u32* scan_ticket) {
+  reset_scan_state(scan_status, scan_words, scan_ticket);  // the segment scan is done
   // the 13 inverse operators (6.5 KiB) staged in LDS: up to 104 dependent table lookups
   // per message read from global memory took 61 us for config C's 1 Mi messages (r01bu)
   __shared__ u32 inv[kNumInvOps * 128];
@@ -387,7 +380,8 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
   if (m >= count) return;
   const u64 t0 = tile_base[m], t1 = tile_base[m + 1];
   if (t1 == t0) return;  // empty message: written by the count kernel
-  u32 v = *overflow ? out[m] : px[t1 - 1] ^ (t0 ? px[t0 - 1] : 0u);
+  u32 v = *overflow ? out[m]
+                    : tile_prefix(local, segx, nw, nwb, t1 - 1) ^ (t0 ? tile_prefix(local, segx, nw, nwb, t0 - 1) : 0u);
   const u32 pad = (u32)(0 - (lengths[m * lstride] + (offsets[m * ostride] & 15))) & 8191u;
 #pragma unroll 1
   for (int b = 0; b < kNumInvOps; b++) {
@@ -400,56 +394,6 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
     }
   }
   out[m] = v ^ final_xor;
-}
-
-// hipcub scan wrappers: exclusive prefix sum of per-message tile counts; inclusive XOR
-// scan of per-tile values in tile order tau, transposed from the kernels' wave-major array
-// (tile tau = k*nw + w sits at w*nkmax + k). The flush stores are the reason for that
-// layout: 64 lanes storing tilecrc[tau] directly hit 64 lines 4*nw bytes apart, each
-// shared by waves of every XCD, and cost 8 % of the long kernel's time at config D
-// (r01aw); the transpose reads and writes 8 B per tile.
-hipError_t ragged_scan(void* temp, size_t& temp_bytes, const u64* in, u64* out, u64 n, hipStream_t stream) {
-  return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, stream);
-}
-
-struct XorOp {
-  __host__ __device__ u32 operator()(u32 a, u32 b) const { return a ^ b; }
-};
-
-// Wave-major tile values -> tile order: out[k*nw + w] = in[w*nkmax + k] for tau < n, through
-// 64 x 64 LDS tiles (reads along k and writes along w both coalesced). Gathering inside the
-// scan instead (a transform iterator, 64-bit div/mod per element and 4-B reads nkmax*4 B apart)
-// cost 185 us at config C's 15.4 M tiles (r01bt).
-__global__ __launch_bounds__(256) void tile_values_to_tau_order(const u32* __restrict__ in, u32 nw, u32 nkmax,
-                                                                u32* __restrict__ out, u64 n) {
-  __shared__ u32 t[64][65];
-  const u32 k0 = blockIdx.x * 64u, w0 = blockIdx.y * 64u;
-  const u32 x = threadIdx.x & 63u, y0 = threadIdx.x >> 6;
-#pragma unroll
-  for (u32 i = 0; i < 16u; i++) {  // row w0 + y, column k0 + x
-    const u32 y = y0 + 4u * i, w = w0 + y, k = k0 + x;
-    t[y][x] = (w < nw && k < nkmax) ? in[(u64)w * nkmax + k] : 0u;
-  }
-  __syncthreads();
-#pragma unroll
-  for (u32 i = 0; i < 16u; i++) {  // tau = (k0 + y)*nw + w0 + x
-    const u32 y = y0 + 4u * i, w = w0 + x, k = k0 + y;
-    const u64 tau = (u64)k * nw + w;
-    if (w < nw && k < nkmax && tau < n) out[tau] = t[x][y];
-  }
-}
-
-// Inclusive XOR-scan of the first n tile values in tile order. `tord` (n words) holds the
-// transposed values; a size query (temp == nullptr) launches nothing.
-hipError_t xor_scan(void* temp, size_t& temp_bytes, const u32* in, u64 nw, u64 nkmax, u32* tord, u32* out, u64 n,
-                    hipStream_t stream) {
-  if (temp != nullptr && n > 0) {
-    const dim3 grid((unsigned)((nkmax + 63) / 64), (unsigned)((nw + 63) / 64));
-    tile_values_to_tau_order<<<grid, 256, 0, stream>>>(in, (u32)nw, (u32)nkmax, tord, n);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  return hipcub::DeviceScan::InclusiveScan(temp, temp_bytes, tord, out, XorOp(), (int)n, stream);
 }
 
 }  // namespace subspace_amd

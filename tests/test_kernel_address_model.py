@@ -196,15 +196,31 @@ def test_xcd_group_slot_is_a_bijection(wg, grid):
         assert len({xcd[16 * g + i] for i in range(16)}) == 1
 
 
-def desc_kernel_messages(ntiles, capacity, per_wave=1024):
-    """Replays crc32_ragged_desc_kernel's message lookup: per wave, one search for its first
-    tile, then per 64-tile window a search over the 64 candidate bases tile_base[m0 + l]
-    (+inf past tile_base[count]), the global search when the last candidate is reached, and
-    the next window's m0 = lane 63's message. Returns {tile: message}."""
+def chunk_index(ntiles, nchunks, per_wave=256, hints=4, stale=None):
+    """Replays the chunk hints crc32_ragged_count_scan_kernel writes: for every message with
+    tiles, chunk_msg[c] = m for the first `hints` chunks c whose first tile c * per_wave lies
+    in it. Other entries keep what an earlier call left (`stale`, default garbage)."""
+    tb = np.concatenate([[0], np.cumsum(ntiles, dtype=np.int64)])
+    chunk = np.array(stale if stale is not None else np.full(nchunks, 2**32 - 1), dtype=np.int64)
+    for m, nt in enumerate(ntiles):
+        if nt:
+            c0, c1 = -(-int(tb[m]) // per_wave), (int(tb[m]) + int(nt) - 1) // per_wave
+            for c in range(c0, min(c1, c0 + hints - 1, nchunks - 1) + 1):
+                chunk[c] = m
+    return chunk
+
+
+def desc_kernel_messages(ntiles, capacity, per_wave=256, stale=None):
+    """Replays crc32_ragged_desc_kernel's message lookup: per wave, its first tile's message
+    from the chunk index, then per 64-tile window a search over the 64 candidate bases
+    tile_base[m0 + l] (+inf past tile_base[count]), the global search when the last candidate
+    is reached, and the next window's m0 = lane 63's message. Returns ({tile: message},
+    tile_base)."""
     count = len(ntiles)
     tb = np.concatenate([[0], np.cumsum(ntiles, dtype=np.int64)])  # tile_base, count + 1 entries
     total = int(tb[count])
     limit = min(total, capacity)
+    chunk = chunk_index(ntiles, -(-capacity // per_wave), per_wave, stale=stale)
 
     def find_msg(tau):  # last m < count with tb[m] <= tau
         return int(np.searchsorted(tb[:count], tau, side="right")) - 1
@@ -212,9 +228,12 @@ def desc_kernel_messages(ntiles, capacity, per_wave=1024):
     got = {}
     for t_begin in range(0, limit, per_wave):
         t_end = min(t_begin + per_wave, limit)
-        m0 = find_msg(t_begin)
+        m0 = int(chunk[t_begin // per_wave])  # a hint, checked against the first window
         for t0 in range(t_begin, t_end, 64):
             cand = [int(tb[m0 + l]) if m0 + l <= count else 1 << 62 for l in range(64)]
+            if t0 == t_begin and not (m0 < count and cand[0] <= t_begin < cand[1]):
+                m0 = find_msg(t_begin)
+                cand = [int(tb[m0 + l]) if m0 + l <= count else 1 << 62 for l in range(64)]
             ms = []
             for lane in range(64):
                 tau = t0 + lane
@@ -242,8 +261,9 @@ def test_desc_window_search_matches_binary_search(seed):
         parts.append(rng.integers(3, 300, int(rng.integers(0, 3))))        # multi-tile messages
     ntiles = np.concatenate(parts).astype(np.int64)
     total = int(ntiles.sum())
-    for capacity in (total, total - 37, 64 * 5 + 3):
-        got, tb = desc_kernel_messages(ntiles, capacity)
+    for capacity, stale in ((total, None), (total - 37, None), (64 * 5 + 3, None),
+                            (total, rng.integers(0, len(ntiles) + 5, -(-total // 256)))):
+        got, tb = desc_kernel_messages(ntiles, capacity, stale=stale)
         assert sorted(got) == list(range(min(total, capacity)))
         for tau, m in got.items():
             assert tb[m] <= tau < tb[m + 1], (capacity, tau, m)

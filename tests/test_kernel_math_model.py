@@ -194,3 +194,56 @@ def test_uniform_per_lane_operators_and_dpp_reduction():
                 lanes.append(apply(ops[31 - l], crc_raw(init if l == 0 else 0, line)))
         red = dpp_half_xor(lanes)
         assert red[31] == ref(init, msgs[0]) and red[63] == ref(init, msgs[1])
+
+
+def _segment_combine_model(values_tau, nw):
+    """Replay of crc_combine.hip on the CPU: the wave-major array the main kernels write
+    (tile tau = k*nw + w at w*nkmax + k), tile_segment_scan_kernel (64-tile row segments,
+    inclusive XOR scan per segment, segment XORs), segment_prefix_kernel (exclusive XOR scan
+    of the segment XORs) and tile_prefix (crc_device.h)."""
+    n = len(values_tau)
+    nkmax = -(-max(n, 1) // nw)
+    nwb = -(-nw // 64)
+    wave_major = np.zeros(nw * nkmax, dtype=np.uint32)
+    tau = np.arange(n)
+    wave_major[(tau % nw) * nkmax + tau // nw] = values_tau
+    local = np.zeros(n, dtype=np.uint32)
+    segx = np.zeros(nkmax * nwb, dtype=np.uint32)
+    for k in range(nkmax):
+        for b in range(nwb):
+            row = np.zeros(64, dtype=np.uint32)
+            for x in range(64):
+                w = 64 * b + x
+                if w < nw:
+                    row[x] = wave_major[w * nkmax + k]
+            scan = np.bitwise_xor.accumulate(row)
+            for x in range(64):
+                w = 64 * b + x
+                t = k * nw + w
+                if w < nw and t < n:
+                    local[t] = scan[x]
+            segx[k * nwb + b] = scan[63]
+    excl = np.zeros_like(segx)
+    excl[1:] = np.bitwise_xor.accumulate(segx)[:-1]
+
+    def tile_prefix(t):
+        k, w = t // nw, t % nw
+        return int(excl[k * nwb + (w >> 6)] ^ local[t])
+    return tile_prefix
+
+
+@pytest.mark.parametrize("nw,n", [(128, 1000), (2048, 5000), (96, 777), (64, 64), (2048, 1)])
+def test_segment_prefix_decomposition_equals_full_xor_scan(nw, n):
+    """P(tau) = segx[s(tau)] ^ local[tau] is the inclusive XOR prefix in tile order, for
+    nw a multiple of 64 or not (the last segment of a row is then short)."""
+    rng = np.random.default_rng(nw * 7 + n)
+    vals = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    tp = _segment_combine_model(vals, nw)
+    full = np.bitwise_xor.accumulate(vals)
+    for t in list(range(min(n, 300))) + list(range(max(0, n - 300), n)):
+        assert tp(t) == int(full[t])
+    # a message [t0, t1) is P(t1 - 1) ^ P(t0 - 1)
+    t0, t1 = n // 3, max(n // 3 + 1, 2 * n // 3)
+    if t1 <= n:
+        want = int(np.bitwise_xor.reduce(vals[t0:t1]))
+        assert tp(t1 - 1) ^ (tp(t0 - 1) if t0 else 0) == want
