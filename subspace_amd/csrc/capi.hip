@@ -16,8 +16,9 @@
 
 namespace subspace_amd {
 
-template <int WG>
-__global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int, u32*);
+template <int WG, bool SLOT>
+__global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int, u32*,
+                                       SlotArgs);
 
 struct TileDesc;
 __global__ void crc32_ragged_count_scan_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
@@ -148,6 +149,8 @@ struct subspace_crc_ctx {
   u32* d_crc0 = nullptr;  // slot batches: payload CRCs from init 0
   u64* d_soff = nullptr;  // slot batches: payload offsets of the contiguous layout
   u64 s_capacity = 0;
+  u64* d_slot_counter = nullptr;  // fused slot kernel: (workgroups done << 32) | mismatches, 0 between calls
+  bool fused_slots = true;        // contiguous 4 KiB slot batches take the fused uniform kernel
 };
 
 namespace {
@@ -403,10 +406,15 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess) e = hipMemcpy(c->d_rops, rops.data(), rops.size() * 4, hipMemcpyHostToDevice);
 #define SET_LDS(WGV)                                                                                         \
   if (e == hipSuccess)                                                                                       \
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                            (int)uniform_lds_bytes(WGV / 64));
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV, false>,                                  \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_lds_bytes(WGV / 64));
   SET_LDS(256) SET_LDS(512) SET_LDS(768) SET_LDS(1024)
 #undef SET_LDS
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)uniform_slot_lds_bytes(8));
+  if (e == hipSuccess) e = hipMalloc(&c->d_slot_counter, sizeof(u64));
+  if (e == hipSuccess) e = hipMemset(c->d_slot_counter, 0, sizeof(u64));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_ragged_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)ragged_lds_bytes());
@@ -457,6 +465,7 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_overflow);
   (void)hipFree(c->d_uoff);
   (void)hipFree(c->d_ulen);
+  (void)hipFree(c->d_slot_counter);
   delete c;
 }
 
@@ -508,10 +517,9 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     if (c->uniform_blocks > 0 && (u64)c->uniform_blocks < (u64)blocks) blocks = c->uniform_blocks;
     const auto* b = static_cast<const uint8_t*>(dev_base);
     const int ord = c->uniform_order;
-#define LAUNCH(WGV)                                                                                    \
-  crc32_uniform4k_kernel<WGV><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(b, stride, count, c->d_tab,         \
-                                                                                c->d_laneops, init, final_xor, dev_out, ord,  \
-                                                                                c->zero_word)
+#define LAUNCH(WGV)                                                                                           \
+  crc32_uniform4k_kernel<WGV, false><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(                             \
+      b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, SlotArgs{})
     switch (wg) {
       case 256: LAUNCH(256); break;
       case 768: LAUNCH(768); break;
@@ -622,9 +630,21 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
     return fail(SUBSPACE_CRC_EINVAL, "slot_stride %llu < prefix %llu + message %llu",
                 (unsigned long long)slot_stride, (unsigned long long)prefix_size, (unsigned long long)message_size);
   HIP_TRY(hipSetDevice(c->device));
+  auto* buf = static_cast<uint8_t*>(dev_buffer);
+  // Fused path (crc_uniform.hip SLOT): 4 KiB payloads, 16-B aligned, no metadata span -- the
+  // payload CRC, the span-0 term and the flag/checksum store or status in one kernel
+  if (!dev_message_sizes && message_size == 4096 && metadata_size == 0 && slot_stride % 16 == 0 &&
+      ((uintptr_t)(buf + prefix_size) % 16) == 0 && c->fused_slots) {
+    const int blocks = grid_for(c, (count + 1) / 2, 512 / 64);
+    SlotArgs sa{prefix_size, mode, dev_status, dev_crc_out, dev_error_count, c->d_slot_counter};
+    crc32_uniform4k_kernel<512, true><<<blocks, 512, uniform_slot_lds_bytes(8), st>>>(
+        buf + prefix_size, slot_stride, count, c->d_tab, c->d_rops, 0u, 0xFFFFFFFFu, nullptr, c->uniform_order,
+        nullptr, sa);
+    HIP_TRY(hipGetLastError());
+    return SUBSPACE_CRC_OK;
+  }
   rc = ensure_slot_ws(c, count);
   if (rc) return rc;
-  auto* buf = static_cast<uint8_t*>(dev_buffer);
   want_zeroed(c, dev_error_count);
   if (dev_message_sizes) {
     slot_payload_offsets_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(slot_stride, prefix_size, count,
@@ -895,12 +915,18 @@ int subspace_crc32_host_slot_list(subspace_crc_ctx* c, const subspace_crc_slot* 
 }
 
 // Experiment hook (not part of the public header): named knobs.
-//   "long_path": 1 (default) whole-8 KiB-piece uniform batches take crc32_long_kernel,
-//                0 they take the ragged path
+//   "long_path":   1 (default) whole-8 KiB-piece uniform batches take crc32_long_kernel,
+//                  0 they take the ragged path
+//   "fused_slots": 1 (default) contiguous 4 KiB slot batches without metadata take the
+//                  fused slot kernel, 0 the payload kernel + crc32_slot_finish_kernel
 int subspace_crc_testutil_set(subspace_crc_ctx* c, const char* key, int value) {
   if (!c || !key) return SUBSPACE_CRC_EINVAL;
   if (!std::strcmp(key, "long_path")) {
     c->long_path = value != 0;
+    return SUBSPACE_CRC_OK;
+  }
+  if (!std::strcmp(key, "fused_slots")) {
+    c->fused_slots = value != 0;
     return SUBSPACE_CRC_OK;
   }
   return SUBSPACE_CRC_EINVAL;

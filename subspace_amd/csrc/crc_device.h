@@ -34,6 +34,23 @@ constexpr int kLaneOpWords = 8 * 16 * 32;  // [nibble k][value n][lane slot s]: 
 constexpr u32 kUniRing = kLdsOps + kLaneOpWords * 4u;
 constexpr int kUniRingResults = 256;  // results per wave ring (128 tiles)
 constexpr size_t uniform_lds_bytes(int waves) { return kUniRing + (size_t)waves * 4u * kUniRingResults; }
+// Slot variant (crc_uniform.hip, SLOT = true): tables, line-shift operators, the Z_4096 opmul
+// slot (the ragged operator array's slot 32), then per-wave rings of one 64-message window.
+constexpr int kUniSlotOpZ4096 = kLaneOpWords * 4 / 512;  // opmul slot 32
+constexpr u32 kUniSlotRing = kLdsOps + (kLaneOpWords + 128) * 4u;
+constexpr int kUniSlotRingResults = 64;
+constexpr size_t uniform_slot_lds_bytes(int waves) { return kUniSlotRing + (size_t)waves * 4u * kUniSlotRingResults; }
+
+// Fused slot checksums of the uniform 4 KiB kernel: the message-slot layout of
+// subspace_crc32_slots_strided with metadata_size 0 (crc_uniform.hip, crc_slots.hip).
+struct SlotArgs {
+  u64 prefix_size;     // payload = prefix + prefix_size; the kernel's base points at payload 0
+  u32 mode;            // SUBSPACE_CRC_SLOT_CALCULATE (0) / _VERIFY (1)
+  u32* status;         // optional, per slot
+  u32* crc_out;        // optional (CALCULATE): stored checksum per slot
+  u32* error_count;    // optional (VERIFY): mismatches of this call
+  u64* counter;        // context word: (workgroups done << 32) | mismatches so far; 0 between calls
+};
 
 // Ragged-kernel layout: tables, the same line-shift operators, then opmul slots Z_4096 and
 // Z_{8192 * 2^k}, k = 0..20 (8 KiB .. 8 GiB). The device operator array continues with

@@ -21,15 +21,29 @@
 //    a store in the stream makes the wait for the next tile's loads wait for the store's
 //    write-back too: a store every 4 tiles cost ~10 % of a streaming kernel's rate
 //    (tools/ubench/streamread.hip lines_store: 6.0 vs 6.6 TB/s).
+//  * SLOT = true: the message-slot checksums of a contiguous channel layout
+//    (subspace_crc32_slots_strided, metadata_size 0) in the same pass, no second kernel.
+//    Message i's payload is at base + i*stride, its MessagePrefix prefix_size bytes before.
+//    The checksum (client/checksum.h:29-37 over common/channel.h:527-542's spans) is
+//      ~crc_raw(~0, span0 || payload) = ~( Z_4096(crc_raw(~0, span0)) ^ crc_raw(0, payload) )
+//    with span0 = prefix[4, 48). The payload term is this kernel's message CRC from init 0.
+//    Per window of 32 tiles (64 messages, one per lane) each lane loads its message's 64-B
+//    prefix line -- issued with the window's first tile loads, so it lands with them -- and at
+//    the window's end computes crc_raw(~0, span0) (11 steps, flag bit set first for a
+//    publish, as SetHasChecksum() precedes the checksum: client/publisher.cc:664-675) and
+//    one Z_4096 opmul, XORs it into its ring slot and stores flag + checksum (publish) or
+//    the status (verify: client/client.cc:1346-1356; no kMessageHasChecksum -> unchecked).
+//    Mismatches are counted per workgroup and summed by one 64-bit atomic per workgroup
+//    that also counts finished workgroups; the last one writes the call's total.
 #include "crc_device.h"
 
 namespace subspace_amd {
 
-template <int WG>
+template <int WG, bool SLOT>
 __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __restrict__ base, u64 stride, u64 count,
                                                              const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                              u32 init, u32 final_xor, u32* __restrict__ out,
-                                                             int order, u32* __restrict__ zero_word) {
+                                                             int order, u32* __restrict__ zero_word, SlotArgs sa) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
   // a word the caller's next kernel accumulates into (a slot batch's mismatch count): zeroed
@@ -42,8 +56,8 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
-  constexpr int kRing = kUniRingResults;
-  const u32 ring = sbase + kUniRing + (u32)wid * (4u * kRing);
+  constexpr int kRing = SLOT ? kUniSlotRingResults : kUniRingResults;
+  const u32 ring = sbase + (SLOT ? kUniSlotRing : kUniRing) + (u32)wid * (4u * kRing);
   const u32 lop = sbase + kLdsOps + 4u * (u32)(31 - (lane & 31));  // this lane's operator slot
   const int l = lane & 31, h = lane >> 5;
   const u64 ntiles = (count + 1) >> 1;
@@ -127,6 +141,61 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
     if (l == 31) lds_st(ring + 4u * (2u * (k - kf) + (u32)h), v ^ final_xor);
   };
+  // SLOT: the current window's prefix lines (lane j: message j of the window), their span-0
+  // term P = Z_4096(crc_raw(~0, span0)), stored checksum S, flags word F, the flag as found.
+  u32x4 Q[4];
+  u32 P = 0, S = 0, F = 0, mism = 0;
+  bool HAS = false;
+  const bool calc = sa.mode == 0u;
+  // message of lane j in the window of tiles kf.. (clamped like load_tile for the loads)
+  auto win_msg = [&](u32 kf, bool clamp) {
+    const u32 t = kf + ((u32)lane >> 1);
+    const u32 kk = !clamp ? t : (t < nk ? t : (nk ? nk - 1 : 0u));
+    u64 msg = (nk || !clamp) ? 2 * (t0 + (u64)kk * tstep) + (u64)(lane & 1) : 0;
+    if (clamp) msg = msg < count ? msg : msg - 1;
+    return msg;
+  };
+  auto load_prefix = [&](u32 kf) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(base + win_msg(kf, true) * stride - sa.prefix_size);
+#pragma unroll
+    for (int i = 0; i < 4; i++) Q[i] = q[i];
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto prefix_pass = [&]() {
+    u32 w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = Q[i >> 2][i & 3];
+    HAS = (w[8] & 4u) != 0u;  // kMessageHasChecksum in MessagePrefix::flags (common/channel.h:62-70)
+    F = calc ? (w[8] | 4u) : w[8];
+    w[8] = F;
+    u32 hh = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 1; i < 12; i++) hh = step4(hh ^ w[i], lc0, lc1);  // span 0 = prefix bytes [4, 48)
+    P = opmul(sbase, kUniSlotOpZ4096, hh);
+    S = w[12];  // the stored checksum (first 4 B of the checksum area, prefix + 48)
+  };
+  // Finish the window's messages: lane j takes ring slot j (its payload CRC, complemented)
+  // and XORs in its span-0 term; then stores flag + checksum, or the status.
+  auto slot_flush = [&](u32 kf, u32 nt) {
+    const u64 msg = win_msg(kf, false);
+    const bool valid = ((u32)lane >> 1) < nt && msg < count;
+    const u32 r = lds_ld(ring + 4u * (u32)lane) ^ P;
+    u32* pw = reinterpret_cast<u32*>(const_cast<uint8_t*>(base) + msg * stride - sa.prefix_size);
+    if (calc) {
+      if (valid) {
+        pw[8] = F;   // SetHasChecksum()
+        pw[12] = r;  // *reinterpret_cast<uint32_t*>(checksum.data()) = ~crc (client/checksum.h:36)
+        if (sa.status) sa.status[msg] = 0u;
+        if (sa.crc_out) sa.crc_out[msg] = r;
+      }
+    } else {
+      const u32 st = !HAS ? 2u : (r == S ? 0u : 1u);  // client/checksum.h:46
+      if (valid && sa.status) sa.status[msg] = st;
+      mism += (u32)__builtin_popcountll(__ballot(valid && st == 1u));
+    }
+    wave_lds_sync();
+  };
+
   // Store the ring's results of tiles kf .. kf+nt-1 (messages 2*tau, 2*tau+1 of each).
   auto flush = [&](u32 kf, u32 nt) {
 #pragma unroll
@@ -141,13 +210,18 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
 
   // Table loads first, then tile 0's loads, then the LDS stores: tile 0's latency hides
   // behind the fill and the barrier.
-  LdsFill<WG, kLaneOpWords / 128> fill;  // step tables + per-lane operators
+  // (SLOT: + the Z_4096 slot; gops is then the ragged operator array, which starts with the
+  // same line-shift operators)
+  LdsFill<WG, kLaneOpWords / 128 + (SLOT ? 1 : 0)> fill;  // step tables + per-lane operators
   fill.load(gtab, gops);
   u32x4 A[8], B[8];
   load_tile(A, 0);
+  if constexpr (SLOT) load_prefix(0);
   fill.store(sbase);
   __syncthreads();
-  if (nk == 0) return;
+  if constexpr (!SLOT) {
+    if (nk == 0) return;
+  }  // SLOT: every wave reaches the workgroup's mismatch sum at the end
 
   // Ping-pong buffers, loop unrolled by two (no early exit: a break between the halves
   // would give the loop head a predecessor with fewer loads in flight, and hipcc's waitcnt
@@ -157,14 +231,31 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // profiles/r01/ceiling.md), and tile k+1's latency still hides behind tile k's compute.
   // A full ring is stored right after the next tile's loads are issued, so the stores
   // retire during that tile's compute instead of stalling the next drain (crc_long.hip).
+  // SLOT: a window's prefix lines are loaded with its first tile's loads and their span-0
+  // terms computed right after the drain that follows (mid-stream, where one wave's short
+  // delay is hidden by the others, instead of in the tail); the window ends right after a
+  // drain, before the next tile's loads, where its messages are finished and stored and the
+  // next window's prefix lines are loaded.
   u32 k = 0, kf = 0;
+  bool pdone = false;  // the current window's prefix pass has run
   for (; k + 1 < nk; k += 2) {
     drain_before_issue();
-    load_tile(B, k + 1);
-    if (k - kf == (u32)(kRing / 2)) {
-      wave_lds_sync();
-      flush(kf, kRing / 2);
-      kf = k;
+    if constexpr (SLOT) {
+      if (k - kf == (u32)(kRing / 2)) {
+        wave_lds_sync();
+        slot_flush(kf, kRing / 2);
+        load_prefix(k);
+        kf = k;
+        pdone = false;
+      }
+      load_tile(B, k + 1);
+    } else {
+      load_tile(B, k + 1);
+      if (k - kf == (u32)(kRing / 2)) {
+        wave_lds_sync();
+        flush(kf, kRing / 2);
+        kf = k;
+      }
     }
     tile_result(line_crc(A), k, kf);
     drain_before_issue();
@@ -173,23 +264,53 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   }
   if (k < nk) {  // odd last tile, already loaded
     if (k - kf == (u32)(kRing / 2)) {
-      wave_lds_sync();
-      flush(kf, kRing / 2);
+      if constexpr (SLOT) {
+        wave_lds_sync();
+        slot_flush(kf, kRing / 2);
+        load_prefix(k);
+        pdone = false;
+      } else {
+        wave_lds_sync();
+        flush(kf, kRing / 2);
+      }
       kf = k;
     }
     tile_result(line_crc(A), k, kf);
   }
   wave_lds_sync();
-  if (nk > kf) flush(kf, nk - kf);
+  if constexpr (SLOT) {
+    if (!pdone) prefix_pass();
+    slot_flush(kf, nk > kf ? nk - kf : 0u);
+    // the call's mismatch count: one 64-bit atomic per workgroup adds (1 << 32) | its count;
+    // the workgroup that sees G - 1 finished before it writes the total and resets the word
+    if (!calc && sa.error_count) {
+      const u32 mring = sbase + kUniSlotRing + (u32)wid * (4u * kRing);
+      if (lane == 0) lds_st(mring, mism);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        u32 n = 0;
+#pragma unroll
+        for (int q = 0; q < WG / 64; q++) n += lds_ld(sbase + kUniSlotRing + (u32)q * (4u * kRing));
+        const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(sa.counter), (1ull << 32) | (u64)n);
+        if ((u32)(old >> 32) == gridDim.x - 1u) {
+          *sa.error_count = (u32)old + n;
+          __hip_atomic_store(sa.counter, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  } else {
+    if (nk > kf) flush(kf, nk - kf);
+  }
 }
 
-template __global__ void crc32_uniform4k_kernel<256>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                     int, u32*);
-template __global__ void crc32_uniform4k_kernel<512>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                     int, u32*);
-template __global__ void crc32_uniform4k_kernel<768>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                     int, u32*);
-template __global__ void crc32_uniform4k_kernel<1024>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*,
-                                                     int, u32*);
+#define INST(WGV, SL)                                                                                          \
+  template __global__ void crc32_uniform4k_kernel<WGV, SL>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, \
+                                                           u32*, int, u32*, SlotArgs);
+INST(256, false)
+INST(512, false)
+INST(768, false)
+INST(1024, false)
+INST(512, true)
+#undef INST
 
 }  // namespace subspace_amd

@@ -306,3 +306,106 @@ def test_drain_helper_cpp(gpu_ctx):
     assert d["device"] and d["failures"] == 0
     assert d["mismatches"] == d["expected_mismatches"] >= 3 and d["unchecked"] >= 1
     assert d["unregistered_rejected"]
+
+
+def _corrupt(host, po, ps, cs, sizes, seed):
+    """Corruptions of test_verify_statuses (payload bit, span 0, stored checksum, uncovered
+    padding, flag cleared) on a published channel; returns the kinds applied per slot."""
+    rng = np.random.default_rng(seed)
+    kinds = rng.integers(0, 8, len(po))
+    for i, k in enumerate(kinds):
+        b, n = int(po[i]), int(sizes[i])
+        if k == 1 and n:
+            host[b + ps + rng.integers(0, n)] ^= np.uint8(1 << rng.integers(0, 8))
+        elif k == 3:
+            host[b + 4 + rng.integers(0, 44)] ^= 0x01
+        elif k == 4:
+            host[b + 48 + rng.integers(0, 4)] ^= 0x80
+        elif k == 5:
+            host[b:b + 4] ^= 0xFF
+            host[b + 48 + cs:b + ps] ^= 0xAA
+        elif k == 6:
+            host[b + 32] &= 0xFB
+    return kinds
+
+
+@pytest.mark.parametrize("count", [1, 2, 3, 63, 4097, 65537, 140001])
+@pytest.mark.parametrize("cs", [4, 20])
+def test_fused_slot_kernel_publish_and_verify(gpu_ctx, oracle, count, cs):
+    """The fused slot kernel (contiguous 4 KiB slots, metadata_size 0: payload CRC, span-0
+    term and flag/checksum store or status in one pass; crc_uniform.hip SLOT): publish is
+    byte-identical to the oracle's publisher restatement; verify statuses and the mismatch
+    count equal the oracle's subscriber restatement after corruptions. Counts cover waves
+    without tiles, odd last tiles, partial and several 32-tile windows per wave."""
+    ms = 0
+    sizes = np.full(count, 4096, dtype=np.uint64)
+    host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=count + cs)
+    dev, status = publish_strided(gpu_ctx, host, stride, count, cs, ms, message_size=4096)
+    po, yo = offsets(count, stride, ps)
+    oracle.publish_slots(host, po, yo, sizes, cs, ms)
+    assert (status == 0).all()
+    got = dev.cpu().numpy()
+    bad = np.nonzero(got != host)[0]
+    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+    _corrupt(host, po, ps, cs, sizes, seed=count * 3 + cs)
+    want = oracle.verify_slots(host, po, yo, sizes, cs, ms)
+    dev = torch.from_numpy(host).to(DEV)
+    st = torch.full((count,), 7, dtype=torch.int32, device=DEV)
+    err = torch.full((1,), 12345, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_slots_strided(dev, stride, count, message_size=4096, checksum_size=cs, metadata_size=ms,
+                                mode=gpu.SLOT_VERIFY, status=st, error_count=err)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy().view(np.uint32), want)
+    assert int(err.item()) == int((want == 1).sum())
+    assert np.array_equal(dev.cpu().numpy(), host)  # verify never writes the channel
+    # the error count of the next call starts from zero again (no status array this time)
+    err2 = torch.full((1,), 999, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_slots_strided(dev, stride, count, message_size=4096, checksum_size=cs, metadata_size=ms,
+                                mode=gpu.SLOT_VERIFY, error_count=err2)
+    torch.cuda.synchronize()
+    assert int(err2.item()) == int((want == 1).sum())
+
+
+def test_fused_and_two_kernel_slot_paths_agree(gpu_ctx):
+    """fused_slots off (payload kernel + crc32_slot_finish_kernel) and on give the same
+    channel bytes and statuses."""
+    from subspace_amd import _lib
+    lib = _lib.load()
+    count, cs, ms = 20001, 4, 0
+    sizes = np.full(count, 4096, dtype=np.uint64)
+    host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=4242)
+    out = []
+    for fused in (0, 1):
+        assert lib.subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", fused) == 0
+        try:
+            dev, status = publish_strided(gpu_ctx, host.copy(), stride, count, cs, ms, message_size=4096)
+            out.append((dev.cpu().numpy(), status))
+        finally:
+            lib.subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", 1)
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+
+
+def test_fused_slot_verify_graph_replay(gpu_ctx):
+    """The fused verify (with its self-resetting mismatch counter) captured in a hipGraph:
+    every replay reports the same mismatch count."""
+    count, cs, ms = 5000, 4, 0
+    sizes = np.full(count, 4096, dtype=np.uint64)
+    host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=31)
+    dev = torch.from_numpy(host).to(DEV)
+    gpu_ctx.crc32_slots_strided(dev, stride, count, message_size=4096, mode=gpu.SLOT_CALCULATE)
+    torch.cuda.synchronize()
+    for i in (5, 777, 4999):
+        dev[i * stride + ps + 100] ^= 1
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            gpu_ctx.crc32_slots_strided(dev, stride, count, message_size=4096, mode=gpu.SLOT_VERIFY, error_count=err)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        err.fill_(-1)
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(err.item()) == 3
