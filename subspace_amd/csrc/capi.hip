@@ -96,7 +96,7 @@ struct subspace_crc_ctx {
   u32* d_tab = nullptr;  // 4 x 256 slice tables
   u32* d_rops = nullptr;  // ragged kernel: line-shift operators, Z_4096, tile shifts, padding inverses
   u32* d_pow2 = nullptr;  // Z_{2^k}, k = 0..63, nibble operators (slot checksums)
-  u32* d_laneops = nullptr;  // uniform kernel: Z_{128*s}, s = 0..31, as [nibble][value][s]
+  u32* d_laneops = nullptr;  // uniform kernel: Z_{128*s}, s = 0..31, as [nibble][value][s]; Z_4096
   Tables host_tab;
   Mat32 zinv1;  // Z_1^{-1}: the ragged kernel's head seeds Z_r^{-1}(init)
   // ragged workspace
@@ -373,7 +373,7 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   c->host_tab = make_tables(poly);
   c->zinv1 = inverse(z_one(c->host_tab));
 
-  std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kLaneOpWords, 0u), rops(kRagOpWords, 0u);
+  std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kUniOpSlots * 128, 0u), rops(kRagOpWords, 0u);
   for (int k = 0; k < 4; k++)
     for (int b = 0; b < 256; b++) tab[k * 256 + b] = c->host_tab.t[k][b];
 
@@ -389,7 +389,8 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
       for (int n = 0; n < 16; n++) laneops[((size_t)k * 16 + n) * 32 + sl] = nt[k * 16 + n];
   }
   // ragged kernel: the line-shift operators, Z_4096, then Z_{8192 * 2^k} for k = 0..30
-  std::copy(laneops.begin(), laneops.end(), rops.begin());
+  std::copy(laneops.begin(), laneops.begin() + kLaneOpWords, rops.begin());
+  nibble_tables(z_bytes(c->host_tab, 4096), &laneops[128 * kUniSlotOpZ4096]);
   nibble_tables(z_bytes(c->host_tab, 4096), &rops[kLaneOpWords]);
   for (int k = 0; k < 31; k++) nibble_tables(z_bytes(c->host_tab, 8192ull << k), &rops[kLaneOpWords + 128 * (1 + k)]);
   // the ragged final kernel's padding inverses Z_{2^b}^{-1}, b = 0..12
@@ -638,7 +639,7 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
     const int blocks = grid_for(c, (count + 1) / 2, 512 / 64);
     SlotArgs sa{prefix_size, mode, dev_status, dev_crc_out, dev_error_count, c->d_slot_counter};
     crc32_uniform4k_kernel<512, true><<<blocks, 512, uniform_slot_lds_bytes(8), st>>>(
-        buf + prefix_size, slot_stride, count, c->d_tab, c->d_rops, 0u, 0xFFFFFFFFu, nullptr, c->uniform_order,
+        buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, c->uniform_order,
         nullptr, sa);
     HIP_TRY(hipGetLastError());
     return SUBSPACE_CRC_OK;

@@ -29,15 +29,20 @@ constexpr u32 kLdsTables = 0;
 constexpr u32 kLdsOps = 128u * 1024u;  // operator area; opmul slot s = 512 B at kLdsOps + 512*s
 
 // Uniform-kernel layout: tables, the per-lane line-shift operators (kLaneOpWords, see
-// crc32_uniform4k_kernel), then a per-wave ring of results awaiting their store.
+// crc32_uniform4k_kernel), the opmul slot Z_4096 (slot variant), then a per-wave ring of
+// results awaiting their store (the device operator array d_laneops holds the same
+// kUniOpSlots slots).
 constexpr int kLaneOpWords = 8 * 16 * 32;  // [nibble k][value n][lane slot s]: 16 KiB
-constexpr u32 kUniRing = kLdsOps + kLaneOpWords * 4u;
-constexpr int kUniRingResults = 256;  // results per wave ring (128 tiles)
-constexpr size_t uniform_lds_bytes(int waves) { return kUniRing + (size_t)waves * 4u * kUniRingResults; }
-// Slot variant (crc_uniform.hip, SLOT = true): tables, line-shift operators, the Z_4096 opmul
-// slot (the ragged operator array's slot 32), then per-wave rings of one 64-message window.
 constexpr int kUniSlotOpZ4096 = kLaneOpWords * 4 / 512;  // opmul slot 32
-constexpr u32 kUniSlotRing = kLdsOps + (kLaneOpWords + 128) * 4u;
+constexpr int kUniOpSlots = kUniSlotOpZ4096 + 1;
+constexpr u32 kUniRing = kLdsOps + kUniOpSlots * 512u;
+// results per wave ring: 256 (128 tiles), or 128 where 16 waves' rings would not fit
+constexpr int uni_ring_results(int waves) { return kUniRing + (u32)waves * 1024u <= 160u * 1024u ? 256 : 128; }
+constexpr size_t uniform_lds_bytes(int waves) { return kUniRing + (size_t)waves * 4u * uni_ring_results(waves); }
+static_assert(uniform_lds_bytes(16) <= 160u * 1024u && uniform_lds_bytes(8) <= 160u * 1024u,
+              "uniform kernel LDS exceeds 160 KiB");
+// Slot variant (crc_uniform.hip, SLOT = true): the same, with rings of one 64-message window.
+constexpr u32 kUniSlotRing = kUniRing;
 constexpr int kUniSlotRingResults = 64;
 constexpr size_t uniform_slot_lds_bytes(int waves) { return kUniSlotRing + (size_t)waves * 4u * kUniSlotRingResults; }
 

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
-  constexpr int kRing = SLOT ? kUniSlotRingResults : kUniRingResults;
+  constexpr int kRing = SLOT ? kUniSlotRingResults : uni_ring_results(WG / 64);
   const u32 ring = sbase + (SLOT ? kUniSlotRing : kUniRing) + (u32)wid * (4u * kRing);
   const u32 lop = sbase + kLdsOps + 4u * (u32)(31 - (lane & 31));  // this lane's operator slot
   const int l = lane & 31, h = lane >> 5;
@@ -128,7 +128,6 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
       for (int j = 0; j < 4; j++) crc = step4(crc ^ d[i][j], lc0, lc1);
     return crc;
   };
-
   // Message CRCs of tile k into ring slots 2*(k - kf) + h (kf = first tile of the window).
   auto tile_result = [&](u32 crc, u32 k, u32 kf) {
     u32 v = 0;
@@ -210,9 +209,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
 
   // Table loads first, then tile 0's loads, then the LDS stores: tile 0's latency hides
   // behind the fill and the barrier.
-  // (SLOT: + the Z_4096 slot; gops is then the ragged operator array, which starts with the
-  // same line-shift operators)
-  LdsFill<WG, kLaneOpWords / 128 + (SLOT ? 1 : 0)> fill;  // step tables + per-lane operators
+  LdsFill<WG, kUniOpSlots> fill;  // step tables, per-lane operators, Z_4096
   fill.load(gtab, gops);
   u32x4 A[8], B[8];
   load_tile(A, 0);
@@ -231,22 +228,21 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // profiles/r01/ceiling.md), and tile k+1's latency still hides behind tile k's compute.
   // A full ring is stored right after the next tile's loads are issued, so the stores
   // retire during that tile's compute instead of stalling the next drain (crc_long.hip).
-  // SLOT: a window's prefix lines are loaded with its first tile's loads and their span-0
-  // terms computed right after the drain that follows (mid-stream, where one wave's short
-  // delay is hidden by the others, instead of in the tail); the window ends right after a
-  // drain, before the next tile's loads, where its messages are finished and stored and the
-  // next window's prefix lines are loaded.
+  // SLOT: a window's prefix lines are loaded with its first tile's loads; the window ends
+  // right after a drain, before the next tile's loads, where its span-0 terms are computed
+  // and its messages finished and stored, and the next window's prefix lines are loaded.
+  // (Computing the span-0 terms right after the window's first drain instead -- so that only
+  // the stores remain at the end -- ran 62 vs 50 us at config S in an interleaved A/B, r02l.)
   u32 k = 0, kf = 0;
-  bool pdone = false;  // the current window's prefix pass has run
   for (; k + 1 < nk; k += 2) {
     drain_before_issue();
     if constexpr (SLOT) {
       if (k - kf == (u32)(kRing / 2)) {
+        prefix_pass();
         wave_lds_sync();
         slot_flush(kf, kRing / 2);
         load_prefix(k);
         kf = k;
-        pdone = false;
       }
       load_tile(B, k + 1);
     } else {
@@ -265,10 +261,10 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   if (k < nk) {  // odd last tile, already loaded
     if (k - kf == (u32)(kRing / 2)) {
       if constexpr (SLOT) {
+        prefix_pass();
         wave_lds_sync();
         slot_flush(kf, kRing / 2);
         load_prefix(k);
-        pdone = false;
       } else {
         wave_lds_sync();
         flush(kf, kRing / 2);
@@ -279,7 +275,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   }
   wave_lds_sync();
   if constexpr (SLOT) {
-    if (!pdone) prefix_pass();
+    prefix_pass();
     slot_flush(kf, nk > kf ? nk - kf : 0u);
     // the call's mismatch count: one 64-bit atomic per workgroup adds (1 << 32) | its count;
     // the workgroup that sees G - 1 finished before it writes the total and resets the word
