@@ -9,7 +9,7 @@ LIB := subspace_amd/libsubspace_crc.so
 OBJDIR := build/obj
 
 HIP_SRCS := $(CSRC)/crc_uniform.hip $(CSRC)/crc_ragged.hip $(CSRC)/crc_long.hip $(CSRC)/crc_combine.hip $(CSRC)/crc_slots.hip $(CSRC)/capi.hip $(CSRC)/testutil.hip
-CPP_SRCS := $(CSRC)/host_crc.cpp
+CPP_SRCS := $(CSRC)/host_crc.cpp $(CSRC)/split_alloc.cpp
 HDRS := $(CSRC)/crc_device.h $(CSRC)/crc_math.h include/subspace_crc.h
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))
 
@@ -42,8 +42,44 @@ tools/drain_demo: tools/drain_demo.cpp include/subspace/checksum.h include/subsp
 test-cpu: all
 	python -m pytest tests/ -x -q -m "not gpu"
 
+# ---- AddressSanitizer + UBSan build of the host code (CPU only; GPU sanitizers are not
+# available on the pool). The g++-compiled host sources (host CRC, split allocator) are
+# instrumented; the HIP objects are linked in unchanged (their host side is the C-ABI
+# argument checking, exercised through the same tests). Everything links against gcc's
+# runtime: python runs with it preloaded, ASan's leak checker off (CPython's own
+# allocations), every UBSan finding fatal.
+ASAN_DIR := build/asan
+ASAN_FLAGS := -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=all -g -O1
+ASAN_LIB := $(ASAN_DIR)/libsubspace_crc.so
+ASAN_HOST_OBJS := $(patsubst $(CSRC)/%.cpp,$(ASAN_DIR)/%.o,$(CPP_SRCS))
+HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
+
+$(ASAN_DIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(ASAN_DIR)
+	g++ -std=c++17 -fPIC -Wall $(ASAN_FLAGS) -c $< -o $@
+
+$(ASAN_LIB): $(ASAN_HOST_OBJS) $(HIP_OBJS)
+	g++ -shared -fPIC $(ASAN_FLAGS) -o $@ $(ASAN_HOST_OBJS) $(HIP_OBJS) -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+
+$(ASAN_DIR)/config_a: tools/config_a.cpp include/subspace/checksum.h $(ASAN_LIB)
+	g++ -std=c++17 $(ASAN_FLAGS) -Iinclude -o $@ tools/config_a.cpp -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN' -ldl
+
+$(ASAN_DIR)/drain_demo: tools/drain_demo.cpp include/subspace/checksum.h include/subspace/checksum_batch.h include/subspace_crc.h $(ASAN_LIB)
+	g++ -std=c++17 -Wall $(ASAN_FLAGS) -Iinclude -o $@ tools/drain_demo.cpp -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN'
+
+$(ASAN_DIR)/c_binding: tests/c/c_binding.c include/subspace_crc.h $(ASAN_LIB)
+	gcc -std=c11 -Wall -Wextra $(ASAN_FLAGS) -Iinclude -o $@ tests/c/c_binding.c -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN'
+
+asan: $(ASAN_LIB) $(ASAN_DIR)/config_a $(ASAN_DIR)/drain_demo $(ASAN_DIR)/c_binding
+
+asan-test: asan oracle
+	ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
+	LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $$(gcc -print-file-name=libubsan.so)" \
+	SUBSPACE_CRC_PROBE_LIB=$(CURDIR)/$(ASAN_LIB) SUBSPACE_CRC_ASAN_DIR=$(CURDIR)/$(ASAN_DIR) \
+	python -m pytest tests/test_host_api.py tests/test_capi.py tests/test_split_alloc.py tests/test_c_binding.py -q -m "not gpu" -p no:cacheprovider
+
 clean:
 	rm -rf build $(LIB) tools/config_a tools/drain_demo
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle test-cpu clean
+.PHONY: all oracle test-cpu clean asan asan-test

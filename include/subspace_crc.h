@@ -25,6 +25,7 @@
 #ifndef SUBSPACE_CRC_H_
 #define SUBSPACE_CRC_H_
 
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -180,6 +181,71 @@ int subspace_crc32_host_slot_list(subspace_crc_ctx* ctx, const subspace_crc_slot
  * mapped + portable); release with subspace_crc_host_unregister (same pointer). */
 int subspace_crc_host_register(void* host_ptr, uint64_t bytes);
 int subspace_crc_host_unregister(void* host_ptr);
+
+/* ---------------------------------------------------------------------------------
+ * Split-buffer allocator: pinned + device-mapped shared memory for a channel's split
+ * buffers (common/split_buffer.h:43-55: the per-slot payload buffers and the prefix buffer
+ * of a channel whose publisher set PublisherOptions::SetSplitBufferCallbacks,
+ * client/options.h:242-249; subscribers: SubscriberOptions, :404-411). The four functions
+ * have exactly the C signatures of the reference C client's SubspaceSplitAllocateCallback,
+ * SubspaceSplitMapCallback and SubspaceSplitReleaseCallback (c_client/subspace.h:140-158);
+ * the two structs below are layout-identical restatements of SubspaceSplitBufferInfo
+ * (c_client/subspace.h:109-119) and SubspaceSplitBufferMapping (:120-127), so a C client
+ * passes them in a SubspaceSplitBufferCallbacks unchanged, and
+ * the C++ client gets them through the reference's own ToCppSplitCallbacks
+ * (c_client/subspace.cc:201-255).
+ *
+ * allocate: a memfd of allocation_size (full_size if 0) bytes, mapped shared read/write,
+ *           then pinned and mapped for device access (subspace_crc_host_register), so the
+ *           zero-copy slot-list path (subspace_crc32_host_slot_list) reads and writes it
+ *           in place. mapping->fd = mapping->handle = the memfd (the reference shares it
+ *           with subscribers through the server), mapping->size, mapping->address.
+ * map:      a subscriber's view of a buffer another process allocated: mmap of the
+ *           descriptor info->registration_fd (else mapping->handle, as the C++ adapter
+ *           presets it) at info->map_offset, then pinned and device-mapped the same way.
+ * unmap:    unpin, munmap. free: unpin, munmap, close the memfd.
+ * user_data: NULL, or a subspace_crc_split_allocator selecting the options below.
+ * Each returns true on success; on failure false, with subspace_crc_last_error() set.
+ * --------------------------------------------------------------------------------- */
+typedef struct subspace_crc_split_info {
+  const char* channel_name;
+  uint64_t session_id;
+  uint32_t buffer_index;
+  uint32_t slot_id;
+  bool is_prefix;
+  uint64_t full_size;
+  uint64_t allocation_size;
+  uintptr_t handle;
+  int registration_fd;
+  int64_t map_offset;
+} subspace_crc_split_info;
+
+typedef struct subspace_crc_split_mapping {
+  uintptr_t handle;
+  void* address;
+  size_t size;
+  void* private_data;
+  int fd;
+  int64_t map_offset;
+} subspace_crc_split_mapping;
+
+/* subspace_crc_split_allocator.flags */
+#define SUBSPACE_CRC_SPLIT_REQUIRE_PIN 0x1u /* fail when pinning fails (default: keep the plain mapping) */
+
+typedef struct subspace_crc_split_allocator {
+  uint32_t flags;
+} subspace_crc_split_allocator;
+
+bool subspace_crc_split_allocate(const subspace_crc_split_info* info, subspace_crc_split_mapping* mapping,
+                                 void* user_data);
+bool subspace_crc_split_map(const subspace_crc_split_info* info, subspace_crc_split_mapping* mapping,
+                            void* user_data);
+bool subspace_crc_split_unmap(const subspace_crc_split_info* info, const subspace_crc_split_mapping* mapping,
+                              void* user_data);
+bool subspace_crc_split_free(const subspace_crc_split_info* info, const subspace_crc_split_mapping* mapping,
+                             void* user_data);
+/* 1 if the mapping of `address` is pinned and device-mapped, 0 if not, -1 if unknown. */
+int subspace_crc_split_is_pinned(const void* address);
 
 #ifdef __cplusplus
 }

@@ -34,6 +34,11 @@ EXPORTED_SYMBOLS = (
     "subspace_crc32_host_slot_list",
     "subspace_crc_host_register",
     "subspace_crc_host_unregister",
+    "subspace_crc_split_allocate",
+    "subspace_crc_split_map",
+    "subspace_crc_split_unmap",
+    "subspace_crc_split_free",
+    "subspace_crc_split_is_pinned",
 )
 
 _lib = None

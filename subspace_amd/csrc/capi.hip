@@ -89,6 +89,17 @@ constexpr u64 ceil_div(u64 a, u64 b) { return (a + b - 1) / b; }
 
 }  // namespace
 
+namespace subspace_amd {
+// The thread-local error string for the library's host-only sources (split_alloc.cpp).
+int set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+}  // namespace subspace_amd
+
 struct subspace_crc_ctx {
   int device = 0;
   uint32_t poly = kPoly;  // reflected CRC polynomial of every table and operator below

@@ -2,6 +2,7 @@
 against the oracle and the golden fixtures. CPU only: these are product host paths,
 not GPU fallbacks (the batch API has none)."""
 import json
+import os
 import shutil
 import subprocess
 from pathlib import Path
@@ -14,6 +15,28 @@ from subspace_amd import checksum as ck
 ROOT = Path(__file__).resolve().parent.parent
 GOLDEN = json.loads((Path(__file__).parent / "golden" / "golden.json").read_text())
 M32 = 0xFFFFFFFF
+# `make asan-test` sets this: the compiled programs below are then AddressSanitizer + UBSan
+# builds linked against the sanitized library (Makefile "asan")
+ASAN_DIR = os.environ.get("SUBSPACE_CRC_ASAN_DIR")
+ASAN_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all", "-g"]
+
+
+def cxx_build(src, exe, *extra):
+    """Compile and link a test program against the library (the sanitized one under asan)."""
+    libdir = Path(ASAN_DIR) if ASAN_DIR else ROOT / "subspace_amd"
+    flags = ASAN_FLAGS if ASAN_DIR else []
+    subprocess.run(["g++", "-std=c++17", "-O1", *flags, *extra, f"-I{ROOT / 'include'}", str(src), "-o", str(exe),
+                    f"-L{libdir}", "-lsubspace_crc", f"-Wl,-rpath,{libdir}"], check=True)
+
+
+def tool(name):
+    """tools/<name>, or its sanitized build under asan."""
+    if ASAN_DIR:
+        return Path(ASAN_DIR) / name
+    exe = ROOT / "tools" / name
+    if not exe.exists():
+        subprocess.run(["make", "-C", str(ROOT), f"tools/{name}"], check=True)
+    return exe
 
 
 def test_kats(lib):
@@ -140,9 +163,7 @@ def test_header_drop_in_compiles_and_links(lib, tmp_path):
     src = tmp_path / "t.cc"
     src.write_text(CPP_TEST)
     exe = tmp_path / "t"
-    libdir = ROOT / "subspace_amd"
-    subprocess.run(["g++", "-std=c++17", "-O1", f"-I{ROOT / 'include'}", str(src), "-o", str(exe),
-                    f"-L{libdir}", "-lsubspace_crc", f"-Wl,-rpath,{libdir}"], check=True)
+    cxx_build(src, exe)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip() == "ok"
@@ -172,9 +193,7 @@ def test_header_castagnoli_build(lib, tmp_path):
     src = tmp_path / "c.cc"
     src.write_text(CPP_CASTAGNOLI)
     exe = tmp_path / "c"
-    libdir = ROOT / "subspace_amd"
-    subprocess.run(["g++", "-std=c++17", "-DSUBSPACE_CRC_CASTAGNOLI", f"-I{ROOT / 'include'}", str(src), "-o",
-                    str(exe), f"-L{libdir}", "-lsubspace_crc", f"-Wl,-rpath,{libdir}"], check=True)
+    cxx_build(src, exe, "-DSUBSPACE_CRC_CASTAGNOLI")
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0 and r.stdout.strip() == "e3069283", r.stdout + r.stderr
 
@@ -182,10 +201,7 @@ def test_header_castagnoli_build(lib, tmp_path):
 def test_config_a_harness(lib):
     """tools/config_a (BASELINE configs[0]): 1 pub x 1 sub calc+verify through the drop-in
     header over a memfd channel; every message verifies, both legs report latencies."""
-    import json
-    exe = ROOT / "tools" / "config_a"
-    if not exe.exists():
-        subprocess.run(["make", "-C", str(ROOT), "tools/config_a"], check=True)
+    exe = tool("config_a")
     r = subprocess.run([str(exe), "500", str(ROOT / "oracle" / "liboracle_crc.so")], capture_output=True, text=True,
                        timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -199,10 +215,7 @@ def test_drain_helper_builds_and_reports_no_device(lib):
     builds; without a usable device the helper reports the context error instead of
     touching memory (exit 77, "device": false). On a GPU machine it runs the whole drain
     (the GPU test checks its results)."""
-    import json
-    exe = ROOT / "tools" / "drain_demo"
-    if not exe.exists():
-        subprocess.run(["make", "-C", str(ROOT), "tools/drain_demo"], check=True)
+    exe = tool("drain_demo")
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     d = json.loads(r.stdout.strip().splitlines()[-1])
     if r.returncode == 77:
