@@ -771,8 +771,8 @@ def main():
             scaling = "strong"
         value = total_bytes / elapsed / 2**30
         achieved = step_bytes / (avg_kern_ms * 1e-3) / 1e9
-        kernel = {"B": "subspace_amd::crc32_uniform4k_kernel<512>",
-                  "E": "subspace_amd::crc32_uniform4k_kernel<512>",
+        kernel = {"B": "subspace_amd::crc32_uniform4k_kernel<512, false>",
+                  "E": "subspace_amd::crc32_uniform4k_kernel<512, false>",
                   "C": "subspace_amd::crc32_ragged_kernel<512> + prep (whole call)"}[args.workload]
         line = {
             "metric": METRIC,
