@@ -544,7 +544,7 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     return SUBSPACE_CRC_OK;
   }
   // Long messages in whole 8 KiB pieces, 16-B aligned (config D): the long-message kernel
-  // (implicit tiles, plain loads), then the XOR-scan combine of the ragged path.
+  // (implicit tiles, plain loads), then the segment-scan combine of the ragged path (crc_combine.hip).
   const u64 pieces = length / 8192;
   const bool long_fast = length >= 8192 && length % 8192 == 0 && (stride % 16) == 0 &&
                          ((uintptr_t)dev_base % 16) == 0 && pieces <= (1ull << kNumTileOps) &&
