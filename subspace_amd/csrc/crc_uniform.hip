@@ -234,7 +234,9 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // (Computing the span-0 terms right after the window's first drain instead -- so that only
   // the stores remain at the end -- ran 62 vs 50 us at config S in an interleaved A/B, r02l.)
   u32 k = 0, kf = 0;
-  for (; k + 1 < nk; k += 2) {
+  // SLOT: the loop stops before the wave's last pair, which follows it: the last window's
+  // span-0 terms are computed while the wave's last tile is in flight
+  for (; SLOT ? k + 2 < nk : k + 1 < nk; k += 2) {
     drain_before_issue();
     if constexpr (SLOT) {
       if (k - kf == (u32)(kRing / 2)) {
@@ -258,6 +260,28 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     load_tile(A, k + 2);
     tile_result(line_crc(B), k + 1, kf);
   }
+  bool pdone = false;  // SLOT: the current window's span-0 terms are computed
+  if constexpr (SLOT) {
+    if (k + 1 < nk) {  // the last pair: tile k loaded, tile k+1 the wave's last
+      drain_before_issue();
+      if (k - kf == (u32)(kRing / 2)) {
+        prefix_pass();
+        wave_lds_sync();
+        slot_flush(kf, kRing / 2);
+        load_prefix(k);
+        kf = k;
+      }
+      load_tile(B, k + 1);
+      if (k != kf) {  // the window's prefix lines landed a tile ago: overlap with tile k+1's loads
+        prefix_pass();
+        pdone = true;
+      }
+      tile_result(line_crc(A), k, kf);
+      drain_before_issue();
+      tile_result(line_crc(B), k + 1, kf);
+      k += 2;
+    }
+  }
   if (k < nk) {  // odd last tile, already loaded
     if (k - kf == (u32)(kRing / 2)) {
       if constexpr (SLOT) {
@@ -275,7 +299,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   }
   wave_lds_sync();
   if constexpr (SLOT) {
-    prefix_pass();
+    if (!pdone) prefix_pass();
     slot_flush(kf, nk > kf ? nk - kf : 0u);
     // the call's mismatch count: one 64-bit atomic per workgroup adds (1 << 32) | its count;
     // the workgroup that sees G - 1 finished before it writes the total and resets the word
