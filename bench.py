@@ -94,6 +94,10 @@ def parse():
                          "default C,D,Du,S with workload B, none otherwise; 'none' disables)")
     ap.add_argument("--config-iters", type=int, default=20)
     ap.add_argument("--no-solo", action="store_true", help="N > 1: skip rank 0's single-GPU reference leg")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N > 1 on a one-GPU machine: every rank on cuda:0, gloo instead of RCCL -- the GPU "
+                         "workload, timing, gather and single-GPU legs of a multi-GPU run, for tests (the ranks "
+                         "share one GPU, so the rates are not scaling numbers)")
     ap.add_argument("--dry-run-cpu", action="store_true",
                     help="CPU + gloo rehearsal of the spawn/shard/gather path (host SubspaceCRC32), for tests")
     return ap.parse_args()
@@ -671,17 +675,21 @@ def main():
     import torch
     import torch.distributed as dist
     from subspace_amd import gpu
-    if torch.cuda.device_count() <= local:
+    gpu_index = 0 if args.rehearse_one_gpu else local
+    if torch.cuda.device_count() <= gpu_index:
         die(f"LOCAL_RANK {local} but only {torch.cuda.device_count()} visible GPU(s)")
     if world > 1:
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(gpu_index)
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu_index))
         if dist.get_world_size() != args.gpus:
-            die(f"RCCL sees {dist.get_world_size()} ranks, --gpus {args.gpus}")
-    dev = torch.device("cuda", local)
+            die(f"the process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    dev = torch.device("cuda", gpu_index)
     torch.cuda.set_device(dev)
-    ctx = gpu.CrcContext(local)
+    ctx = gpu.CrcContext(gpu_index)
     stream = torch.cuda.current_stream()
 
     wl = Workload(args.workload, ctx, dev, world, rank)

@@ -1,0 +1,36 @@
+"""bench.py's multi-rank GPU path, rehearsed on one GPU (the 8-GPU runs are the driver's).
+
+`python bench.py --gpus 2 --rehearse-one-gpu` spawns two ranks through
+torch.distributed.run exactly as `--gpus 2` does, but both ranks use cuda:0 and gloo stands
+in for RCCL: each rank builds its shard on the GPU, runs the kernels, times its steps
+between barriers (max over ranks), all_gathers its 4-byte CRCs from device tensors, rank 0
+checks the whole list against the fixture hash and then times the whole batch alone on its
+GPU (the efficiency leg). Rates are not scaling numbers here (the ranks share one GPU)."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+
+
+@pytest.mark.parametrize("workload", ["E", "B"])
+def test_two_ranks_on_one_gpu(workload):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--rehearse-one-gpu", "--workload",
+                        workload, "--steps", "5", "--warmup", "1", "--settle", "0"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["single_gpu"]["bitexact_vs_golden"] is True
+    if workload == "E":
+        assert d["bitexact_vs_golden"] is True and d["scaling"] == "strong"
+        assert d["config"]["gather_ms"] is not None
+    assert d["efficiency"] > 0 and d["per_gpu_value"] == pytest.approx(d["value"] / 2, rel=1e-2)
