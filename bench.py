@@ -487,7 +487,7 @@ def secondary_configs(ctx, dev, names, iters) -> dict:
     def u64t(a):
         return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(dev)
 
-    for name in names:
+    def one_config(name):
         if name in ("C", "Cu"):
             lengths = synth.ragged_lengths(synth.SEED_C, GOLD["C"]["count"])
             offsets, total = synth.packed_offsets(lengths, 1 if name == "Cu" else 64)
@@ -520,6 +520,12 @@ def secondary_configs(ctx, dev, names, iters) -> dict:
             del buf, out
         elif name == "S":
             res.update(slot_configs(ctx, dev, iters))
+
+    for name in names:
+        try:
+            one_config(name)
+        except Exception as e:  # a secondary config must never cost the headline line
+            res[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
         torch.cuda.empty_cache()
     return res
 
@@ -713,33 +719,49 @@ def main():
         if rank == 0:
             wl.free()
             torch.cuda.empty_cache()
-            one = Workload(args.workload, ctx, dev, 1, 0)
-            torch.cuda.synchronize()
-            solo_steps = max(1, min(args.steps, 200 if args.workload == "B" else 20))
-            el1, avg1, _ = run_timed(one, solo_steps, min(args.warmup, 3), 0, [stream], 1, None)
-            ok1, _ = one.check(None)
-            solo = {"value": round(one.total_bytes * solo_steps / el1 / 2**30, 2), "steps": solo_steps,
-                    "ms_per_step": round(el1 / solo_steps * 1e3, 4), "bitexact_vs_golden": ok1,
-                    "what": f"workload {args.workload} at N = 1 (the whole batch) on rank 0's GPU, timed after the "
-                            "N-rank region while the other ranks wait"}
-            one.free()
+            try:
+                one = Workload(args.workload, ctx, dev, 1, 0)
+                torch.cuda.synchronize()
+                solo_steps = max(1, min(args.steps, 200 if args.workload == "B" else 20))
+                el1, avg1, _ = run_timed(one, solo_steps, min(args.warmup, 3), 0, [stream], 1, None)
+                ok1, _ = one.check(None)
+                solo = {"value": round(one.total_bytes * solo_steps / el1 / 2**30, 2), "steps": solo_steps,
+                        "ms_per_step": round(el1 / solo_steps * 1e3, 4), "bitexact_vs_golden": ok1,
+                        "what": f"workload {args.workload} at N = 1 (the whole batch) on rank 0's GPU, timed after "
+                                "the N-rank region while the other ranks wait"}
+                one.free()
+            except Exception as e:  # the efficiency leg must never cost the N-rank line
+                solo = {"error": f"{type(e).__name__}: {e}"[:300]}
+                torch.cuda.empty_cache()
         dist.barrier()
     wl.free()
     torch.cuda.empty_cache()
 
     # ---- N = 1 extras (rank 0 only): secondary configs, end-to-end, CPU baseline
+    def optional(fn):  # an extra leg must never cost the headline line
+        try:
+            return fn()
+        except Exception as e:
+            torch.cuda.empty_cache()
+            return {"error": f"{type(e).__name__}: {e}"[:300]}
+
     configs = None
     cfg_names = args.configs if args.configs is not None else ("C,D,Du,S" if args.workload == "B" else "none")
     if world == 1 and cfg_names != "none":
-        configs = secondary_configs(ctx, dev, [c for c in cfg_names.split(",") if c], args.config_iters)
+        configs = optional(lambda: secondary_configs(ctx, dev, [c for c in cfg_names.split(",") if c],
+                                                     args.config_iters))
     e2e = None
     if world == 1 and not args.no_e2e and args.workload == "B":
-        e2e = end_to_end(ctx, gpu)
+        e2e = optional(lambda: end_to_end(ctx, gpu))
     cpu = None
     if world == 1 and not args.no_cpu_baseline and args.workload == "B":
-        wl_b = Workload("B", ctx, dev, 1, 0)
-        cpu = cpu_baseline(cpu_samples(dev, wl_b.bufs), args.cpu_runs)
-        wl_b.free()
+        def cpu_leg():
+            wl_b = Workload("B", ctx, dev, 1, 0)
+            samples = cpu_samples(dev, wl_b.bufs)
+            wl_b.free()
+            torch.cuda.empty_cache()
+            return cpu_baseline(samples, args.cpu_runs)
+        cpu = optional(cpu_leg)
 
     traffic = None
     # PMC-measured HBM bytes per config-B launch (tools/summarize_profile.py); other
@@ -810,7 +832,7 @@ def main():
         }
         if solo is not None:
             line["single_gpu"] = solo
-            line["efficiency"] = round(value / (world * solo["value"]), 4)
+            line["efficiency"] = round(value / (world * solo["value"]), 4) if "value" in solo else None
         line["configs"] = configs
         line["cpu_baseline"] = cpu
         line["e2e_pcie"] = e2e
