@@ -444,17 +444,20 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0):
 
 # ------------------------------------------------------------------------------ secondary configs
 def time_calls(fn, iters, warm_ms=60.0):
-    """ms per call: one HIP event pair around `iters` back-to-back calls (after >= warm_ms of
-    warm-up calls), / iters -- the headline's timing rule."""
+    """ms per call: one HIP event pair around `iters` back-to-back calls (after ~warm_ms of
+    back-to-back warm-up calls: a stop-and-go warm-up leaves short calls in the GPU's
+    power-management ramp), / iters -- the headline's timing rule."""
     import torch
     fn()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    while (time.perf_counter() - t0) * 1e3 < warm_ms:
-        for _ in range(4):
-            fn()
-        torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    fn()
+    b.record()
+    torch.cuda.synchronize()
+    for _ in range(max(2, min(4000, int(warm_ms / max(a.elapsed_time(b), 1e-3))))):
+        fn()
+    torch.cuda.synchronize()
     a.record()
     for _ in range(iters):
         fn()
@@ -558,7 +561,7 @@ def slot_configs(ctx, dev, iters) -> dict:
             ctx.crc32_slots_strided(b, stride, n, message_size=size, checksum_size=cs, metadata_size=ms_, mode=mode,
                                     status=status if mode == gpu.SLOT_VERIFY else None,
                                     error_count=errs if mode == gpu.SLOT_VERIFY else None)
-        ms = time_calls(call, 100)
+        ms = time_calls(call, 400)
         ok = None
         if mode == gpu.SLOT_VERIFY:
             torch.cuda.synchronize()
@@ -801,8 +804,8 @@ def main():
             scaling = "strong"
         value = total_bytes / elapsed / 2**30
         achieved = step_bytes / (avg_kern_ms * 1e-3) / 1e9
-        kernel = {"B": "subspace_amd::crc32_uniform4k_kernel<512, false>",
-                  "E": "subspace_amd::crc32_uniform4k_kernel<512, false>",
+        kernel = {"B": "subspace_amd::crc32_uniform4k_kernel<512, false, false>",
+                  "E": "subspace_amd::crc32_uniform4k_kernel<512, false, false>",
                   "C": "subspace_amd::crc32_ragged_kernel<512> + prep (whole call)"}[args.workload]
         line = {
             "metric": METRIC,

@@ -16,7 +16,7 @@
 
 namespace subspace_amd {
 
-template <int WG, bool SLOT>
+template <int WG, bool SLOT, bool PROBE>
 __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int, u32*,
                                        SlotArgs);
 
@@ -162,6 +162,7 @@ struct subspace_crc_ctx {
   u64 s_capacity = 0;
   u64* d_slot_counter = nullptr;  // fused slot kernel: (workgroups done << 32) | mismatches, 0 between calls
   bool fused_slots = true;        // contiguous 4 KiB slot batches take the fused uniform kernel
+  u64* probe = nullptr;           // experiment hook: per-wave timestamps (subspace_crc_testutil_probe)
 };
 
 namespace {
@@ -418,13 +419,19 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess) e = hipMemcpy(c->d_rops, rops.data(), rops.size() * 4, hipMemcpyHostToDevice);
 #define SET_LDS(WGV)                                                                                         \
   if (e == hipSuccess)                                                                                       \
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV, false>,                                  \
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV, false, false>,                                  \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_lds_bytes(WGV / 64));
   SET_LDS(256) SET_LDS(512) SET_LDS(768) SET_LDS(1024)
 #undef SET_LDS
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)uniform_slot_lds_bytes(8));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_lds_bytes(8));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_slot_lds_bytes(8));
   if (e == hipSuccess) e = hipMalloc(&c->d_slot_counter, sizeof(u64));
   if (e == hipSuccess) e = hipMemset(c->d_slot_counter, 0, sizeof(u64));
   if (e == hipSuccess)
@@ -529,8 +536,17 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     if (c->uniform_blocks > 0 && (u64)c->uniform_blocks < (u64)blocks) blocks = c->uniform_blocks;
     const auto* b = static_cast<const uint8_t*>(dev_base);
     const int ord = c->uniform_order;
+    if (c->probe != nullptr) {  // experiment hook: the timestamp-recording instantiation (512 threads)
+      SlotArgs sa{};
+      sa.probe = c->probe;
+      crc32_uniform4k_kernel<512, false, true><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), st>>>(
+          b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, sa);
+      c->zero_word = nullptr;
+      HIP_TRY(hipGetLastError());
+      return SUBSPACE_CRC_OK;
+    }
 #define LAUNCH(WGV)                                                                                           \
-  crc32_uniform4k_kernel<WGV, false><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(                             \
+  crc32_uniform4k_kernel<WGV, false, false><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(                             \
       b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, SlotArgs{})
     switch (wg) {
       case 256: LAUNCH(256); break;
@@ -648,10 +664,15 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
   if (!dev_message_sizes && message_size == 4096 && metadata_size == 0 && slot_stride % 16 == 0 &&
       ((uintptr_t)(buf + prefix_size) % 16) == 0 && c->fused_slots) {
     const int blocks = grid_for(c, (count + 1) / 2, 512 / 64);
-    SlotArgs sa{prefix_size, mode, dev_status, dev_crc_out, dev_error_count, c->d_slot_counter};
-    crc32_uniform4k_kernel<512, true><<<blocks, 512, uniform_slot_lds_bytes(8), st>>>(
-        buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, c->uniform_order,
-        nullptr, sa);
+    SlotArgs sa{prefix_size, mode, dev_status, dev_crc_out, dev_error_count, c->d_slot_counter, c->probe};
+    if (c->probe)  // experiment hook: the timestamp-recording instantiation
+      crc32_uniform4k_kernel<512, true, true><<<blocks, 512, uniform_slot_lds_bytes(8), st>>>(
+          buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, c->uniform_order,
+          nullptr, sa);
+    else
+      crc32_uniform4k_kernel<512, true, false><<<blocks, 512, uniform_slot_lds_bytes(8), st>>>(
+          buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, c->uniform_order,
+          nullptr, sa);
     HIP_TRY(hipGetLastError());
     return SUBSPACE_CRC_OK;
   }
@@ -942,6 +963,22 @@ int subspace_crc_testutil_set(subspace_crc_ctx* c, const char* key, int value) {
     return SUBSPACE_CRC_OK;
   }
   return SUBSPACE_CRC_EINVAL;
+}
+
+// Experiment hook (not part of the public header): while dev_words is non-null, fixed-size 4 KiB
+// batches run the uniform kernel's PROBE instantiation (512 threads, all CUs), which writes
+// kProbeWords u64 per wave (timestamps, HW_ID, XCC_ID, tile count) to dev_words; the caller
+// sizes it for grid x 8 waves (subspace_crc_testutil_probe_waves).
+int subspace_crc_testutil_probe(subspace_crc_ctx* c, void* dev_words) {
+  if (!c) return SUBSPACE_CRC_EINVAL;
+  c->probe = static_cast<u64*>(dev_words);
+  return SUBSPACE_CRC_OK;
+}
+
+// The number of waves (records) the PROBE launch of a count-message batch has.
+uint64_t subspace_crc_testutil_probe_waves(subspace_crc_ctx* c, uint64_t count) {
+  if (!c) return 0;
+  return (u64)grid_for(c, (count + 1) / 2, 8) * 8u;
 }
 
 // Tuning hook for experiments (not part of the public header): uniform-kernel workgroup

@@ -55,7 +55,13 @@ struct SlotArgs {
   u32* crc_out;        // optional (CALCULATE): stored checksum per slot
   u32* error_count;    // optional (VERIFY): mismatches of this call
   u64* counter;        // context word: (workgroups done << 32) | mismatches so far; 0 between calls
+  u64* probe;          // PROBE instantiation only: per-wave timestamps (tools/wave_timeline.py)
 };
+// Per-wave probe record of the uniform kernel's PROBE instantiation: realtime clock (100 MHz)
+// at entry, after the LDS fill + barrier, after the tile loop, at exit, after the table and
+// tile-0 loads were issued; then XCC_ID | tile count << 32; the clock before the last slot
+// flush (slot instantiation, else 0) and when the wave's first tile had landed.
+constexpr int kProbeWords = 8;
 
 // Ragged-kernel layout: tables, the same line-shift operators, then opmul slots Z_4096 and
 // Z_{8192 * 2^k}, k = 0..20 (8 KiB .. 8 GiB). The device operator array continues with
@@ -168,6 +174,37 @@ __device__ __forceinline__ u32 step4(u32 x, u32 lc0, u32 lc1) {
   const u32 a2 = __builtin_amdgcn_perm(x, lc1, 0x0c020600u);
   const u32 a3 = __builtin_amdgcn_perm(x, lc1, 0x0c020700u);
   return lds_ld(a0) ^ lds_ld(a1 + 128) ^ lds_ld(a2) ^ lds_ld(a3 + 128);
+}
+
+// The same step with the next data word folded in: T4(x) ^ next, the four lookups and
+// `next` joined by two 3-input XORs (v_bitop3_b32 0x96) instead of four v_xor_b32.
+__device__ __forceinline__ u32 step4n(u32 x, u32 lc0, u32 lc1, u32 next) {
+  const u32 a0 = __builtin_amdgcn_perm(x, lc0, 0x0c020400u);
+  const u32 a1 = __builtin_amdgcn_perm(x, lc0, 0x0c020500u);
+  const u32 a2 = __builtin_amdgcn_perm(x, lc1, 0x0c020600u);
+  const u32 a3 = __builtin_amdgcn_perm(x, lc1, 0x0c020700u);
+  const u32 t = __builtin_amdgcn_bitop3_b32(lds_ld(a0), lds_ld(a1 + 128), lds_ld(a2), 0x96);
+  return __builtin_amdgcn_bitop3_b32(t, lds_ld(a3 + 128), next, 0x96);
+}
+
+// CRC of one 128-B line (8 x 16 B), from state `init`: 32 steps of step4n.
+__device__ __forceinline__ u32 line_crc32(const u32x4 (&d)[8], u32 init, u32 lc0, u32 lc1) {
+  u32 x = init ^ d[0][0];
+#pragma unroll
+  for (int w = 0; w < 32; w++) x = step4n(x, lc0, lc1, w < 31 ? d[(w + 1) >> 2][(w + 1) & 3] : 0u);
+  return x;
+}
+
+// Per-lane line-shift operator applied to a line CRC: 8 nibble lookups in the table laid
+// out [nibble k][value n][lane slot] (lop = this lane's slot), joined by 3-input XORs.
+__device__ __forceinline__ u32 lane_shift(u32 lop, u32 crc) {
+  u32 t[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) t[j] = lds_ld(lop + 2048u * j + (((crc >> (4 * j)) & 15u) << 7));
+  const u32 a = __builtin_amdgcn_bitop3_b32(t[0], t[1], t[2], 0x96);
+  const u32 b = __builtin_amdgcn_bitop3_b32(a, t[3], t[4], 0x96);
+  const u32 c = __builtin_amdgcn_bitop3_b32(b, t[5], t[6], 0x96);
+  return c ^ t[7];
 }
 
 // Apply GF(2) operator `slot` to v: 8 conflict-free nibble lookups.

@@ -66,14 +66,8 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
 
   u32 H0 = 0, H1 = 0, AF = 0;  // parked half values and pieces-after | first-piece flag
   auto process = [&](const u32x4 (&d)[8], u32 j, u32 k) {
-    u32 crc = (j == 0 && lane == 0) ? init : 0u;
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-      for (int q = 0; q < 4; q++) crc = step4(crc ^ d[i][q], lc0, lc1);
-    u32 v = 0;
-#pragma unroll
-    for (int q = 0; q < 8; q++) v ^= lds_ld(lop + 2048u * q + (((crc >> (4 * q)) & 15u) << 7));
+    const u32 crc = line_crc32(d, (j == 0 && lane == 0) ? init : 0u, lc0, lc1);
+    u32 v = lane_shift(lop, crc);
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4

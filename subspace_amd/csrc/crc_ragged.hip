@@ -238,17 +238,11 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
       const u32 lo = (head && lane == 0) ? mis : 0u;
       keep_bytes(d, lo, hi);
     }
-    u32 crc = (first && lane == 0) ? seeds.v[mis] : 0u;
-#pragma unroll
-    for (int b = 0; b < 8; b++)
-#pragma unroll
-      for (int q = 0; q < 4; q++) crc = step4(crc ^ d[b][q], lc0, lc1);
+    const u32 crc = line_crc32(d, (first && lane == 0) ? seeds.v[mis] : 0u, lc0, lc1);
 
     // line l of half h -> Z_{128*(31-l)}(line): 8 conflict-free nibble lookups; then XOR
     // over each half with DPP (lane 31: lines 0..31, lane 63: lines 32..63)
-    u32 v = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) v ^= lds_ld(lop + 2048u * j + (((crc >> (4 * j)) & 15u) << 7));
+    u32 v = lane_shift(lop, crc);
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4

@@ -37,18 +37,25 @@
 //    that also counts finished workgroups; the last one writes the call's total.
 #include "crc_device.h"
 
+
 namespace subspace_amd {
 
-template <int WG, bool SLOT>
+template <int WG, bool SLOT, bool PROBE>
 __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __restrict__ base, u64 stride, u64 count,
                                                              const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                              u32 init, u32 final_xor, u32* __restrict__ out,
                                                              int order, u32* __restrict__ zero_word, SlotArgs sa) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
-  // a word the caller's next kernel accumulates into (a slot batch's mismatch count): zeroed
-  // here so the call needs no separate memset
-  if (zero_word != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0u;
+  u64 pt[4] = {0, 0, 0, 0};  // PROBE: timestamps, stored at exit (no store inside the stream)
+  if constexpr (PROBE) pt[0] = __builtin_amdgcn_s_memrealtime();
+  // Prologue: every kernel argument in one scalar round trip, then the table
+  // loads first of all (they need only gtab/gops), then tile 0's loads once its address is
+  // known; the LDS stores and the barrier follow, under tile 0's latency.
+  asm volatile("" ::"s"(base), "s"(stride), "s"(count), "s"(init), "s"(final_xor), "s"(out), "s"(order),
+               "s"(gridDim.x));
+  LdsFill<WG, kUniOpSlots> fill;  // step tables, per-lane operators, Z_4096
+  fill.load(gtab, gops);
 
   const int lane = threadIdx.x & 63;
   // wave-uniform (SGPR) wave index: keeps the tile loop a scalar loop, so hipcc's waitcnt
@@ -100,7 +107,8 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // this wave's tiles: tau = t0 + k*tstep, k < nk. 32-bit tile counters keep the loop
   // control scalar (a 64-bit compare needs VALU temporaries, which hipcc may place in a
   // buffer register still being loaded, forcing a vmcnt drain at the loop head).
-  const u32 nk = t0 < tend ? (u32)((tend - t0 + tstep - 1) / tstep) : 0u;
+  // (32-bit division: every tile count here is < 2^32, as count < 2^33 messages)
+  const u32 nk = t0 < tend ? ((u32)(tend - t0) + (u32)tstep - 1u) / (u32)tstep : 0u;
   const u32 s_init = (l == 0) ? init : 0u;
 
   // Tile k's lines. Past the wave's last tile it re-reads that tile, and the missing odd
@@ -120,19 +128,10 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   };
 
   // CRC of this lane's line of a tile (from the batch init for line 0, else from 0).
-  auto line_crc = [&](const u32x4 (&d)[8]) {
-    u32 crc = s_init;
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) crc = step4(crc ^ d[i][j], lc0, lc1);
-    return crc;
-  };
+  auto line_crc = [&](const u32x4 (&d)[8]) { return line_crc32(d, s_init, lc0, lc1); };
   // Message CRCs of tile k into ring slots 2*(k - kf) + h (kf = first tile of the window).
   auto tile_result = [&](u32 crc, u32 k, u32 kf) {
-    u32 v = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) v ^= lds_ld(lop + 2048u * j + (((crc >> (4 * j)) & 15u) << 7));
+    u32 v = lane_shift(lop, crc);
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
@@ -209,16 +208,20 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
 
   // Table loads first, then tile 0's loads, then the LDS stores: tile 0's latency hides
   // behind the fill and the barrier.
-  LdsFill<WG, kUniOpSlots> fill;  // step tables, per-lane operators, Z_4096
-  fill.load(gtab, gops);
+  u64 pt_args = 0;
+  if constexpr (PROBE) pt_args = __builtin_amdgcn_s_memrealtime();
   u32x4 A[8], B[8];
   load_tile(A, 0);
-  if constexpr (SLOT) load_prefix(0);
   fill.store(sbase);
   __syncthreads();
-  if constexpr (!SLOT) {
-    if (nk == 0) return;
-  }  // SLOT: every wave reaches the workgroup's mismatch sum at the end
+  // Wait for tile 0 right here (the loop's first drain is then a no-op). Waves without tiles
+  // run through the loop without iterations rather than returning early: the early return
+  // cost 0.5 us per config-B launch (bench.py A/B, r02af), as did the waves' late start
+  // when the table loads waited behind the kernel-argument math.
+  u64 pt_landed = 0;
+  if constexpr (PROBE) pt[1] = __builtin_amdgcn_s_memrealtime();
+  drain_before_issue();
+  if constexpr (PROBE) pt_landed = __builtin_amdgcn_s_memrealtime();
 
   // Ping-pong buffers, loop unrolled by two (no early exit: a break between the halves
   // would give the loop head a predecessor with fewer loads in flight, and hipcc's waitcnt
@@ -228,12 +231,32 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // profiles/r01/ceiling.md), and tile k+1's latency still hides behind tile k's compute.
   // A full ring is stored right after the next tile's loads are issued, so the stores
   // retire during that tile's compute instead of stalling the next drain (crc_long.hip).
-  // SLOT: a window's prefix lines are loaded with its first tile's loads; the window ends
-  // right after a drain, before the next tile's loads, where its span-0 terms are computed
-  // and its messages finished and stored, and the next window's prefix lines are loaded.
+  // SLOT: a window's prefix lines are loaded with its first tile's loads (window 0's with
+  // tile 1's, below); the window ends right after a drain, before the next tile's loads,
+  // where its span-0 terms are computed and its messages finished and stored, and the next
+  // window's prefix lines are loaded.
   // (Computing the span-0 terms right after the window's first drain instead -- so that only
   // the stores remain at the end -- ran 62 vs 50 us at config S in an interleaved A/B, r02l.)
   u32 k = 0, kf = 0;
+  // SLOT: window 0's prefix lines go out with tile 1's loads, not with tile 0's: 4 MiB of
+  // scattered 64-B reads in the kernel's first flood delayed every wave's tile 0 by 1.6 us
+  // (tools/wave_timeline.py --mode publish, r02ai; config S publish 49.65 -> 49.42 us, verify
+  // 48.67 -> 48.45 us, tools/session_slotab.sh r02ak). The pair is peeled so that the wait for
+  // tile 0 counts the prefix loads exactly (inside the loop, a conditional load would make
+  // hipcc's merged count wait for the next tile's loads before computing the current one).
+  if constexpr (SLOT) {
+    if (k + 2 < nk) {
+      load_tile(B, 1);
+      load_prefix(0);
+      tile_result(line_crc(A), 0, 0);
+      drain_before_issue();
+      load_tile(A, 2);
+      tile_result(line_crc(B), 1, 0);
+      k = 2;
+    } else {
+      load_prefix(0);
+    }
+  }
   // SLOT: the loop stops before the wave's last pair, which follows it: the last window's
   // span-0 terms are computed while the wave's last tile is in flight
   for (; SLOT ? k + 2 < nk : k + 1 < nk; k += 2) {
@@ -260,6 +283,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     load_tile(A, k + 2);
     tile_result(line_crc(B), k + 1, kf);
   }
+  if constexpr (PROBE) pt[2] = __builtin_amdgcn_s_memrealtime();
   bool pdone = false;  // SLOT: the current window's span-0 terms are computed
   if constexpr (SLOT) {
     if (k + 1 < nk) {  // the last pair: tile k loaded, tile k+1 the wave's last
@@ -298,8 +322,10 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     tile_result(line_crc(A), k, kf);
   }
   wave_lds_sync();
+  u64 pt_flush = 0;
   if constexpr (SLOT) {
     if (!pdone) prefix_pass();
+    if constexpr (PROBE) pt_flush = __builtin_amdgcn_s_memrealtime();
     slot_flush(kf, nk > kf ? nk - kf : 0u);
     // the call's mismatch count: one 64-bit atomic per workgroup adds (1 << 32) | its count;
     // the workgroup that sees G - 1 finished before it writes the total and resets the word
@@ -321,16 +347,29 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   } else {
     if (nk > kf) flush(kf, nk - kf);
   }
+  // a word the caller's next kernel accumulates into (a slot batch's mismatch count): zeroed
+  // here, at the end, so the call needs no separate memset
+  if (zero_word != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0u;
+  if constexpr (PROBE) {
+    pt[3] = __builtin_amdgcn_s_memrealtime();
+    u64* r = sa.probe + ((u64)blockIdx.x * wpb + (u64)wid) * kProbeWords;
+    const u64 xcc = (u64)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    const u64 v = lane == 0 ? pt[0] : lane == 1 ? pt[1] : lane == 2 ? pt[2] : lane == 3 ? pt[3]
+                : lane == 4 ? pt_args : lane == 5 ? (xcc | ((u64)nk << 32)) : lane == 6 ? pt_flush : pt_landed;
+    if (lane < 8) r[lane] = v;
+  }
 }
 
-#define INST(WGV, SL)                                                                                          \
-  template __global__ void crc32_uniform4k_kernel<WGV, SL>(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, \
-                                                           u32*, int, u32*, SlotArgs);
-INST(256, false)
-INST(512, false)
-INST(768, false)
-INST(1024, false)
-INST(512, true)
+#define INST(WGV, SL, PR)                                                                                 \
+  template __global__ void crc32_uniform4k_kernel<WGV, SL, PR>(const uint8_t*, u64, u64, const u32*, const u32*, u32, \
+                                                               u32, u32*, int, u32*, SlotArgs);
+INST(256, false, false)
+INST(512, false, false)
+INST(768, false, false)
+INST(1024, false, false)
+INST(512, true, false)
+INST(512, false, true)
+INST(512, true, true)
 #undef INST
 
 }  // namespace subspace_amd

@@ -73,8 +73,8 @@ def main():
     for r in rows:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
                      f"{float(r['MinNs']) / 1e3:.2f} | {float(r['MaxNs']) / 1e3:.2f} |")
-    # the headline kernel (not its slot variant crc32_uniform4k_kernel<512, true>)
-    timed = timed_launches(sess / "prof" / "run_kernel_trace.csv", "crc32_uniform4k_kernel<512, false>", 1000)
+    # the headline kernel (not its slot variant crc32_uniform4k_kernel<512, true, false>)
+    timed = timed_launches(sess / "prof" / "run_kernel_trace.csv", "crc32_uniform4k_kernel<512, false, false>", 1000)
     if timed:
         avg, per, n = timed
         lines += ["", f"bench.py's timed region = the last {n} dispatches of the uniform kernel (the earlier "
@@ -94,7 +94,7 @@ def main():
         w_kib = sum(ww) / len(ww) if ww else float("nan")
         rd = 2 * f_kib * 1024
         lines.append(f"| `{name[:90]}` | {len(v)} | {f_kib:.0f} | {rd:.4g} | {w_kib:.0f} |")
-        if "crc32_uniform4k_kernel<512, false>" in name:
+        if "crc32_uniform4k_kernel<512, false, false>" in name:
             traffic = {"kernel": name, "fetch_size_kib_per_launch": f_kib, "write_size_kib_per_launch": w_kib,
                        "hbm_bytes_per_launch": rd + (w_kib * 1024 if w_kib == w_kib else 0.0),
                        "hbm_read_bytes_per_launch": rd, "algorithmic_bytes_per_launch": 65536 * 4096,
@@ -103,8 +103,8 @@ def main():
     # HBM bytes per launch against the algorithmic bytes, for the launches whose size is fixed
     # in bench.py's PMC passes: config B (65,536 x 4 KiB) and config S (65,536 slots: 4 KiB
     # payload + the 64-B prefix line each)
-    algo = {"crc32_uniform4k_kernel<512, false>": ("B", 65536 * 4096),
-            "crc32_uniform4k_kernel<512, true>": ("S", 65536 * (4096 + 64))}
+    algo = {"crc32_uniform4k_kernel<512, false, false>": ("B", 65536 * 4096),
+            "crc32_uniform4k_kernel<512, true, false>": ("S", 65536 * (4096 + 64))}
     ratio_lines = []
     for name, v in fetch.items():
         for part, (cfg, nbytes) in algo.items():
