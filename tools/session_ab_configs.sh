@@ -6,7 +6,7 @@ set -u
 TAG=$1; CFG=$2; A=$3; B=$4
 OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/$TAG
 mkdir -p $OUT
-for i in 1 2; do
+for i in $(seq 1 ${PAIRS:-2}); do
   for v in A B; do
     lib=$A; [ $v = B ] && lib=$B
     SUBSPACE_CRC_PROBE_LIB=$lib timeout -k 10 200 python tools/bench_configs.py --configs $CFG > $OUT/$v$i.out 2> $OUT/$v$i.err
