@@ -8,7 +8,7 @@ mkdir -p $OUT
 for i in $(seq 1 $ROUNDS); do
   for lib in "$@"; do
     n=$(basename $lib .so)
-    SUBSPACE_CRC_PROBE_LIB=$lib timeout -k 10 200 python tools/slot_gap.py 3 > $OUT/g_${n}_$i.out 2> $OUT/g_${n}_$i.err
+    SUBSPACE_CRC_PROBE_LIB=$lib timeout -k 10 200 python tools/slot_gap.py ${SLOT_GAP_ROUNDS:-3} > $OUT/g_${n}_$i.out 2> $OUT/g_${n}_$i.err
     rc=$?; echo "g_${n}_$i rc=$rc" >> $OUT/status.txt; [ $rc -ne 0 ] && exit $rc
   done
 done
