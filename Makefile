@@ -78,8 +78,39 @@ asan-test: asan oracle
 	SUBSPACE_CRC_PROBE_LIB=$(CURDIR)/$(ASAN_LIB) SUBSPACE_CRC_ASAN_DIR=$(CURDIR)/$(ASAN_DIR) \
 	python -m pytest tests/test_host_api.py tests/test_capi.py tests/test_split_alloc.py tests/test_c_binding.py -q -m "not gpu" -p no:cacheprovider
 
+# ---- ThreadSanitizer build of the host code: the g++ host sources and capi.hip's host side
+# (-Xarch_host) instrumented, compiled and linked with ROCm's clang so one TSan runtime serves
+# all; tools/tsan_stress.cpp drives every host entry point from 8 threads at once.
+TSAN_DIR := build/tsan
+TSAN_CXX := /opt/rocm/llvm/bin/clang++
+TSAN_FLAGS := -fsanitize=thread -g -O1
+TSAN_LIB := $(TSAN_DIR)/libsubspace_crc.so
+TSAN_HOST_OBJS := $(patsubst $(CSRC)/%.cpp,$(TSAN_DIR)/%.o,$(CPP_SRCS)) $(TSAN_DIR)/capi.o
+TSAN_HIP_OBJS := $(filter-out $(OBJDIR)/capi.o,$(HIP_OBJS))
+
+$(TSAN_DIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(TSAN_DIR)
+	$(TSAN_CXX) -std=c++17 -fPIC -Wall $(TSAN_FLAGS) -c $< -o $@
+
+$(TSAN_DIR)/capi.o: $(CSRC)/capi.hip $(HDRS)
+	@mkdir -p $(TSAN_DIR)
+	$(HIPCC) $(HIPFLAGS) -g -Xarch_host -fsanitize=thread -c $< -o $@
+
+$(TSAN_LIB): $(TSAN_HOST_OBJS) $(TSAN_HIP_OBJS)
+	$(TSAN_CXX) -shared -fPIC -fsanitize=thread -o $@ $(TSAN_HOST_OBJS) $(TSAN_HIP_OBJS) \
+	    -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+
+$(TSAN_DIR)/tsan_stress: tools/tsan_stress.cpp include/subspace_crc.h include/subspace/checksum.h $(TSAN_LIB)
+	$(TSAN_CXX) -std=c++17 -Wall $(TSAN_FLAGS) -Iinclude -o $@ tools/tsan_stress.cpp -L$(TSAN_DIR) -lsubspace_crc \
+	    -Wl,-rpath,'$$ORIGIN' -lpthread
+
+tsan: $(TSAN_DIR)/tsan_stress
+
+tsan-test: tsan
+	TSAN_OPTIONS=halt_on_error=1:exitcode=66 $(TSAN_DIR)/tsan_stress 8 200
+
 clean:
 	rm -rf build $(LIB) tools/config_a tools/drain_demo
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle test-cpu clean asan asan-test
+.PHONY: all oracle test-cpu clean asan asan-test tsan tsan-test
