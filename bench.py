@@ -83,6 +83,9 @@ def parse():
                     help="0 (default): one HIP event pair around the whole timed region, launch duration = "
                          "region / K (an event record between launches costs ~9 us per step on MI355X); "
                          "N > 0: also bracket every N-th launch (perturbs the timed region)")
+    ap.add_argument("--roctx-region", action="store_true",
+                    help="bracket exactly the timed region with roctxProfilerResume/Pause, so that "
+                         "`rocprofv3 --selected-regions` records only the K timed launches")
     ap.add_argument("--workload", default=None, choices=["B", "C", "E"],
                     help="default B at 1 GPU, E at N > 1. "
                          "B: 65,536 x 4 KiB per GPU per step (weak scaling); "
@@ -398,7 +401,26 @@ class Workload:
         self.bufs, self.outs = [], []
 
 
-def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0):
+class RoctxRegion:
+    """roctxProfilerResume/Pause (librocprofiler-sdk-roctx) around the timed region, for
+    `rocprofv3 --selected-regions`; a no-op unless --roctx-region."""
+
+    def __init__(self, on: bool):
+        self.lib = None
+        if on:
+            import ctypes
+            self.lib = ctypes.CDLL("/opt/rocm/lib/librocprofiler-sdk-roctx.so")
+
+    def resume(self):
+        if self.lib:
+            self.lib.roctxProfilerResume(0)
+
+    def pause(self):
+        if self.lib:
+            self.lib.roctxProfilerPause(0)
+
+
+def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, region_marks=None):
     """W untimed warm-up steps (after settle launches), then EXACTLY `steps` steps between
     barrier + synchronize on both sides. Returns (max-over-ranks seconds, HIP-event span of
     the region / steps in ms, sampled per-launch ms or None)."""
@@ -415,6 +437,8 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if region_marks:
+        region_marks.resume()
     t0 = time.perf_counter()
     region[0].record(stream)
     for s2 in streams[1:]:
@@ -433,6 +457,8 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if region_marks:
+        region_marks.pause()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=stream.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -710,7 +736,7 @@ def main():
         s2.wait_stream(stream)
     settle = max(0, args.settle - args.warmup)
     elapsed, avg_kern_ms, sampled_ms = run_timed(wl, args.steps, args.warmup, args.settle, streams, world, dist,
-                                                 args.event_every)
+                                                 args.event_every, RoctxRegion(args.roctx_region and rank == 0))
     bitexact, gather_ms = wl.check(dist)
     step_bytes, total_step_bytes, nmsg = wl.step_bytes, wl.total_bytes, wl.nmsg
     bounds = getattr(wl, "bounds", None)

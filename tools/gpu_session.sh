@@ -2,7 +2,7 @@
 # One GPU-box session: parity tests, smoke, bench, rocprofv3 summaries.
 # Each GPU step has its own time limit; the script stops at the first fault,
 # abort, segfault or timeout (exit status >= 124 or > 128) and never retries.
-#   usage: bash tools/gpu_session.sh [tag] [steps...]   steps: test smoke bench prof pmc
+#   usage: bash tools/gpu_session.sh [tag] [steps...]   steps: test smoke bench prof profsel pmc configs
 set -u
 TAG=${1:-r01}
 shift || true
@@ -40,6 +40,11 @@ for s in $STEPS; do
         --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline \
         --no-e2e > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err")
       stop_if_fault $? prof ;;
+    profsel)  # the timed region only: roctxProfilerResume/Pause around it (--marker-trace routes them to the tool)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --marker-trace --selected-regions -d "$GRAFT_REPO_ROOT/$OUT/profsel" -o run \
+        --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --no-e2e --configs none \
+        --roctx-region > "$GRAFT_REPO_ROOT/$OUT/profsel_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/profsel.err")
+      stop_if_fault $? profsel ;;
     pmc)
       for ctr in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $ctr -d "$GRAFT_REPO_ROOT/$OUT/pmc_$ctr" -o run \
