@@ -61,24 +61,32 @@ def main():
     sess, tag = Path(sys.argv[1]), sys.argv[2]
     out = ROOT / "profiles" / tag
     out.mkdir(parents=True, exist_ok=True)
-    stats = sess / "prof" / "run_kernel_stats.csv"
+    # profsel: rocprofv3 --selected-regions around bench.py --roctx-region (exactly the K timed
+    # launches); prof: the whole run (settle and warm-up launches included)
+    pdir = next((sess / d for d in ("profsel", "prof") if (sess / d / "run_kernel_stats.csv").exists()), sess / "prof")
+    stats = pdir / "run_kernel_stats.csv"
     rows = list(csv.DictReader(open(stats))) if stats.exists() else []
     if stats.exists():
         shutil.copy(stats, out / "kernel_stats.csv")
     fetch = per_dispatch(sess / "pmc_FETCH_SIZE", "FETCH_SIZE")
     write = per_dispatch(sess / "pmc_WRITE_SIZE", "WRITE_SIZE")
     lines = [f"# rocprofv3 summary ({tag})", "",
-             f"Source: `{sess}` (rocprofv3 --kernel-trace --stats; PMC FETCH_SIZE and WRITE_SIZE in separate passes).",
+             f"Source: `{sess}` (rocprofv3 --kernel-trace --stats"
+             + (" --selected-regions: only bench.py's timed region, bracketed by roctxProfilerResume/Pause"
+                if pdir.name == "profsel" else "") + "; PMC FETCH_SIZE and WRITE_SIZE in separate passes).",
              "", "| kernel | calls | avg us | min us | max us |", "|---|---|---|---|---|"]
     for r in rows:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
                      f"{float(r['MinNs']) / 1e3:.2f} | {float(r['MaxNs']) / 1e3:.2f} |")
     # the headline kernel (not its slot variant crc32_uniform4k_kernel<512, true, false>)
-    timed = timed_launches(sess / "prof" / "run_kernel_trace.csv", "crc32_uniform4k_kernel<512, false, false>", 1000)
+    timed = timed_launches(pdir / "run_kernel_trace.csv", "crc32_uniform4k_kernel<512, false, false>", 1000)
     if timed:
         avg, per, n = timed
-        lines += ["", f"bench.py's timed region = the last {n} dispatches of the uniform kernel (the earlier "
-                  "ones are the settle and warm-up launches, which include the power-management ramp): "
+        where = (f"bench.py's timed region = the {n} dispatches recorded (rocprofv3 --selected-regions)"
+                 if pdir.name == "profsel" else
+                 f"bench.py's timed region = the last {n} dispatches of the uniform kernel (the earlier "
+                 "ones are the settle and warm-up launches, which include the power-management ramp)")
+        lines += ["", where + ": "
                   f"average kernel duration {avg:.2f} us, dispatch-to-dispatch interval {per:.2f} us "
                   f"(= {65536 * 4096 / per / 1e3:.0f} GB/s of payload; bench.py's roofline.achieved uses the "
                   "HIP-event span of the same region / K)."]
