@@ -230,7 +230,7 @@ def cpu_baseline(samples: dict, runs: int) -> dict:
             orc.crc32c_sse42_batch(arena_b, offs_b, lens_b, threads=threads)
             ts.append(time.perf_counter() - t)
         sse = round(BATCH_BYTES / float(np.median(ts)) / 2**30, 3)
-    # informational: the library's own host SubspaceCRC32 (PCLMULQDQ body) on one core, over
+    # informational: the library's own host SubspaceCRC32 (carry-less folding body) on one core, over
     # the whole 256 MiB batch (per-message calls would time Python's call overhead instead)
     from subspace_amd import checksum
     ts = []
@@ -259,7 +259,8 @@ def cpu_baseline(samples: dict, runs: int) -> dict:
             "sse42_crc32c_note": "client/checksum.cc:56-76 (-msse4.2 builds) restated on config B's sample and "
                                  "the same threads: CRC-32C, NOT bit-exact with the IEEE parity path; informational",
             "dropin_host_1core_value": dropin,
-            "dropin_host_note": "libsubspace_crc.so's host SubspaceCRC32 (bit-exact IEEE; PCLMULQDQ folding) on one "
+            "dropin_host_note": "libsubspace_crc.so's host SubspaceCRC32 (bit-exact IEEE; 4 x 512-bit VPCLMULQDQ "
+                                "folding where the CPU has AVX-512 VPCLMULQDQ, else 4 x 128-bit PCLMULQDQ) on one "
                                 "core over config B's sample; informational",
             "config_a": config_a,
             "sample": f"bounded samples of configs B, C, D, E (~256 MiB each, host copies of device-generated "

@@ -13,10 +13,14 @@
 // 16-B-multiple body of an IEEE CRC of 64 bytes or more is folded with carry-less
 // multiplies (4 x 128-bit lanes, then one, then a Barrett reduction to 32 bits; the
 // published folding scheme for reflected CRCs, with the constants below derived for
-// 0xEDB88320), the remaining bytes by slice-by-16. tests/test_host_api.py checks every
-// boundary of the split against zlib.
+// 0xEDB88320), the remaining bytes by slice-by-16. Where the CPU also has AVX-512 with
+// VPCLMULQDQ (Zen 4/5 EPYC such as the MI355X hosts' 9575F, Ice Lake and later Xeons), bodies
+// of 256 bytes or more are folded 4 x 512 bits per step first. SUBSPACE_CRC_HOST_ISA=
+// vpclmul|pclmul|table caps the path (read once; tests use it to cover every path on one
+// machine). tests/test_host_api.py checks every boundary of the split against zlib.
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 
 #if defined(__x86_64__)
@@ -87,22 +91,13 @@ SUBSPACE_PCLMUL inline __m128i fold128(__m128i x, __m128i k, __m128i next) {  //
   return _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(x, k, 0x00), _mm_clmulepi64_si128(x, k, 0x11)), next);
 }
 
-SUBSPACE_PCLMUL uint32_t crc_pclmul(uint32_t crc, const uint8_t* p, size_t len) {
-  const __m128i k12 = _mm_set_epi64x(0x1c6e41596ll, 0x154442bd4ll);
+// Fold four 128-bit lanes (x1 oldest) and the remaining 16-B blocks into one, then reduce to
+// the raw 32-bit state.
+SUBSPACE_PCLMUL uint32_t finish128(__m128i x1, __m128i x2, __m128i x3, __m128i x4, const uint8_t* p, size_t len) {
   const __m128i k34 = _mm_set_epi64x(0x0ccaa009ell, 0x1751997d0ll);
   const __m128i k5 = _mm_set_epi64x(0, 0x163cd6124ll);
   const __m128i mup = _mm_set_epi64x(0x1f7011641ll, 0x1db710641ll);
   const __m128i mask32 = _mm_set_epi32(0, 0, 0, -1);
-  __m128i x1 = _mm_xor_si128(ld128(p), _mm_cvtsi32_si128((int)crc));
-  __m128i x2 = ld128(p + 16), x3 = ld128(p + 32), x4 = ld128(p + 48);
-  p += 64;
-  len -= 64;
-  for (; len >= 64; p += 64, len -= 64) {
-    x1 = fold128(x1, k12, ld128(p));
-    x2 = fold128(x2, k12, ld128(p + 16));
-    x3 = fold128(x3, k12, ld128(p + 32));
-    x4 = fold128(x4, k12, ld128(p + 48));
-  }
   x1 = fold128(x1, k34, x2);
   x1 = fold128(x1, k34, x3);
   x1 = fold128(x1, k34, x4);
@@ -115,6 +110,53 @@ SUBSPACE_PCLMUL uint32_t crc_pclmul(uint32_t crc, const uint8_t* p, size_t len) 
   __m128i t = _mm_clmulepi64_si128(_mm_and_si128(x1, mask32), mup, 0x10);
   t = _mm_clmulepi64_si128(_mm_and_si128(t, mask32), mup, 0x00);
   return (uint32_t)_mm_extract_epi32(_mm_xor_si128(x1, t), 1);
+}
+
+SUBSPACE_PCLMUL uint32_t crc_pclmul(uint32_t crc, const uint8_t* p, size_t len) {
+  const __m128i k12 = _mm_set_epi64x(0x1c6e41596ll, 0x154442bd4ll);
+  __m128i x1 = _mm_xor_si128(ld128(p), _mm_cvtsi32_si128((int)crc));
+  __m128i x2 = ld128(p + 16), x3 = ld128(p + 32), x4 = ld128(p + 48);
+  p += 64;
+  len -= 64;
+  for (; len >= 64; p += 64, len -= 64) {
+    x1 = fold128(x1, k12, ld128(p));
+    x2 = fold128(x2, k12, ld128(p + 16));
+    x3 = fold128(x3, k12, ld128(p + 32));
+    x4 = fold128(x4, k12, ld128(p + 48));
+  }
+  return finish128(x1, x2, x3, x4, p, len);
+}
+
+// The same scheme on 512-bit registers (len >= 256, len % 16 == 0): four zmm accumulators
+// fold by 2,048 bits per step (k = x^(2048+32), x^(2048-32) mod P, reflected and shifted
+// as above), then into one zmm by 512 bits (k12), 64-B blocks likewise, and its four
+// 128-bit lanes go to finish128.
+#define SUBSPACE_VPCLMUL __attribute__((target("avx512f,avx512vl,vpclmulqdq,pclmul,sse4.1")))
+SUBSPACE_VPCLMUL inline __m512i ld512(const uint8_t* q) { return _mm512_loadu_si512(q); }
+SUBSPACE_VPCLMUL inline __m512i fold512(__m512i x, __m512i k, __m512i next) {
+  return _mm512_ternarylogic_epi64(_mm512_clmulepi64_epi128(x, k, 0x00), _mm512_clmulepi64_epi128(x, k, 0x11), next,
+                                   0x96);  // a ^ b ^ c
+}
+
+SUBSPACE_VPCLMUL uint32_t crc_vpclmul(uint32_t crc, const uint8_t* p, size_t len) {
+  const __m512i k2048 = _mm512_broadcast_i32x4(_mm_set_epi64x(0x1322d1430ll, 0x11542778all));
+  const __m512i k512 = _mm512_broadcast_i32x4(_mm_set_epi64x(0x1c6e41596ll, 0x154442bd4ll));
+  __m512i z0 = _mm512_xor_si512(ld512(p), _mm512_zextsi128_si512(_mm_cvtsi32_si128((int)crc)));
+  __m512i z1 = ld512(p + 64), z2 = ld512(p + 128), z3 = ld512(p + 192);
+  p += 256;
+  len -= 256;
+  for (; len >= 256; p += 256, len -= 256) {
+    z0 = fold512(z0, k2048, ld512(p));
+    z1 = fold512(z1, k2048, ld512(p + 64));
+    z2 = fold512(z2, k2048, ld512(p + 128));
+    z3 = fold512(z3, k2048, ld512(p + 192));
+  }
+  z0 = fold512(z0, k512, z1);
+  z0 = fold512(z0, k512, z2);
+  z0 = fold512(z0, k512, z3);
+  for (; len >= 64; p += 64, len -= 64) z0 = fold512(z0, k512, ld512(p));
+  return finish128(_mm512_extracti32x4_epi32(z0, 0), _mm512_extracti32x4_epi32(z0, 1),
+                   _mm512_extracti32x4_epi32(z0, 2), _mm512_extracti32x4_epi32(z0, 3), p, len);
 }
 
 // CRC-32C with the SSE4.2 crc32 instruction (the same instruction the reference's
@@ -136,9 +178,24 @@ bool have_sse42() {
   return ok;
 }
 
-bool have_pclmul() {
-  static const bool ok = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
-  return ok;
+// The widest folding path this CPU has, capped by SUBSPACE_CRC_HOST_ISA: 2 = VPCLMULQDQ on
+// AVX-512, 1 = PCLMULQDQ, 0 = tables only.
+int host_isa() {
+  static const int isa = [] {
+    int v = 0;
+    if (__builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1")) {
+      v = 1;
+      if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") &&
+          __builtin_cpu_supports("vpclmulqdq"))
+        v = 2;
+    }
+    if (const char* e = std::getenv("SUBSPACE_CRC_HOST_ISA")) {
+      const int cap = !std::strcmp(e, "table") ? 0 : !std::strcmp(e, "pclmul") ? 1 : 2;
+      v = v < cap ? v : cap;
+    }
+    return v;
+  }();
+  return isa;
 }
 #endif
 
@@ -146,9 +203,9 @@ bool have_pclmul() {
 
 extern "C" uint32_t SubspaceCRC32(uint32_t crc, const uint8_t* data, size_t length) {
 #if defined(__x86_64__)
-  if (length >= 64 && have_pclmul()) {
+  if (length >= 64 && host_isa() > 0) {
     const size_t body = length & ~(size_t)15;
-    crc = crc_pclmul(crc, data, body);
+    crc = body >= 256 && host_isa() == 2 ? crc_vpclmul(crc, data, body) : crc_pclmul(crc, data, body);
     data += body;
     length -= body;
   }

@@ -5,6 +5,7 @@ import json
 import os
 import shutil
 import subprocess
+import sys
 from pathlib import Path
 
 import numpy as np
@@ -241,3 +242,36 @@ def test_host_crc_pclmul_boundaries(lib):
     a, b = buf[:1000], buf[1000:5000]  # chaining: body, tail, body
     st = lib.SubspaceCRC32(lib.SubspaceCRC32(0xFFFFFFFF, a, len(a)), b, len(b))
     assert st == (~zlib.crc32(a + b)) & 0xFFFFFFFF
+
+
+_ISA_CHECK = r"""
+import ctypes, sys, zlib
+import numpy as np
+lib = ctypes.CDLL(sys.argv[1])
+lib.SubspaceCRC32.restype = ctypes.c_uint32
+lib.SubspaceCRC32.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
+rng = np.random.default_rng(2048)
+buf = rng.integers(0, 256, 140000, dtype=np.uint8).tobytes()
+bad = []
+base = (64, 128, 192, 256, 320, 448, 512, 576, 1024, 4096, 65536)
+for n in sorted({n + d for n in base for d in (-17, -16, -1, 0, 1, 15, 16, 63, 64, 65, 255, 256)}):
+    for off in (0, 5):
+        s = int(rng.integers(0, 1 << 32))
+        d = buf[off:off + n]
+        if lib.SubspaceCRC32(s, d, n) != (~zlib.crc32(d, (~s) & 0xFFFFFFFF)) & 0xFFFFFFFF:
+            bad.append((n, off))
+print(len(bad), bad[:5])
+"""
+
+
+@pytest.mark.parametrize("isa", ["table", "pclmul", "vpclmul"])
+def test_host_crc_every_isa_path(lib, isa):
+    """Each folding path of SubspaceCRC32 (tables only, 4 x 128-bit PCLMULQDQ, 4 x 512-bit
+    VPCLMULQDQ for bodies >= 256 B), forced with SUBSPACE_CRC_HOST_ISA, against zlib around
+    every boundary of both folding widths (a path the CPU lacks falls back to the next one)."""
+    so = (Path(ASAN_DIR) if ASAN_DIR else ROOT / "subspace_amd") / "libsubspace_crc.so"
+    env = dict(os.environ, SUBSPACE_CRC_HOST_ISA=isa)
+    r = subprocess.run([sys.executable, "-c", _ISA_CHECK, str(so)], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split()[0] == "0", r.stdout
