@@ -159,6 +159,16 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     for (int i = 0; i < 4; i++) Q[i] = q[i];
     __builtin_amdgcn_sched_barrier(0);
   };
+  // After the drain that follows window 0's prefix loads: every loaded prefix word counts as
+  // used here. Words the checksum never reads (bytes 0-3, the checksum area's tail) would
+  // otherwise leave their registers free while the loads are in flight, and hipcc reused such
+  // a register in tile 0's compute -- which then waited for the prefix loads and for tile 1's,
+  // issued before them (config S publish 50.2 -> 49.6 us, verify 49.2 -> 48.4, r02c5). The
+  // same hint after the loop's drains ran 8.7 us slower (r02c4): only here.
+  auto prefix_landed = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; i++) asm volatile("" ::"v"(Q[i]));
+  };
   auto prefix_pass = [&]() {
     u32 w[16];
 #pragma unroll
@@ -250,6 +260,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
       load_prefix(0);
       tile_result(line_crc(A), 0, 0);
       drain_before_issue();
+      prefix_landed();
       load_tile(A, 2);
       tile_result(line_crc(B), 1, 0);
       k = 2;
