@@ -134,6 +134,10 @@ def main():
     wid = np.arange(waves) % 8
     t2 = np.stack([(r[i, :, 2] - r[i, :, 0].min()) * TICK_US for i in range(r.shape[0])])
     med["loop_end_by_wave_in_wg"] = [round(float(np.median(t2[:, wid == w])), 2) for w in range(8)]
+    # the same per wave of a workgroup for entry, tile 0's loads issued, tile 0 landed and exit
+    for name, col in (("entry", 0), ("issued", 4), ("tile0_landed", 7), ("exit", 3)):
+        tt = np.stack([(r[i, :, col].astype(np.float64) - r[i, :, 0].min()) * TICK_US for i in range(r.shape[0])])
+        med[f"{name}_by_wave_in_wg"] = [round(float(np.median(tt[:, wid == w])), 2) for w in range(8)]
     med["event_span_us_per_launch"] = round(span_ms * 1e3, 2)
     med["waves"] = waves
     med["tiles_per_wave"] = sorted(set(int(x) >> 32 for x in r[0, :, 5]))
