@@ -3,11 +3,12 @@
 // Same function, same result as the reference's default x86-64 build (IEEE 802.3
 // reflected polynomial 0xEDB88320, raw state in and out), computed 16 bytes per
 // step (slice-by-16) instead of one table lookup per byte. The batched GPU path
-// lives in crc_kernels.hip; this host function is what per-message callers
+// lives in crc_uniform.hip / crc_ragged.hip / crc_long.hip; this host function is what per-message callers
 // (publisher.cc:673, subscriber.h:274, user callbacks such as client_test.cc:5234)
 // keep calling, because a kernel launch per 4 KiB message would cost more than
 // the CRC itself. SubspaceCRC32C is the same function for the CRC-32C polynomial (the
-// SSE4.2 crc32 instruction where the CPU has it, slice-by-16 otherwise).
+// folding below with the Castagnoli constants for bodies of 256 B or more where the CPU has
+// AVX-512 VPCLMULQDQ, the SSE4.2 crc32 instruction for the rest, slice-by-16 otherwise).
 //
 // On x86-64 CPUs with PCLMULQDQ (every current server part; checked at run time) the
 // 16-B-multiple body of an IEEE CRC of 64 bytes or more is folded with carry-less
@@ -79,12 +80,22 @@ uint32_t crc_slice16(const Slice16& s, uint32_t crc, const uint8_t* data, size_t
 }
 
 #if defined(__x86_64__)
-// Raw-state IEEE CRC of len bytes (len >= 64, len % 16 == 0) by carry-less folding.
+// Raw-state CRC of len bytes (len >= 64, len % 16 == 0) by carry-less folding.
 // Folding constants, bit-reflected and shifted left by one (reflected-domain products):
-//   k1, k2 = x^(4*128+32), x^(4*128-32) mod P   (fold 4 x 128 bits by 512 bits)
-//   k3, k4 = x^(128+32),   x^(128-32)   mod P   (fold by 128 bits)
-//   k5     = x^64 mod P                          (128 -> 64 -> 32 bits)
+//   k_D    = x^(D+32), x^(D-32) mod P (low, high qword)  fold a 128-bit lane forward by D bits
+//            (D = 2048: 4 x 512-bit step; 512: 4 x 128-bit step and zmm -> zmm; 128: lane -> lane)
+//   k5     = x^64 mod P                                   (128 -> 64 -> 32 bits)
 //   mu, p  = x^64 div P and P, reflected (33 bits), for the Barrett reduction.
+// The two sets below were derived from the polynomials (tools-free: a few lines of GF(2)
+// arithmetic); the CRC-32C set equals the published one for 0x82F63B78.
+struct FoldConsts {
+  long long k2048[2], k512[2], k128[2], k5, mu, p;
+};
+constexpr FoldConsts kFoldIeee = {{0x11542778all, 0x1322d1430ll}, {0x154442bd4ll, 0x1c6e41596ll},
+                                  {0x1751997d0ll, 0x0ccaa009ell}, 0x163cd6124ll, 0x1f7011641ll, 0x1db710641ll};
+constexpr FoldConsts kFoldCastagnoli = {{0x0dcb17aa4ll, 0x0b9e02b86ll}, {0x0740eef02ll, 0x09e4addf8ll},
+                                        {0x0f20c0dfell, 0x14cd00bd6ll}, 0x0dd45aab8ll, 0x0dea713f1ll, 0x105ec76f1ll};
+
 #define SUBSPACE_PCLMUL __attribute__((target("pclmul,sse4.1")))
 SUBSPACE_PCLMUL inline __m128i ld128(const uint8_t* q) { return _mm_loadu_si128(reinterpret_cast<const __m128i*>(q)); }
 SUBSPACE_PCLMUL inline __m128i fold128(__m128i x, __m128i k, __m128i next) {  // x * k (both halves) + next
@@ -93,10 +104,11 @@ SUBSPACE_PCLMUL inline __m128i fold128(__m128i x, __m128i k, __m128i next) {  //
 
 // Fold four 128-bit lanes (x1 oldest) and the remaining 16-B blocks into one, then reduce to
 // the raw 32-bit state.
-SUBSPACE_PCLMUL uint32_t finish128(__m128i x1, __m128i x2, __m128i x3, __m128i x4, const uint8_t* p, size_t len) {
-  const __m128i k34 = _mm_set_epi64x(0x0ccaa009ell, 0x1751997d0ll);
-  const __m128i k5 = _mm_set_epi64x(0, 0x163cd6124ll);
-  const __m128i mup = _mm_set_epi64x(0x1f7011641ll, 0x1db710641ll);
+SUBSPACE_PCLMUL uint32_t finish128(const FoldConsts& c, __m128i x1, __m128i x2, __m128i x3, __m128i x4,
+                                   const uint8_t* p, size_t len) {
+  const __m128i k34 = _mm_set_epi64x(c.k128[1], c.k128[0]);
+  const __m128i k5 = _mm_set_epi64x(0, c.k5);
+  const __m128i mup = _mm_set_epi64x(c.mu, c.p);
   const __m128i mask32 = _mm_set_epi32(0, 0, 0, -1);
   x1 = fold128(x1, k34, x2);
   x1 = fold128(x1, k34, x3);
@@ -112,8 +124,8 @@ SUBSPACE_PCLMUL uint32_t finish128(__m128i x1, __m128i x2, __m128i x3, __m128i x
   return (uint32_t)_mm_extract_epi32(_mm_xor_si128(x1, t), 1);
 }
 
-SUBSPACE_PCLMUL uint32_t crc_pclmul(uint32_t crc, const uint8_t* p, size_t len) {
-  const __m128i k12 = _mm_set_epi64x(0x1c6e41596ll, 0x154442bd4ll);
+SUBSPACE_PCLMUL uint32_t crc_pclmul(const FoldConsts& c, uint32_t crc, const uint8_t* p, size_t len) {
+  const __m128i k12 = _mm_set_epi64x(c.k512[1], c.k512[0]);
   __m128i x1 = _mm_xor_si128(ld128(p), _mm_cvtsi32_si128((int)crc));
   __m128i x2 = ld128(p + 16), x3 = ld128(p + 32), x4 = ld128(p + 48);
   p += 64;
@@ -124,13 +136,12 @@ SUBSPACE_PCLMUL uint32_t crc_pclmul(uint32_t crc, const uint8_t* p, size_t len) 
     x3 = fold128(x3, k12, ld128(p + 32));
     x4 = fold128(x4, k12, ld128(p + 48));
   }
-  return finish128(x1, x2, x3, x4, p, len);
+  return finish128(c, x1, x2, x3, x4, p, len);
 }
 
 // The same scheme on 512-bit registers (len >= 256, len % 16 == 0): four zmm accumulators
-// fold by 2,048 bits per step (k = x^(2048+32), x^(2048-32) mod P, reflected and shifted
-// as above), then into one zmm by 512 bits (k12), 64-B blocks likewise, and its four
-// 128-bit lanes go to finish128.
+// fold by 2,048 bits per step, then into one zmm by 512 bits, 64-B blocks likewise, and its
+// four 128-bit lanes go to finish128.
 #define SUBSPACE_VPCLMUL __attribute__((target("avx512f,avx512vl,vpclmulqdq,pclmul,sse4.1")))
 SUBSPACE_VPCLMUL inline __m512i ld512(const uint8_t* q) { return _mm512_loadu_si512(q); }
 SUBSPACE_VPCLMUL inline __m512i fold512(__m512i x, __m512i k, __m512i next) {
@@ -138,9 +149,9 @@ SUBSPACE_VPCLMUL inline __m512i fold512(__m512i x, __m512i k, __m512i next) {
                                    0x96);  // a ^ b ^ c
 }
 
-SUBSPACE_VPCLMUL uint32_t crc_vpclmul(uint32_t crc, const uint8_t* p, size_t len) {
-  const __m512i k2048 = _mm512_broadcast_i32x4(_mm_set_epi64x(0x1322d1430ll, 0x11542778all));
-  const __m512i k512 = _mm512_broadcast_i32x4(_mm_set_epi64x(0x1c6e41596ll, 0x154442bd4ll));
+SUBSPACE_VPCLMUL uint32_t crc_vpclmul(const FoldConsts& c, uint32_t crc, const uint8_t* p, size_t len) {
+  const __m512i k2048 = _mm512_broadcast_i32x4(_mm_set_epi64x(c.k2048[1], c.k2048[0]));
+  const __m512i k512 = _mm512_broadcast_i32x4(_mm_set_epi64x(c.k512[1], c.k512[0]));
   __m512i z0 = _mm512_xor_si512(ld512(p), _mm512_zextsi128_si512(_mm_cvtsi32_si128((int)crc)));
   __m512i z1 = ld512(p + 64), z2 = ld512(p + 128), z3 = ld512(p + 192);
   p += 256;
@@ -155,7 +166,7 @@ SUBSPACE_VPCLMUL uint32_t crc_vpclmul(uint32_t crc, const uint8_t* p, size_t len
   z0 = fold512(z0, k512, z2);
   z0 = fold512(z0, k512, z3);
   for (; len >= 64; p += 64, len -= 64) z0 = fold512(z0, k512, ld512(p));
-  return finish128(_mm512_extracti32x4_epi32(z0, 0), _mm512_extracti32x4_epi32(z0, 1),
+  return finish128(c, _mm512_extracti32x4_epi32(z0, 0), _mm512_extracti32x4_epi32(z0, 1),
                    _mm512_extracti32x4_epi32(z0, 2), _mm512_extracti32x4_epi32(z0, 3), p, len);
 }
 
@@ -205,7 +216,8 @@ extern "C" uint32_t SubspaceCRC32(uint32_t crc, const uint8_t* data, size_t leng
 #if defined(__x86_64__)
   if (length >= 64 && host_isa() > 0) {
     const size_t body = length & ~(size_t)15;
-    crc = body >= 256 && host_isa() == 2 ? crc_vpclmul(crc, data, body) : crc_pclmul(crc, data, body);
+    crc = body >= 256 && host_isa() == 2 ? crc_vpclmul(kFoldIeee, crc, data, body)
+                                         : crc_pclmul(kFoldIeee, crc, data, body);
     data += body;
     length -= body;
   }
@@ -217,7 +229,15 @@ extern "C" uint32_t SubspaceCRC32(uint32_t crc, const uint8_t* data, size_t leng
 // build of the reference computes with _mm_crc32_u64/u32/u8 (client/checksum.cc:56-76).
 extern "C" uint32_t SubspaceCRC32C(uint32_t crc, const uint8_t* data, size_t length) {
 #if defined(__x86_64__)
-  if (have_sse42()) return crc32c_sse42(crc, data, length);
+  // bodies of 256 B or more by 4 x 512-bit folding where the CPU has it (one serial crc32
+  // chain is latency-bound at ~8 B per 3 cycles), the rest by the crc32 instruction
+  if (length >= 256 && host_isa() == 2) {
+    const size_t body = length & ~(size_t)15;
+    crc = crc_vpclmul(kFoldCastagnoli, crc, data, body);
+    data += body;
+    length -= body;
+  }
+  if (have_sse42() && host_isa() > 0) return crc32c_sse42(crc, data, length);
 #endif
   return crc_slice16(slice16c(), crc, data, length);
 }

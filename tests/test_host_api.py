@@ -275,3 +275,38 @@ def test_host_crc_every_isa_path(lib, isa):
                        timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.split()[0] == "0", r.stdout
+
+
+_ISA_CHECK_C = r"""
+import ctypes, sys
+import numpy as np
+lib = ctypes.CDLL(sys.argv[1])
+orc = ctypes.CDLL(sys.argv[2])
+for f in (lib.SubspaceCRC32C, orc.oracle_crc32c):
+    f.restype = ctypes.c_uint32
+    f.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
+rng = np.random.default_rng(3270)
+buf = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+bad = []
+base = (64, 256, 320, 512, 1024, 4096, 65536)
+for n in sorted({n + d for n in base for d in (-17, -16, -1, 0, 1, 15, 16, 63, 64, 65, 255)}):
+    for off in (0, 9):
+        s = int(rng.integers(0, 1 << 32))
+        d = buf[off:off + n]
+        if lib.SubspaceCRC32C(s, d, n) != orc.oracle_crc32c(s, d, n):
+            bad.append((n, off))
+print(len(bad), bad[:5])
+"""
+
+
+@pytest.mark.parametrize("isa", ["table", "pclmul", "vpclmul"])
+def test_host_crc32c_every_isa_path(lib, isa):
+    """SubspaceCRC32C's paths (slice-by-16 tables; the SSE4.2 crc32 instruction; 4 x 512-bit
+    VPCLMULQDQ folding with the Castagnoli constants for bodies >= 256 B), forced with
+    SUBSPACE_CRC_HOST_ISA, against the oracle's table CRC-32C around every boundary."""
+    so = (Path(ASAN_DIR) if ASAN_DIR else ROOT / "subspace_amd") / "libsubspace_crc.so"
+    env = dict(os.environ, SUBSPACE_CRC_HOST_ISA=isa)
+    r = subprocess.run([sys.executable, "-c", _ISA_CHECK_C, str(so), str(ROOT / "oracle" / "liboracle_crc.so")],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split()[0] == "0", r.stdout
