@@ -29,11 +29,13 @@ __device__ __forceinline__ u64 front(u32 b, u32 G, u32 wid) { return ((u64)b + (
 // SHAPE 0: lane <-> 128-B line (lane reads 8 consecutive 16-B blocks);
 // SHAPE 1: coalesced (instruction i reads 1 KiB: lane l gets block 64*i + l).
 // PF: explicit ping-pong prefetch of the next tile (as the CRC kernel does).
-template <int SHAPE, bool PF>
-__global__ __launch_bounds__(512) void readk(const u32x4* __restrict__ p, u64 ntiles, u32* __restrict__ out) {
+// WG: 512 (8 waves per CU) or 256 (4 waves per CU: with PF the same bytes in flight per CU
+// as 8 waves without, one wave per SIMD).
+template <int SHAPE, bool PF, int WG = 512>
+__global__ __launch_bounds__(WG) void readk(const u32x4* __restrict__ p, u64 ntiles, u32* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const u32 wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const u64 w = front(blockIdx.x, gridDim.x, wid), nw = (u64)gridDim.x * 8;
+  const u64 w = front(blockIdx.x, gridDim.x, wid), nw = (u64)gridDim.x * (WG / 64);
   const u32 nk = w < ntiles ? (u32)((ntiles - w + nw - 1) / nw) : 0u;
   auto addr = [&](u32 k, int i) -> const u32x4* {
     const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
@@ -70,7 +72,7 @@ __global__ __launch_bounds__(512) void readk(const u32x4* __restrict__ p, u64 nt
 #pragma unroll
       for (int i = 0; i < 8; i++) acc ^= a[i].x ^ a[i].y ^ a[i].z ^ a[i].w;
   }
-  out[blockIdx.x * 512 + threadIdx.x] = acc;
+  out[blockIdx.x * WG + threadIdx.x] = acc;
 }
 
 // lines (drain, then issue the next tile) + optional LDS fill prologue + optional dependent
@@ -162,6 +164,8 @@ int main() {
   std::vector<V> vs = {
       {"lines", [&](const u32x4* p) { readk<0, false><<<256, 512>>>(p, ntiles, out); }},
       {"lines+pf", [&](const u32x4* p) { readk<0, true><<<256, 512>>>(p, ntiles, out); }},
+      {"lines wg256", [&](const u32x4* p) { readk<0, false, 256><<<256, 256>>>(p, ntiles, out); }},
+      {"lines+pf wg256", [&](const u32x4* p) { readk<0, true, 256><<<256, 256>>>(p, ntiles, out); }},
       {"coalesced", [&](const u32x4* p) { readk<1, false><<<256, 512>>>(p, ntiles, out); }},
       {"coalesced+pf", [&](const u32x4* p) { readk<1, true><<<256, 512>>>(p, ntiles, out); }},
       {"lines + 152 KiB LDS fill", [&](const u32x4* p) { linesx<1, 0><<<256, 512, 152 * 1024>>>(p, ntiles, out); }},
