@@ -54,7 +54,7 @@ def timed_launches(trace: Path, name_part: str, k: int):
         return None
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last]
     span = int(last[-1]["End_Timestamp"]) - int(last[0]["Start_Timestamp"])
-    return sum(durs) / len(durs) / 1e3, span / len(last) / 1e3, len(last)
+    return sum(durs) / len(durs) / 1e3, span / len(last) / 1e3, len(last), sorted(d / 1e3 for d in durs)
 
 
 def main():
@@ -81,7 +81,7 @@ def main():
     # the headline kernel (not its slot variant crc32_uniform4k_kernel<512, true, false>)
     timed = timed_launches(pdir / "run_kernel_trace.csv", "crc32_uniform4k_kernel<512, false, false>", 1000)
     if timed:
-        avg, per, n = timed
+        avg, per, n, sd = timed
         where = (f"bench.py's timed region = the {n} dispatches recorded (rocprofv3 --selected-regions)"
                  if pdir.name == "profsel" else
                  f"bench.py's timed region = the last {n} dispatches of the uniform kernel (the earlier "
@@ -89,7 +89,9 @@ def main():
         lines += ["", where + ": "
                   f"average kernel duration {avg:.2f} us, dispatch-to-dispatch interval {per:.2f} us "
                   f"(= {65536 * 4096 / per / 1e3:.0f} GB/s of payload; bench.py's roofline.achieved uses the "
-                  "HIP-event span of the same region / K)."]
+                  "HIP-event span of the same region / K). Per-launch durations: median "
+                  f"{sd[len(sd) // 2]:.2f} us, best {sd[0]:.2f}, 10th percentile {sd[len(sd) // 10]:.2f}, "
+                  f"90th {sd[(9 * len(sd)) // 10]:.2f}, worst {sd[-1]:.2f}."]
     lines += ["", "| kernel | dispatches | FETCH_SIZE KiB/launch (raw) | HBM read bytes/launch (x2, gfx950) | "
               "WRITE_SIZE KiB/launch |", "|---|---|---|---|---|"]
     traffic = {}
