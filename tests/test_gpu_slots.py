@@ -366,6 +366,35 @@ def test_fused_slot_kernel_publish_and_verify(gpu_ctx, oracle, count, cs):
     assert int(err2.item()) == int((want == 1).sum())
 
 
+@pytest.mark.parametrize("slot_size,cs", [(4200, 4), (8192, 4), (8192, 20)])
+def test_fused_slot_kernel_wider_slots(gpu_ctx, oracle, slot_size, cs):
+    """4 KiB messages in slots larger than the message (stride 4,288 / 8,256 / 8,320): the
+    fused kernel reads each payload and prefix at the slot stride and never touches the
+    slot bytes past the message; publish byte-identical to the oracle, verify statuses equal
+    the oracle's after corruptions."""
+    count, ms = 5003, 0
+    sizes = np.full(count, 4096, dtype=np.uint64)
+    host, ps, stride = build_channel(count, slot_size, cs, ms, sizes, seed=slot_size + cs)
+    dev, status = publish_strided(gpu_ctx, host, stride, count, cs, ms, message_size=4096)
+    po, yo = offsets(count, stride, ps)
+    oracle.publish_slots(host, po, yo, sizes, cs, ms)
+    assert (status == 0).all()
+    got = dev.cpu().numpy()
+    bad = np.nonzero(got != host)[0]
+    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+    _corrupt(host, po, ps, cs, sizes, seed=slot_size * 7 + cs)
+    want = oracle.verify_slots(host, po, yo, sizes, cs, ms)
+    dev = torch.from_numpy(host).to(DEV)
+    st = torch.full((count,), 7, dtype=torch.int32, device=DEV)
+    err = torch.full((1,), 12345, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_slots_strided(dev, stride, count, message_size=4096, checksum_size=cs, metadata_size=ms,
+                                mode=gpu.SLOT_VERIFY, status=st, error_count=err)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy().view(np.uint32), want)
+    assert int(err.item()) == int((want == 1).sum())
+    assert np.array_equal(dev.cpu().numpy(), host)
+
+
 def test_fused_and_two_kernel_slot_paths_agree(gpu_ctx):
     """fused_slots off (payload kernel + crc32_slot_finish_kernel) and on give the same
     channel bytes and statuses."""
