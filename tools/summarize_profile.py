@@ -125,6 +125,24 @@ def main():
                 rd = 2 * sum(vv) / len(vv) * 1024
                 wr = sum(ww) / len(ww) * 1024 if ww else 0.0
                 ratio_lines.append(f"| `{part}` (config {cfg}) | {nbytes:.4g} | {rd + wr:.4g} | {(rd + wr) / nbytes:.3f} |")
+    # configs C and D (bench.py's default configs; the ragged kernel's dispatches split by size:
+    # C reads ~118 GB per call, D 17 GB) and D through the uniform API (the long-message kernel).
+    # FETCH_SIZE x 2 is the streaming-read calibration; for C's many partial last lines it
+    # may overstate the bytes a little.
+    big = {"C": (117844131581, lambda v: v * 2048 > 60e9), "D": (256 * (64 << 20), lambda v: v * 2048 <= 60e9)}
+    for name, v in fetch.items():
+        if "crc32_ragged_kernel" in name:
+            for cfg, (nbytes, sel) in big.items():
+                vv = [x for x in v if sel(x)]
+                if vv:
+                    rd = 2 * sum(vv) / len(vv) * 1024
+                    ratio_lines.append(f"| `crc32_ragged_kernel<512>` (config {cfg}, {len(vv)} calls) | {nbytes:.4g} | "
+                                       f"{rd:.4g} (read) | {rd / nbytes:.3f} |")
+        elif "crc32_long_kernel" in name and v:
+            rd = 2 * sum(v) / len(v) * 1024
+            nbytes = 256 * (64 << 20)
+            ratio_lines.append(f"| `crc32_long_kernel<512>` (config D, uniform API, {len(v)} calls) | {nbytes:.4g} | "
+                               f"{rd:.4g} (read) | {rd / nbytes:.3f} |")
     if ratio_lines:
         lines += ["", "| kernel | algorithmic bytes / launch | HBM bytes / launch (read x2 + write) | ratio |",
                   "|---|---|---|---|"] + ratio_lines
