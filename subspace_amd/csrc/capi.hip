@@ -403,6 +403,13 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   // ragged kernel: the line-shift operators, Z_4096, then Z_{8192 * 2^k} for k = 0..30
   std::copy(laneops.begin(), laneops.begin() + kLaneOpWords, rops.begin());
   nibble_tables(z_bytes(c->host_tab, 4096), &laneops[128 * kUniSlotOpZ4096]);
+  {  // Z_64, replicated 4x as [nibble k][value n][copy] (crc_device.h kUniSlotOpZ64)
+    u32 nt[128];
+    nibble_tables(z_bytes(c->host_tab, 64), nt);
+    for (int k = 0; k < 8; k++)
+      for (int n = 0; n < 16; n++)
+        for (int cp = 0; cp < 4; cp++) laneops[128 * kUniSlotOpZ64 + k * 64 + n * 4 + cp] = nt[k * 16 + n];
+  }
   nibble_tables(z_bytes(c->host_tab, 4096), &rops[kLaneOpWords]);
   for (int k = 0; k < 31; k++) nibble_tables(z_bytes(c->host_tab, 8192ull << k), &rops[kLaneOpWords + 128 * (1 + k)]);
   // the ragged final kernel's padding inverses Z_{2^b}^{-1}, b = 0..12

@@ -34,7 +34,12 @@ constexpr u32 kLdsOps = 128u * 1024u;  // operator area; opmul slot s = 512 B at
 // kUniOpSlots slots).
 constexpr int kLaneOpWords = 8 * 16 * 32;  // [nibble k][value n][lane slot s]: 16 KiB
 constexpr int kUniSlotOpZ4096 = kLaneOpWords * 4 / 512;  // opmul slot 32
-constexpr int kUniOpSlots = kUniSlotOpZ4096 + 1;
+// slots 33..36: Z_64 as a nibble table replicated 4x, [nibble k][value n][copy c], lane l
+// reading copy l & 3 (conflict-free): the join of a line's two 64-B chains (two-chain line
+// CRC of the plain uniform kernel; the slot variant loads slots 0..32 only)
+constexpr int kUniSlotOpZ64 = kUniSlotOpZ4096 + 1;
+constexpr int kUniOpSlots = kUniSlotOpZ64 + 4;
+constexpr int kUniOpSlotsOneChain = kUniSlotOpZ4096 + 1;
 constexpr u32 kUniRing = kLdsOps + kUniOpSlots * 512u;
 // results per wave ring: 256 (128 tiles), or 128 where 16 waves' rings would not fit
 constexpr int uni_ring_results(int waves) { return kUniRing + (u32)waves * 1024u <= 160u * 1024u ? 256 : 128; }
@@ -185,6 +190,29 @@ __device__ __forceinline__ u32 step4n(u32 x, u32 lc0, u32 lc1, u32 next) {
   const u32 a3 = __builtin_amdgcn_perm(x, lc1, 0x0c020700u);
   const u32 t = __builtin_amdgcn_bitop3_b32(lds_ld(a0), lds_ld(a1 + 128), lds_ld(a2), 0x96);
   return __builtin_amdgcn_bitop3_b32(t, lds_ld(a3 + 128), next, 0x96);
+}
+
+// Z_64 of v from the 4x replicated nibble table at z64 (= its base + 4 * (lane & 3)).
+__device__ __forceinline__ u32 opmul_z64(u32 z64, u32 v) {
+  u32 t[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) t[k] = lds_ld(z64 + 256u * k + (((v >> (4 * k)) & 15u) << 4));
+  const u32 a = __builtin_amdgcn_bitop3_b32(t[0], t[1], t[2], 0x96);
+  const u32 b = __builtin_amdgcn_bitop3_b32(a, t[3], t[4], 0x96);
+  const u32 c = __builtin_amdgcn_bitop3_b32(b, t[5], t[6], 0x96);
+  return c ^ t[7];
+}
+
+// The same CRC as two independent 16-step chains (bytes 0..63 from `init`, 64..127 from 0)
+// joined by linearity: crc_raw(init, A || B) = Z_64(crc_raw(init, A)) ^ crc_raw(0, B).
+__device__ __forceinline__ u32 line_crc32_2chain(const u32x4 (&d)[8], u32 init, u32 lc0, u32 lc1, u32 z64) {
+  u32 x = init ^ d[0][0], y = d[4][0];
+#pragma unroll
+  for (int w = 0; w < 16; w++) {
+    x = step4n(x, lc0, lc1, w < 15 ? d[(w + 1) >> 2][(w + 1) & 3] : 0u);
+    y = step4n(y, lc0, lc1, w < 15 ? d[(w + 17) >> 2][(w + 17) & 3] : 0u);
+  }
+  return opmul_z64(z64, x) ^ y;
 }
 
 // CRC of one 128-B line (8 x 16 B), from state `init`: 32 steps of step4n.

@@ -54,7 +54,14 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // known; the LDS stores and the barrier follow, under tile 0's latency.
   asm volatile("" ::"s"(base), "s"(stride), "s"(count), "s"(init), "s"(final_xor), "s"(out), "s"(order),
                "s"(gridDim.x));
-  LdsFill<WG, kUniOpSlots> fill;  // step tables, per-lane operators, Z_4096
+  // Two 64-B lookup chains per line, joined by Z_64 (crc_device.h line_crc32_2chain): half
+  // the dependent chain per tile for 8 more conflict-free lookups per line; config B 45.36 ->
+  // 45.10 us (r02c17, slot_gap interleaved) and 45.4-45.8 -> 45.0-45.4 us (r02c18, sweep A/B,
+  // four pairs), bit-exact. The slot variant keeps one chain: its loop does not tolerate
+  // changes.
+  constexpr bool kTwoChain = !SLOT;
+  // step tables, per-lane operators, Z_4096 (and Z_64 for the two-chain line CRC)
+  LdsFill<WG, kTwoChain ? kUniOpSlots : kUniOpSlotsOneChain> fill;
   fill.load(gtab, gops);
 
   const int lane = threadIdx.x & 63;
@@ -128,7 +135,11 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   };
 
   // CRC of this lane's line of a tile (from the batch init for line 0, else from 0).
-  auto line_crc = [&](const u32x4 (&d)[8]) { return line_crc32(d, s_init, lc0, lc1); };
+  const u32 z64 = sbase + kLdsOps + 512u * (u32)kUniSlotOpZ64 + 4u * (u32)(lane & 3);
+  auto line_crc = [&](const u32x4 (&d)[8]) {
+    if constexpr (kTwoChain) return line_crc32_2chain(d, s_init, lc0, lc1, z64);
+    else return line_crc32(d, s_init, lc0, lc1);
+  };
   // Message CRCs of tile k into ring slots 2*(k - kf) + h (kf = first tile of the window).
   auto tile_result = [&](u32 crc, u32 k, u32 kf) {
     u32 v = lane_shift(lop, crc);
