@@ -411,7 +411,12 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
         for (int cp = 0; cp < 4; cp++) laneops[128 * kUniSlotOpZ64 + k * 64 + n * 4 + cp] = nt[k * 16 + n];
   }
   nibble_tables(z_bytes(c->host_tab, 4096), &rops[kLaneOpWords]);
-  for (int k = 0; k < 31; k++) nibble_tables(z_bytes(c->host_tab, 8192ull << k), &rops[kLaneOpWords + 128 * (1 + k)]);
+  for (int k = 0; k < 31; k++)
+    nibble_tables(z_bytes(c->host_tab, 8192ull << k),
+                  &rops[k < kNumTileOps ? kLaneOpWords + 128 * (1 + k) : kRagHighOps + 128 * (k - kNumTileOps)]);
+  {  // Z_64 replicated 4x, the same table as the uniform kernel's slots 33..36
+    std::copy(laneops.begin() + 128 * kUniSlotOpZ64, laneops.begin() + 128 * (kUniSlotOpZ64 + 4), rops.begin() + kRagZ64Words);
+  }
   // the ragged final kernel's padding inverses Z_{2^b}^{-1}, b = 0..12
   for (int b = 0; b < kNumInvOps; b++)
     nibble_tables(inverse(z_bytes(c->host_tab, 1ull << b)), &rops[kRagInvOps + 128 * b]);

@@ -69,13 +69,15 @@ struct SlotArgs {
 constexpr int kProbeWords = 8;
 
 // Ragged-kernel layout: tables, the same line-shift operators, then opmul slots Z_4096 and
-// Z_{8192 * 2^k}, k = 0..20 (8 KiB .. 8 GiB). The device operator array continues with
+// Z_{8192 * 2^k}, k = 0..20 (8 KiB .. 8 GiB), and Z_64 (4 slots). The device operator array continues with
 // Z_{8192 * 2^k}, k = 21..30, read from global memory (messages of 16 GiB and more), and
 // the padding inverses Z_{2^b}^{-1}, b = 0..12, of the ragged final kernel.
 constexpr int kNumTileOps = 21;
 constexpr int kRagOpZ4096 = kLaneOpWords * 4 / 512;  // opmul slot 32
 constexpr int kRagOpZTile = kRagOpZ4096 + 1;
-constexpr int kRagLdsOpWords = kLaneOpWords + (1 + kNumTileOps) * 128;
+// then Z_64 replicated 4x (the two-chain line CRC's join, as in the uniform kernel)
+constexpr int kRagZ64Words = kLaneOpWords + (1 + kNumTileOps) * 128;
+constexpr int kRagLdsOpWords = kRagZ64Words + 512;
 constexpr int kRagHighOps = kRagLdsOpWords;  // word offset of Z_{8192 * 2^21} in the device array
 constexpr int kNumInvOps = 13;
 constexpr int kRagInvOps = kRagHighOps + (31 - kNumTileOps) * 128;  // word offset of Z_1^{-1}

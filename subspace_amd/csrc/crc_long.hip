@@ -32,6 +32,7 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
   const u32 wid = rfl(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
+  const u32 z64 = sbase + kLdsOps + 4u * (u32)kRagZ64Words + 4u * (u32)(lane & 3);  // Z_64 copy lane & 3
   const u32 lop = sbase + kLdsOps + 4u * (u32)(31 - (lane & 31));
   const u32 total = pieces * count;  // < 2^32 (checked on the host)
   const u32 w = (u32)front_slot(blockIdx.x, gridDim.x, wid);
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
 
   u32 H0 = 0, H1 = 0, AF = 0;  // parked half values and pieces-after | first-piece flag
   auto process = [&](const u32x4 (&d)[8], u32 j, u32 k) {
-    const u32 crc = line_crc32(d, (j == 0 && lane == 0) ? init : 0u, lc0, lc1);
+    const u32 crc = line_crc32_2chain(d, (j == 0 && lane == 0) ? init : 0u, lc0, lc1, z64);
     u32 v = lane_shift(lop, crc);
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2

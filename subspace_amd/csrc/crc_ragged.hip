@@ -170,6 +170,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   const u32 wid = rfl(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
+  const u32 z64 = sbase + kLdsOps + 4u * (u32)kRagZ64Words + 4u * (u32)(lane & 3);  // Z_64 copy lane & 3
   const u32 lop = sbase + kLdsOps + 4u * (u32)(31 - (lane & 31));  // this lane's line-shift operator
   const u64 total = tile_base[count];
   const u64 w = front_slot(blockIdx.x, gridDim.x, wid);  // sweep front slot (crc_device.h)
@@ -238,7 +239,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
       const u32 lo = (head && lane == 0) ? mis : 0u;
       keep_bytes(d, lo, hi);
     }
-    const u32 crc = line_crc32(d, (first && lane == 0) ? seeds.v[mis] : 0u, lc0, lc1);
+    const u32 crc = line_crc32_2chain(d, (first && lane == 0) ? seeds.v[mis] : 0u, lc0, lc1, z64);
 
     // line l of half h -> Z_{128*(31-l)}(line): 8 conflict-free nibble lookups; then XOR
     // over each half with DPP (lane 31: lines 0..31, lane 63: lines 32..63)
