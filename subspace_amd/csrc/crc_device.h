@@ -36,7 +36,7 @@ constexpr int kLaneOpWords = 8 * 16 * 32;  // [nibble k][value n][lane slot s]: 
 constexpr int kUniSlotOpZ4096 = kLaneOpWords * 4 / 512;  // opmul slot 32
 // slots 33..36: Z_64 as a nibble table replicated 4x, [nibble k][value n][copy c], lane l
 // reading copy l & 3 (conflict-free): the join of a line's two 64-B chains (two-chain line
-// CRC of the plain uniform kernel; the slot variant loads slots 0..32 only)
+// CRC)
 constexpr int kUniSlotOpZ64 = kUniSlotOpZ4096 + 1;
 constexpr int kUniOpSlots = kUniSlotOpZ64 + 4;
 constexpr int kUniOpSlotsOneChain = kUniSlotOpZ4096 + 1;

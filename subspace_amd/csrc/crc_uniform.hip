@@ -57,10 +57,9 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // Two 64-B lookup chains per line, joined by Z_64 (crc_device.h line_crc32_2chain): half
   // the dependent chain per tile for 8 more conflict-free lookups per line; config B 45.36 ->
   // 45.10 us (r02c17, slot_gap interleaved) and 45.4-45.8 -> 45.0-45.4 us (r02c18, sweep A/B,
-  // four pairs), bit-exact. The slot variant keeps one chain: its loop does not tolerate
-  // changes.
-  constexpr bool kTwoChain = !SLOT;
-  // step tables, per-lane operators, Z_4096 (and Z_64 for the two-chain line CRC)
+  // four pairs); config S publish 48.96 -> 48.70 us, verify 47.87 -> 47.62 (r02c20); bit-exact.
+  constexpr bool kTwoChain = true;  // (false: the one-chain line CRC, for A/B builds)
+  // step tables, per-lane operators, Z_4096 and Z_64 (the two-chain line CRC's join)
   LdsFill<WG, kTwoChain ? kUniOpSlots : kUniOpSlotsOneChain> fill;
   fill.load(gtab, gops);
 
