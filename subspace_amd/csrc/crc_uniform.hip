@@ -8,7 +8,8 @@
 //  * Each wave streams tiles tau = t0 + k*tstep (all waves sweep one compact front) and
 //    always has the next tile's 8 loads in flight while it computes the current one.
 //  * Per line: 32 slice-by-4 steps from 32-way replicated LDS tables (4 conflict-free
-//    ds_read_b32 + 4 v_perm + 4 v_xor per word).
+//    ds_read_b32 + 4 v_perm + 2 v_bitop3 per word), as two 16-step chains (bytes 0..63,
+//    64..127) joined by a 4x-replicated Z_64 nibble table (crc_device.h line_crc32_2chain).
 //  * Combine, per tile: lane l of half h holds line l's CRC; the message CRC is
 //      crc(msg) = XOR_l Z_{128*(31-l)}(line_l)      (crc_raw linearity)
 //    Each lane applies its own operator Z_{128*(31-l)} from nibble tables laid out
