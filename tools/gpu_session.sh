@@ -3,10 +3,11 @@
 # Each GPU step has its own time limit; the script stops at the first fault,
 # abort, segfault or timeout (exit status >= 124 or > 128) and never retries.
 #   usage: bash tools/gpu_session.sh [tag] [steps...]   steps: test smoke bench prof profsel pmc configs
+#   (profsel: rocprofv3 --selected-regions around bench.py --roctx-region = exactly the timed launches)
 set -u
 TAG=${1:-r01}
 shift || true
-STEPS=${*:-"test smoke bench prof pmc"}
+STEPS=${*:-"test smoke bench profsel pmc"}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
