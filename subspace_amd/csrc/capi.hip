@@ -400,7 +400,8 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
     for (int k = 0; k < 8; k++)
       for (int n = 0; n < 16; n++) laneops[((size_t)k * 16 + n) * 32 + sl] = nt[k * 16 + n];
   }
-  // ragged kernel: the line-shift operators, Z_4096, then Z_{8192 * 2^k} for k = 0..30
+  // ragged kernel: the line-shift operators, Z_4096, Z_{8192 * 2^k} for k = 0..20, Z_64 (x4)
+  // -- the LDS part -- then Z_{8192 * 2^k} for k = 21..30 (crc_device.h ragged layout)
   std::copy(laneops.begin(), laneops.begin() + kLaneOpWords, rops.begin());
   nibble_tables(z_bytes(c->host_tab, 4096), &laneops[128 * kUniSlotOpZ4096]);
   {  // Z_64, replicated 4x as [nibble k][value n][copy] (crc_device.h kUniSlotOpZ64)
