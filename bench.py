@@ -69,8 +69,11 @@ def parse():
     # After an idle spell the first ~300 back-to-back launches of this kernel run up to 25 %
     # slower while the GPU's power management settles (profiles/r01/sustained.md). Before
     # the W warm-up steps the bench runs untimed settle launches until SETTLE launches have
-    # run in all; reported as "settle_launches" (0 disables).
+    # run in all and at least SETTLE_S seconds have passed (a cold box -- the first GPU process
+    # after boot -- ran config B at 5,368 GiB/s with 380 settle launches and 5,549-5,583 after
+    # about a second of them, r02c25/r02c26); reported as "settle_launches" (--settle 0 disables both).
     ap.add_argument("--settle", type=int, default=400)
+    ap.add_argument("--settle-s", type=float, default=1.0)
     # --streams 2: consecutive steps alternate between two HIP streams (independent batches)
     # and overlap (45.2 vs 46.7 us per launch in profiles/r01/ceiling.md). Off by default:
     # overlapping dispatches make rocprofv3's per-dispatch duration (~2x, both kernels
@@ -421,14 +424,19 @@ class RoctxRegion:
             self.lib.roctxProfilerPause(0)
 
 
-def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, region_marks=None):
-    """W untimed warm-up steps (after settle launches), then EXACTLY `steps` steps between
-    barrier + synchronize on both sides. Returns (max-over-ranks seconds, HIP-event span of
-    the region / steps in ms, sampled per-launch ms or None)."""
+def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, region_marks=None, settle_s=0.0):
+    """W untimed warm-up steps (after settle launches: at least `settle` - W of them and at
+    least `settle_s` seconds of them), then EXACTLY `steps` steps between barrier +
+    synchronize on both sides. Returns (max-over-ranks seconds, HIP-event span of the region
+    / steps in ms, sampled per-launch ms or None, settle launches run)."""
     import torch
     stream = streams[0]
-    for i in range(max(0, settle - warmup)):
-        wl.step(i, streams)
+    n_settle, t_settle = 0, time.perf_counter()
+    while n_settle < max(0, settle - warmup) or time.perf_counter() - t_settle < settle_s:
+        for _ in range(50):  # back to back; the clock is read with a sync every 50 launches
+            wl.step(n_settle, streams)
+            n_settle += 1
+        torch.cuda.synchronize()
     for i in range(warmup):
         wl.step(i, streams)
     torch.cuda.synchronize()
@@ -466,7 +474,7 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, re
         elapsed = float(t.item())
     avg_ms = region[0].elapsed_time(region[1]) / steps
     sampled = float(np.mean([a.elapsed_time(b) for a, b in ev.values()])) if ev else None
-    return elapsed, avg_ms, sampled
+    return elapsed, avg_ms, sampled, n_settle + warmup
 
 
 # ------------------------------------------------------------------------------ secondary configs
@@ -735,9 +743,11 @@ def main():
     streams = [stream] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
     for s2 in streams[1:]:
         s2.wait_stream(stream)
-    settle = max(0, args.settle - args.warmup)
-    elapsed, avg_kern_ms, sampled_ms = run_timed(wl, args.steps, args.warmup, args.settle, streams, world, dist,
-                                                 args.event_every, RoctxRegion(args.roctx_region and rank == 0))
+    elapsed, avg_kern_ms, sampled_ms, settle = run_timed(wl, args.steps, args.warmup, args.settle, streams, world,
+                                                         dist, args.event_every,
+                                                         RoctxRegion(args.roctx_region and rank == 0),
+                                                         args.settle_s if args.settle > 0 else 0.0)
+    settle = max(0, settle - args.warmup)
     bitexact, gather_ms = wl.check(dist)
     step_bytes, total_step_bytes, nmsg = wl.step_bytes, wl.total_bytes, wl.nmsg
     bounds = getattr(wl, "bounds", None)
@@ -753,7 +763,7 @@ def main():
                 one = Workload(args.workload, ctx, dev, 1, 0)
                 torch.cuda.synchronize()
                 solo_steps = max(1, min(args.steps, 200 if args.workload == "B" else 20))
-                el1, avg1, _ = run_timed(one, solo_steps, min(args.warmup, 3), 0, [stream], 1, None)
+                el1, avg1, _, _ = run_timed(one, solo_steps, min(args.warmup, 3), 0, [stream], 1, None)
                 ok1, _ = one.check(None)
                 solo = {"value": round(one.total_bytes * solo_steps / el1 / 2**30, 2), "steps": solo_steps,
                         "ms_per_step": round(el1 / solo_steps * 1e3, 4), "bitexact_vs_golden": ok1,
