@@ -69,11 +69,12 @@ def parse():
     # After an idle spell the first ~300 back-to-back launches of this kernel run up to 25 %
     # slower while the GPU's power management settles (profiles/r01/sustained.md). Before
     # the W warm-up steps the bench runs untimed settle launches until SETTLE launches have
-    # run in all and at least SETTLE_S seconds have passed (a cold box -- the first GPU process
-    # after boot -- ran config B at 5,368 GiB/s with 380 settle launches and 5,549-5,583 after
-    # about a second of them, r02c25/r02c26); reported as "settle_launches" (--settle 0 disables both).
+    # run in all and at least SETTLE_S seconds have passed: a fresh box's first GPU process ran
+    # config B at 5,368 GiB/s after 380 settle launches (r02c25) and 5,374 after 1 s of them
+    # (r02c27), 5,583 after 0.9 s on another box (r02c26) and 5,550 after 5 s (r02c28), later
+    # processes 5,520-5,583; reported as "settle_launches" (--settle 0 disables both).
     ap.add_argument("--settle", type=int, default=400)
-    ap.add_argument("--settle-s", type=float, default=1.0)
+    ap.add_argument("--settle-s", type=float, default=5.0)
     # --streams 2: consecutive steps alternate between two HIP streams (independent batches)
     # and overlap (45.2 vs 46.7 us per launch in profiles/r01/ceiling.md). Off by default:
     # overlapping dispatches make rocprofv3's per-dispatch duration (~2x, both kernels
