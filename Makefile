@@ -13,7 +13,7 @@ CPP_SRCS := $(CSRC)/host_crc.cpp $(CSRC)/split_alloc.cpp
 HDRS := $(CSRC)/crc_device.h $(CSRC)/crc_math.h include/subspace_crc.h
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))
 
-all: $(LIB) oracle tools/config_a tools/drain_demo
+all: $(LIB) oracle tools/config_a tools/drain_demo tools/batch_gates
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -37,6 +37,11 @@ tools/config_a: tools/config_a.cpp include/subspace/checksum.h $(LIB)
 # subscriber drain / batch publish through the header-only C++ helper (a GPU test runs it)
 tools/drain_demo: tools/drain_demo.cpp include/subspace/checksum.h include/subspace/checksum_batch.h include/subspace_crc.h $(LIB)
 	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ tools/drain_demo.cpp -Lsubspace_amd -lsubspace_crc \
+	    -Wl,-rpath,'$$ORIGIN/../subspace_amd'
+
+# the ValidateChecksum / publisher gates of the C++ helper (tests/test_batch_gates.py)
+tools/batch_gates: tests/c/batch_gates.cpp include/subspace/checksum.h include/subspace/checksum_batch.h include/subspace_crc.h $(LIB)
+	g++ -O2 -std=c++17 -Wall -Wextra -Iinclude -o $@ tests/c/batch_gates.cpp -Lsubspace_amd -lsubspace_crc \
 	    -Wl,-rpath,'$$ORIGIN/../subspace_amd'
 
 test-cpu: all
@@ -67,16 +72,19 @@ $(ASAN_DIR)/config_a: tools/config_a.cpp include/subspace/checksum.h $(ASAN_LIB)
 $(ASAN_DIR)/drain_demo: tools/drain_demo.cpp include/subspace/checksum.h include/subspace/checksum_batch.h include/subspace_crc.h $(ASAN_LIB)
 	g++ -std=c++17 -Wall $(ASAN_FLAGS) -Iinclude -o $@ tools/drain_demo.cpp -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN'
 
+$(ASAN_DIR)/batch_gates: tests/c/batch_gates.cpp include/subspace/checksum.h include/subspace/checksum_batch.h include/subspace_crc.h $(ASAN_LIB)
+	g++ -std=c++17 -Wall $(ASAN_FLAGS) -Iinclude -o $@ tests/c/batch_gates.cpp -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN'
+
 $(ASAN_DIR)/c_binding: tests/c/c_binding.c include/subspace_crc.h $(ASAN_LIB)
 	gcc -std=c11 -Wall -Wextra $(ASAN_FLAGS) -Iinclude -o $@ tests/c/c_binding.c -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN'
 
-asan: $(ASAN_LIB) $(ASAN_DIR)/config_a $(ASAN_DIR)/drain_demo $(ASAN_DIR)/c_binding
+asan: $(ASAN_LIB) $(ASAN_DIR)/config_a $(ASAN_DIR)/drain_demo $(ASAN_DIR)/c_binding $(ASAN_DIR)/batch_gates
 
 asan-test: asan oracle
 	ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
 	LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $$(gcc -print-file-name=libubsan.so)" \
 	SUBSPACE_CRC_PROBE_LIB=$(CURDIR)/$(ASAN_LIB) SUBSPACE_CRC_ASAN_DIR=$(CURDIR)/$(ASAN_DIR) \
-	python -m pytest tests/test_host_api.py tests/test_capi.py tests/test_split_alloc.py tests/test_c_binding.py -q -m "not gpu" -p no:cacheprovider
+	python -m pytest tests/test_host_api.py tests/test_capi.py tests/test_split_alloc.py tests/test_c_binding.py tests/test_batch_gates.py -q -m "not gpu" -p no:cacheprovider
 
 # ---- ThreadSanitizer build of the host code: the g++ host sources and capi.hip's host side
 # (-Xarch_host) instrumented, compiled and linked with ROCm's clang so one TSan runtime serves
@@ -110,7 +118,7 @@ tsan-test: tsan
 	TSAN_OPTIONS=halt_on_error=1:exitcode=66 $(TSAN_DIR)/tsan_stress 8 200
 
 clean:
-	rm -rf build $(LIB) tools/config_a tools/drain_demo
+	rm -rf build $(LIB) tools/config_a tools/drain_demo tools/batch_gates
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle test-cpu clean asan asan-test tsan tsan-test

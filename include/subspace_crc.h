@@ -18,9 +18,10 @@
  * Conventions: plain pointers and sizes only; device pointers are HIP device memory
  * on the context's device; `stream` is a hipStream_t (NULL = default stream). Calls
  * return SUBSPACE_CRC_OK or a negative code, never throw, and set a thread-local
- * message readable with subspace_crc_last_error(). A context is used by one host
- * thread at a time (like the reference client's per-channel state); distinct
- * contexts are independent.
+ * message readable with subspace_crc_last_error(). A context serialises its own calls
+ * (a mutex on the host; a call on another stream than the previous call's first waits
+ * for that stream's work, so the context's device workspaces are never shared by two
+ * calls in flight); distinct contexts are independent.
  */
 #ifndef SUBSPACE_CRC_H_
 #define SUBSPACE_CRC_H_
@@ -38,6 +39,9 @@ extern "C" {
 #define SUBSPACE_CRC_EHIP (-2)    /* a HIP runtime call failed */
 #define SUBSPACE_CRC_ENOMEM (-3)  /* device workspace allocation failed */
 #define SUBSPACE_CRC_ENODEV (-4)  /* no usable gfx950 device */
+#define SUBSPACE_CRC_EFAULT (-5)  /* a kernel of an earlier call on the context gave up a bounded wait
+                                     (stale device state or calls racing on one context): its
+                                     results are not valid (subspace_crc_ctx_check) */
 
 /* flags */
 #define SUBSPACE_CRC_FINALIZE 0x1u /* store ~crc (the stored checksum) instead of the raw state */
@@ -70,6 +74,16 @@ int subspace_crc_ctx_create(int device, subspace_crc_ctx** out);
  * function. The kernels are table-driven; only the tables and operators differ. */
 int subspace_crc_ctx_create_poly(int device, uint32_t reflected_poly, subspace_crc_ctx** out);
 void subspace_crc_ctx_destroy(subspace_crc_ctx* ctx);
+
+/* Synchronise `stream` and report whether any kernel launched on the context since the last
+ * check gave up a bounded wait (a look-back scan predecessor or a slot ring entry that never
+ * arrived): SUBSPACE_CRC_EFAULT with the reason in subspace_crc_last_error(), and the fault
+ * is cleared (the context's scan state is reset before its next call); else SUBSPACE_CRC_OK.
+ * The synchronous calls (subspace_crc32_host_slots, subspace_crc32_host_slot_list) check
+ * it themselves. Device-side state is per context: calls on one context are serialised
+ * across streams (a call on a new stream waits for the previous stream's work), and a
+ * context is thread-safe (one call at a time). */
+int subspace_crc_ctx_check(subspace_crc_ctx* ctx, void* stream);
 
 /* Pre-size the ragged-batch workspace for up to `max_messages` messages and
  * `max_tiles` 8 KiB tiles so later subspace_crc32_batch calls never allocate

@@ -25,6 +25,7 @@ EXPORTED_SYMBOLS = (
     "subspace_crc_ctx_create",
     "subspace_crc_ctx_create_poly",
     "subspace_crc_ctx_destroy",
+    "subspace_crc_ctx_check",
     "subspace_crc_ctx_reserve",
     "subspace_crc32_batch_uniform",
     "subspace_crc32_batch",
@@ -72,6 +73,8 @@ def load() -> ctypes.CDLL:
     lib.subspace_crc_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
     lib.subspace_crc_ctx_destroy.restype = None
     lib.subspace_crc_ctx_destroy.argtypes = [vp]
+    lib.subspace_crc_ctx_check.restype = i32
+    lib.subspace_crc_ctx_check.argtypes = [vp, vp]
     lib.subspace_crc_ctx_reserve.restype = i32
     lib.subspace_crc_ctx_reserve.argtypes = [vp, u64, u64]
     lib.subspace_crc32_batch_uniform.restype = i32

@@ -22,16 +22,17 @@ __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, con
 
 struct TileDesc;
 __global__ void crc32_ragged_count_scan_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
-                                               u64*, u32*, u32*, u64);
+                                               u64*, u32*, u32*, u64, u32*);
 __global__ void tile_segment_scan_kernel(const u32*, u32, u32, u32, const u64*, u64, u32*, u32*);
-__global__ void segment_prefix_kernel(u32*, u64, u32, u32, const u64*, u64, u64*, u32*);
+__global__ void segment_prefix_kernel(u32*, u64, u32, u32, const u64*, u64, u64*, u32*, u32*);
 __global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, u64, u64, const u32*,
-                                         TileDesc*, u32*, u64*, u64, u32*);
+                                         TileDesc*, u32*, u64*, u64, u32*, const u32*);
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
-                                    const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds, u32*, u32*, u64);
+                                    const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds, u32*, u32*, u64,
+                                    const u32*);
 __global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, const u64*, u32, u64, const u32*, const u32*,
-                                          u32, u32, const u32*, const u32*, u32, u32*, u64*, u64, u32*);
+                                          u32, u32, const u32*, const u32*, u32, u32*, u64*, u64, u32*, const u32*);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, int, int, u32, const u32*,
                                          const u32*, const u32*, u32*, u32*, u32*);
 __global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*);
@@ -160,12 +161,93 @@ struct subspace_crc_ctx {
   u32* d_crc0 = nullptr;  // slot batches: payload CRCs from init 0
   u64* d_soff = nullptr;  // slot batches: payload offsets of the contiguous layout
   u64 s_capacity = 0;
-  u64* d_slot_counter = nullptr;  // fused slot kernel: (workgroups done << 32) | mismatches, 0 between calls
+  // fused slot kernel: a ring of counter words, (workgroups done << 32) | mismatches, each 0
+  // between calls (the last workgroup resets its word); consecutive calls take consecutive
+  // words, so even calls that overlap on the device never share one
+  u64* d_slot_counter = nullptr;
+  u32 slot_counter_next = 0;
   bool fused_slots = true;        // contiguous 4 KiB slot batches take the fused uniform kernel
   u64* probe = nullptr;           // experiment hook: per-wave timestamps (subspace_crc_testutil_probe)
+  u32* d_fault = nullptr;         // fault word (crc_device.h kFault*): read and cleared by subspace_crc_ctx_check
+  // One call at a time per context (a recursive mutex: the host-slot paths call the device
+  // paths), and device workspace use ordered across streams: a call that uses the context's
+  // device workspaces (ragged / long / two-kernel slot paths, the host-slot staging) on another
+  // stream than the previous such call first waits for ws_done, recorded at the end of every
+  // such call on its own stream. Calls that use no context workspace (the uniform 4 KiB kernel,
+  // the fused slot kernel) take neither step.
+  std::recursive_mutex mu;
+  int depth = 0;                  // nesting of public calls on this thread (under mu)
+  hipEvent_t ws_done = nullptr;
+  hipStream_t ws_stream = nullptr;
+  bool ws_recorded = false;       // ws_done holds the last workspace call
+  bool ws_waited = false;         // the current (outermost) call has ordered its stream
+  hipStream_t ws_call_stream = nullptr;
 };
 
 namespace {
+
+constexpr u32 kSlotCounters = 64;  // the fused slot kernel's counter ring (subspace_crc_ctx::d_slot_counter)
+
+bool capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// Scope of a public call: the context's mutex; when the outermost call ends, ws_done is
+// recorded on the stream on which the call used the context's workspaces (if it did).
+struct CallScope {
+  subspace_crc_ctx* c;
+  std::lock_guard<std::recursive_mutex> lk;
+  explicit CallScope(subspace_crc_ctx* ctx) : c(ctx), lk(ctx->mu) {
+    if (c->depth++ == 0) c->ws_waited = false;
+  }
+  ~CallScope() {
+    if (--c->depth == 0 && c->ws_waited) {
+      // (a captured call is ordered by the graph's launch stream; nothing is recorded)
+      if (!capturing(c->ws_call_stream) && hipEventRecord(c->ws_done, c->ws_call_stream) == hipSuccess) {
+        c->ws_stream = c->ws_call_stream;
+        c->ws_recorded = true;
+      }
+      c->ws_waited = false;
+    }
+  }
+  CallScope(const CallScope&) = delete;
+  CallScope& operator=(const CallScope&) = delete;
+};
+
+// Before the first kernel of a call that uses the context's device workspaces on stream st:
+// wait for the previous such call if it ran on another stream.
+int use_workspace(subspace_crc_ctx* c, hipStream_t st) {
+  if (c->ws_waited) return SUBSPACE_CRC_OK;
+  if (!c->ws_done) HIP_TRY(hipEventCreateWithFlags(&c->ws_done, hipEventDisableTiming));
+  if (c->ws_recorded && c->ws_stream != st && !capturing(st)) HIP_TRY(hipStreamWaitEvent(st, c->ws_done, 0));
+  c->ws_waited = true;
+  c->ws_call_stream = st;
+  return SUBSPACE_CRC_OK;
+}
+
+const char* fault_text(u32 f) {
+  if (f & kFaultTicket) return "a look-back scan ticket was beyond its grid (stale scan state)";
+  if (f & kFaultLookbackSpin) return "a look-back scan predecessor never published (stale scan state)";
+  if (f & kFaultSlotRing) return "the fused slot kernel's finisher never received a payload CRC";
+  if (f & kFaultSlotRoom) return "a fused slot payload wave never got ring room";
+  return "unknown fault";
+}
+
+// Read (after synchronising st) and clear the context's fault word; EFAULT if it was set. The
+// scan state and the slot counters are reset before the next call.
+int fault_status(subspace_crc_ctx* c, hipStream_t st) {
+  u32 f = 0;
+  HIP_TRY(hipMemcpyAsync(&f, c->d_fault, sizeof(u32), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (f == 0) return SUBSPACE_CRC_OK;
+  HIP_TRY(hipMemsetAsync(c->d_fault, 0, sizeof(u32), st));
+  HIP_TRY(hipMemsetAsync(c->d_slot_counter, 0, kSlotCounters * sizeof(u64), st));
+  HIP_TRY(hipStreamSynchronize(st));
+  c->scan_dirty = true;
+  return fail(SUBSPACE_CRC_EFAULT, "device fault 0x%x: %s; the results of the calls since the last check are not valid",
+              f, fault_text(f));
+}
 
 // Geometry of the wave-major tile values of the persistent ragged / long kernels: nw waves,
 // nkmax values per wave, segments of 64 tiles of one sweep row (crc_combine.hip).
@@ -250,7 +332,8 @@ int combine_tiles(subspace_crc_ctx* c, const TileGeom& g, const u64* total_ptr, 
   HIP_TRY(hipGetLastError());
   u32* tickets = reinterpret_cast<u32*>(c->d_scan_state);
   segment_prefix_kernel<<<(unsigned)ceil_div(g.nseg, kScanTile), 256, 0, st>>>(
-      c->d_segx, g.nseg, (u32)g.nw, (u32)g.nwb, total_ptr, tiles, c->d_scan_state + 1 + c->scan_a_words, tickets + 1);
+      c->d_segx, g.nseg, (u32)g.nw, (u32)g.nwb, total_ptr, tiles, c->d_scan_state + 1 + c->scan_a_words, tickets + 1,
+      c->d_fault);
   HIP_TRY(hipGetLastError());
   return SUBSPACE_CRC_OK;
 }
@@ -268,8 +351,10 @@ int grid_for(subspace_crc_ctx* c, u64 work_units, int waves_per_block) {
 // `cap` sizes the descriptor workspace; a batch with more tiles takes the search path.
 int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* offsets, u32 ostride, const u64* lengths,
                u32 lstride, u64 count, u32 init, u32 final_xor, u32* out, hipStream_t st) {
+  int rc = use_workspace(c, st);
+  if (rc) return rc;
   cap = clamp_capacity(c, cap, count);
-  int rc = ensure_ragged_ws(c, count, cap);
+  rc = ensure_ragged_ws(c, count, cap);
   if (rc) return rc;
   const TileGeom g = tile_geom(c, cap);
   const u64 n1 = count + 1;
@@ -279,13 +364,13 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   u32* tickets = reinterpret_cast<u32*>(c->d_scan_state);
   crc32_ragged_count_scan_kernel<<<(unsigned)ceil_div(n1, kCountTile), 256, 0, st>>>(
       offsets, ostride, lengths, lstride, count, init, final_xor, c->d_tbase, out, c->zero_word, c->d_scan_state + 1,
-      reinterpret_cast<u32*>(c->d_scan_state), c->d_chunk, ceil_div(cap, kDescTilesPerWave));
+      reinterpret_cast<u32*>(c->d_scan_state), c->d_chunk, ceil_div(cap, kDescTilesPerWave), c->d_fault);
   c->zero_word = nullptr;
   HIP_TRY(hipGetLastError());
   // one wave per kDescTilesPerWave tiles, four waves per block
   crc32_ragged_desc_kernel<<<(unsigned)ceil_div(cap, 4 * kDescTilesPerWave), 256, 0, st>>>(
       offsets, ostride, lengths, lstride, c->d_tbase, count, cap, c->d_chunk, reinterpret_cast<TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_scan_state + 1, ceil_div(n1, kCountTile), tickets);
+      c->d_overflow, c->d_scan_state + 1, ceil_div(n1, kCountTile), tickets, c->d_fault);
   HIP_TRY(hipGetLastError());
   const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU
   HeadSeeds seeds;  // Z_r^{-1}(init), r = 0..15: the seed of a message's first line, mis = r
@@ -293,7 +378,7 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   for (int r = 1; r < 16; r++) seeds.v[r] = apply(c->zinv1, seeds.v[r - 1]);
   crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, ragged_lds_bytes(), st>>>(
       base, offsets, ostride, lengths, lstride, c->d_tbase, count, reinterpret_cast<const TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_tab, c->d_rops, seeds, out, c->d_tilecrc, g.nkmax);
+      c->d_overflow, c->d_tab, c->d_rops, seeds, out, c->d_tilecrc, g.nkmax, c->d_fault);
   HIP_TRY(hipGetLastError());
   // padded message CRC = XOR of its tiles' values = difference of two entries of their
   // XOR prefix (only the batch's real tiles are combined); the final kernel undoes the last
@@ -303,7 +388,7 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   crc32_ragged_final_kernel<<<(unsigned)ceil_div(count, 256), 256, 0, st>>>(
       c->d_tbase, offsets, ostride, lengths, lstride, count, c->d_local, c->d_segx, (u32)g.nw, (u32)g.nwb,
       c->d_overflow, c->d_rops, final_xor, out, c->d_scan_state + 1 + c->scan_a_words, ceil_div(g.nseg, kScanTile),
-      tickets + 1);
+      tickets + 1, c->d_fault);
   HIP_TRY(hipGetLastError());
   c->scan_dirty = false;
   return SUBSPACE_CRC_OK;
@@ -445,8 +530,11 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_slot_lds_bytes(8));
-  if (e == hipSuccess) e = hipMalloc(&c->d_slot_counter, sizeof(u64));
-  if (e == hipSuccess) e = hipMemset(c->d_slot_counter, 0, sizeof(u64));
+  if (e == hipSuccess) e = hipMalloc(&c->d_slot_counter, kSlotCounters * sizeof(u64));
+  if (e == hipSuccess) e = hipMemset(c->d_slot_counter, 0, kSlotCounters * sizeof(u64));
+  if (e == hipSuccess) e = hipMalloc(&c->d_fault, 4 * sizeof(u32));
+  if (e == hipSuccess) e = hipMemset(c->d_fault, 0, 4 * sizeof(u32));
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ws_done, hipEventDisableTiming);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_ragged_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)ragged_lds_bytes());
@@ -463,6 +551,7 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
 
 void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   if (!c) return;
+  if (c->ws_done && c->ws_recorded) (void)hipEventSynchronize(c->ws_done);
   if (c->hcompute) (void)hipStreamSynchronize(c->hcompute);
   for (auto& h : c->hstage) {
     if (h.stream) (void)hipStreamSynchronize(h.stream);
@@ -498,12 +587,26 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_uoff);
   (void)hipFree(c->d_ulen);
   (void)hipFree(c->d_slot_counter);
+  (void)hipFree(c->d_fault);
+  if (c->ws_done) (void)hipEventDestroy(c->ws_done);
   delete c;
+}
+
+int subspace_crc_ctx_check(subspace_crc_ctx* c, void* stream) {
+  g_err[0] = 0;
+  if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  CallScope scope(c);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  // the last workspace call may have run on another stream
+  if (c->ws_recorded) HIP_TRY(hipEventSynchronize(c->ws_done));
+  return fault_status(c, st);
 }
 
 int subspace_crc_ctx_reserve(subspace_crc_ctx* c, uint64_t max_messages, uint64_t max_tiles) {
   g_err[0] = 0;
   if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  CallScope scope(c);
   HIP_TRY(hipSetDevice(c->device));
   return ensure_ragged_ws(c, max_messages, clamp_capacity(c, max_tiles, max_messages));
 }
@@ -514,6 +617,7 @@ int subspace_crc32_batch(subspace_crc_ctx* c, const void* dev_base, uint64_t are
   g_err[0] = 0;
   if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
   if (count == 0) return SUBSPACE_CRC_OK;
+  CallScope scope(c);
   if (!dev_base || !dev_offsets || !dev_lengths || !dev_out)
     return fail(SUBSPACE_CRC_EINVAL, "null device pointer");
   if (flags & ~SUBSPACE_CRC_FINALIZE) return fail(SUBSPACE_CRC_EINVAL, "unknown flags 0x%x", flags);
@@ -534,6 +638,7 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
   g_err[0] = 0;
   if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
   if (count == 0) return SUBSPACE_CRC_OK;
+  CallScope scope(c);
   if (!dev_base || !dev_out) return fail(SUBSPACE_CRC_EINVAL, "null device pointer");
   if (flags & ~SUBSPACE_CRC_FINALIZE) return fail(SUBSPACE_CRC_EINVAL, "unknown flags 0x%x", flags);
   if (stride < length && count > 1) return fail(SUBSPACE_CRC_EINVAL, "stride %llu < length %llu",
@@ -580,7 +685,9 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
                          count < (1ull << 32) && pieces * count < (1ull << 32);
   if (long_fast && c->long_path) {
     const u64 tiles = pieces * count;
-    int rc = ensure_ragged_ws(c, 0, tiles);
+    int rc = use_workspace(c, st);
+    if (rc) return rc;
+    rc = ensure_ragged_ws(c, 0, tiles);
     if (rc) return rc;
     const TileGeom g = tile_geom(c, tiles);
     rc = scan_state_clean(c, st);
@@ -621,6 +728,7 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
                          uint32_t* dev_status, uint32_t* dev_error_count, void* stream) {
   g_err[0] = 0;
   if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  CallScope scope(c);
   int rc = check_slot_args(checksum_size, metadata_size, mode);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
@@ -631,6 +739,8 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
   if (!dev_slots) return fail(SUBSPACE_CRC_EINVAL, "null device pointer");
   if (count >= (1ull << 32)) return fail(SUBSPACE_CRC_EINVAL, "count %llu exceeds 2^32-1", (unsigned long long)count);
   HIP_TRY(hipSetDevice(c->device));
+  rc = use_workspace(c, st);
+  if (rc) return rc;
   rc = ensure_slot_ws(c, count);
   if (rc) return rc;
   // payload CRCs from init 0 at absolute addresses (base 0; fields 1 and 2 of each record)
@@ -676,19 +786,21 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
   // payload CRC, the span-0 term and the flag/checksum store or status in one kernel
   if (!dev_message_sizes && message_size == 4096 && metadata_size == 0 && slot_stride % 16 == 0 &&
       ((uintptr_t)(buf + prefix_size) % 16) == 0 && c->fused_slots) {
+    // 8 payload waves + the finisher wave per workgroup, tile order 0 (the finisher replays it)
     const int blocks = grid_for(c, (count + 1) / 2, 512 / 64);
-    SlotArgs sa{prefix_size, mode, dev_status, dev_crc_out, dev_error_count, c->d_slot_counter, c->probe};
+    SlotArgs sa{prefix_size, mode, dev_status, dev_crc_out, dev_error_count,
+                c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters), c->probe, c->d_fault};
     if (c->probe)  // experiment hook: the timestamp-recording instantiation
-      crc32_uniform4k_kernel<512, true, true><<<blocks, 512, uniform_slot_lds_bytes(8), st>>>(
-          buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, c->uniform_order,
-          nullptr, sa);
+      crc32_uniform4k_kernel<512, true, true><<<blocks, 512 + 64, uniform_slot_lds_bytes(8), st>>>(
+          buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, 0, nullptr, sa);
     else
-      crc32_uniform4k_kernel<512, true, false><<<blocks, 512, uniform_slot_lds_bytes(8), st>>>(
-          buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, c->uniform_order,
-          nullptr, sa);
+      crc32_uniform4k_kernel<512, true, false><<<blocks, 512 + 64, uniform_slot_lds_bytes(8), st>>>(
+          buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, 0, nullptr, sa);
     HIP_TRY(hipGetLastError());
     return SUBSPACE_CRC_OK;
   }
+  rc = use_workspace(c, st);
+  if (rc) return rc;
   rc = ensure_slot_ws(c, count);
   if (rc) return rc;
   want_zeroed(c, dev_error_count);
@@ -718,6 +830,7 @@ int subspace_crc32_slots_strided(subspace_crc_ctx* c, void* dev_buffer, uint64_t
                                  uint32_t* dev_error_count, void* stream) {
   g_err[0] = 0;
   if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  CallScope scope(c);
   return slots_strided_impl(c, dev_buffer, slot_stride, count, message_size, dev_message_sizes, checksum_size,
                             metadata_size, mode, dev_status, dev_error_count, nullptr, (hipStream_t)stream);
 }
@@ -826,6 +939,7 @@ int subspace_crc32_host_slots(subspace_crc_ctx* c, void* host_buffer, uint64_t s
                               uint32_t* host_error_count) {
   g_err[0] = 0;
   if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  CallScope scope(c);
   int rc = check_slot_args(checksum_size, metadata_size, mode);
   if (rc) return rc;
   if (host_error_count) *host_error_count = 0;
@@ -849,6 +963,8 @@ int subspace_crc32_host_slots(subspace_crc_ctx* c, void* host_buffer, uint64_t s
   // in flight let one chunk's copy overlap the previous chunk's kernels.
   const u64 chunk = std::max<u64>(1, std::min<u64>(count, (32ull << 20) / slot_stride));
   rc = ensure_host_stage(c, chunk * slot_stride, chunk);
+  if (rc) return rc;
+  rc = use_workspace(c, c->hcompute);  // the staging buffers and the slot workspaces
   if (rc) return rc;
   auto* host = static_cast<uint8_t*>(host_buffer);
   const u64 nchunks = (count + chunk - 1) / chunk;
@@ -892,6 +1008,8 @@ int subspace_crc32_host_slots(subspace_crc_ctx* c, void* host_buffer, uint64_t s
     (void)hipStreamSynchronize(c->hcompute);
     return first_rc;
   }
+  rc = fault_status(c, c->hcompute);
+  if (rc) return rc;
   if (host_error_count) *host_error_count = (u32)errors;
   return SUBSPACE_CRC_OK;
 }
@@ -905,6 +1023,7 @@ int subspace_crc32_host_slot_list(subspace_crc_ctx* c, const subspace_crc_slot* 
                                   uint32_t mode, uint32_t* host_status, uint32_t* host_error_count) {
   g_err[0] = 0;
   if (!c) return fail(SUBSPACE_CRC_EINVAL, "ctx is null");
+  CallScope scope(c);
   int rc = check_slot_args(checksum_size, metadata_size, mode);
   if (rc) return rc;
   if (host_error_count) *host_error_count = 0;
@@ -955,6 +1074,8 @@ int subspace_crc32_host_slot_list(subspace_crc_ctx* c, const subspace_crc_slot* 
   }
   HIP_TRY(hipMemcpyAsync(c->l_hstatus, dstatus, (count + 1) * sizeof(u32), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  rc = fault_status(c, st);
+  if (rc) return rc;
   if (host_status) std::memcpy(host_status, c->l_hstatus, count * sizeof(u32));
   if (host_error_count) *host_error_count = c->l_hstatus[count];
   return SUBSPACE_CRC_OK;
@@ -967,6 +1088,17 @@ int subspace_crc32_host_slot_list(subspace_crc_ctx* c, const subspace_crc_slot* 
 //                  fused slot kernel, 0 the payload kernel + crc32_slot_finish_kernel
 int subspace_crc_testutil_set(subspace_crc_ctx* c, const char* key, int value) {
   if (!c || !key) return SUBSPACE_CRC_EINVAL;
+  CallScope scope(c);
+  if (!std::strcmp(key, "stale_ticket")) {
+    // plant a stale tile-count scan ticket (the state a racing or half-finished call could
+    // leave): the next ragged call must report SUBSPACE_CRC_EFAULT through subspace_crc_ctx_check
+    int rc = ensure_ragged_ws(c, 1, 16);
+    if (rc) return rc;
+    const u32 v = (u32)value;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(c->d_scan_state, &v, sizeof(u32), hipMemcpyHostToDevice));
+    return SUBSPACE_CRC_OK;
+  }
   if (!std::strcmp(key, "long_path")) {
     c->long_path = value != 0;
     return SUBSPACE_CRC_OK;

@@ -88,19 +88,28 @@ __device__ __forceinline__ typename Op::T shfl_xor_t(typename Op::T v, int m) {
   }
 }
 
-// Workgroup ticket: the scan position of this workgroup (0, 1, ... in start order).
-__device__ __forceinline__ u64 scan_ticket(u32* ticket) {
+// Workgroup ticket: the scan position of this workgroup (0, 1, ... in start order). A ticket
+// beyond the grid means the counter was not zero at launch (stale state, or a call racing
+// another on the context's workspace): kFaultTicket is raised and the caller leaves at once
+// (its status word would lie past the scan's words), workgroup-uniformly.
+__device__ __forceinline__ u64 scan_ticket(u32* ticket, u32* fault, bool* stale) {
   __shared__ u32 s_tile;
   if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
   __syncthreads();
-  return s_tile;
+  const u64 t = s_tile;
+  *stale = t >= gridDim.x;
+  if (*stale && threadIdx.x == 0) raise_fault(fault, kFaultTicket);
+  return t;
 }
 
 // Exclusive scan of the workgroup's kScanThreads * ITEMS elements x (thread t holds elements
 // t*ITEMS .. +ITEMS-1 of tile `tile`), in place, continued from every earlier tile's
-// elements through the look-back on `status`.
+// elements through the look-back on `status`. A predecessor that never publishes (stale
+// state: it cannot happen in a correct call) ends the wait after a bound and raises
+// kFaultLookbackSpin in the context's fault word, so the call reports an error
+// (subspace_crc_ctx_check) instead of returning wrong CRCs as OK, and the GPU never hangs.
 template <class Op, int ITEMS>
-__device__ __forceinline__ void scan_tile_lookback(typename Op::T (&x)[ITEMS], u64 tile, u64* status) {
+__device__ __forceinline__ void scan_tile_lookback(typename Op::T (&x)[ITEMS], u64 tile, u64* status, u32* fault) {
   using T = typename Op::T;
   __shared__ T s_wave[kScanThreads / 64];
   __shared__ T s_prefix;
@@ -137,13 +146,16 @@ __device__ __forceinline__ void scan_tile_lookback(typename Op::T (&x)[ITEMS], u
         const i64 idx = base - lane;  // lane 0: the nearest predecessor
         u64 s = Op::pack(kFlagInclusive, Op::identity());
         if (idx >= 0) {
-          // every predecessor holds an earlier ticket and publishes; the bound only turns a
-          // broken invariant (stale state) into wrong results instead of a hung GPU
+          // every predecessor holds an earlier ticket and publishes; the bound turns a broken
+          // invariant (stale state) into a reported fault instead of a hung GPU
           u32 spins = 0;
           do {
             s = __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          } while (Op::flag(s) == 0 && ++spins < (1u << 22));
-          if (Op::flag(s) == 0) s = Op::pack(kFlagInclusive, Op::identity());
+          } while (Op::flag(s) == 0 && ++spins < kSpinBound);
+          if (Op::flag(s) == 0) {
+            raise_fault(fault, kFaultLookbackSpin);
+            s = Op::pack(kFlagInclusive, Op::identity());
+          }
         }
         const u64 incl = __ballot(Op::flag(s) == kFlagInclusive);
         const int first = incl ? __ffsll((unsigned long long)incl) - 1 : 63;
@@ -179,9 +191,12 @@ __device__ __forceinline__ u64 msg_tiles(u64 s, u64 len) { return len ? (len + (
 __global__ __launch_bounds__(kScanThreads) void crc32_ragged_count_scan_kernel(
     const u64* __restrict__ offsets, u32 ostride, const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
     u32 final_xor, u64* __restrict__ tile_base, u32* __restrict__ out, u32* __restrict__ zero_word,
-    u64* __restrict__ status, u32* __restrict__ ticket, u32* __restrict__ chunk_msg, u64 nchunks) {
+    u64* __restrict__ status, u32* __restrict__ ticket, u32* __restrict__ chunk_msg, u64 nchunks,
+    u32* __restrict__ fault) {
   __shared__ u64 sx[kCountTile];  // striped (coalesced) global order <-> per-thread runs
-  const u64 tile = scan_ticket(ticket);
+  bool stale;
+  const u64 tile = scan_ticket(ticket, fault, &stale);
+  if (stale) return;
   const u64 base = tile * kCountTile;
   const int tid = threadIdx.x;
 #pragma unroll
@@ -200,7 +215,7 @@ __global__ __launch_bounds__(kScanThreads) void crc32_ragged_count_scan_kernel(
   u64 x[kCountItems], nt[kCountItems];
 #pragma unroll
   for (int j = 0; j < kCountItems; j++) x[j] = nt[j] = sx[tid * kCountItems + j];
-  scan_tile_lookback<SumOp, kCountItems>(x, tile, status);  // synchronises before returning
+  scan_tile_lookback<SumOp, kCountItems>(x, tile, status, fault);  // synchronises before returning
 #pragma unroll
   for (int j = 0; j < kCountItems; j++) {
     sx[tid * kCountItems + j] = x[j];
@@ -273,8 +288,10 @@ __global__ __launch_bounds__(256) void tile_segment_scan_kernel(const u32* __res
 __global__ __launch_bounds__(kScanThreads) void segment_prefix_kernel(u32* __restrict__ segx, u64 nseg, u32 nw,
                                                                       u32 nwb, const u64* __restrict__ total_ptr,
                                                                       u64 n_cap, u64* __restrict__ status,
-                                                                      u32* __restrict__ ticket) {
-  const u64 tile = scan_ticket(ticket);
+                                                                      u32* __restrict__ ticket, u32* __restrict__ fault) {
+  bool stale;
+  const u64 tile = scan_ticket(ticket, fault, &stale);
+  if (stale) return;
   const u64 n = tiles_present(total_ptr, n_cap);
   if (n == 0) return;
   const u64 last = n - 1, need = (last / nw) * nwb + (last % nw) / 64u + 1;  // segments up to the last tile
@@ -284,7 +301,7 @@ __global__ __launch_bounds__(kScanThreads) void segment_prefix_kernel(u32* __res
   u32 x[kScanItems];
 #pragma unroll
   for (int j = 0; j < kScanItems; j++) x[j] = i0 + j < lim ? segx[i0 + j] : 0u;
-  scan_tile_lookback<XorOp, kScanItems>(x, tile, status);
+  scan_tile_lookback<XorOp, kScanItems>(x, tile, status, fault);
 #pragma unroll
   for (int j = 0; j < kScanItems; j++)
     if (i0 + j < lim) segx[i0 + j] = x[j];

@@ -46,10 +46,16 @@ constexpr int uni_ring_results(int waves) { return kUniRing + (u32)waves * 1024u
 constexpr size_t uniform_lds_bytes(int waves) { return kUniRing + (size_t)waves * 4u * uni_ring_results(waves); }
 static_assert(uniform_lds_bytes(16) <= 160u * 1024u && uniform_lds_bytes(8) <= 160u * 1024u,
               "uniform kernel LDS exceeds 160 KiB");
-// Slot variant (crc_uniform.hip, SLOT = true): the same, with rings of one 64-message window.
+// Slot variant (crc_uniform.hip, SLOT = true): the payload waves' results go to per-wave rings
+// of kSlotRingRounds tiles (2 tagged 8-B entries per tile: CRC | tile index << 32), read by the
+// workgroup's finisher wave; then the finisher's progress word (tiles consumed).
 constexpr u32 kUniSlotRing = kUniRing;
-constexpr int kUniSlotRingResults = 64;
-constexpr size_t uniform_slot_lds_bytes(int waves) { return kUniSlotRing + (size_t)waves * 4u * kUniSlotRingResults; }
+constexpr int kSlotRingRounds = 32;
+constexpr int kSlotCheckRounds = 16;  // payload waves check the finisher's progress every 16 tiles
+constexpr u32 kSlotRingBytesPerWave = 2u * 8u * kSlotRingRounds;
+constexpr u32 uniform_slot_progress(int waves) { return kUniSlotRing + (u32)waves * kSlotRingBytesPerWave; }
+constexpr size_t uniform_slot_lds_bytes(int waves) { return uniform_slot_progress(waves) + 16u; }
+static_assert(uniform_slot_lds_bytes(8) <= 160u * 1024u, "slot kernel LDS exceeds 160 KiB");
 
 // Fused slot checksums of the uniform 4 KiB kernel: the message-slot layout of
 // subspace_crc32_slots_strided with metadata_size 0 (crc_uniform.hip, crc_slots.hip).
@@ -61,7 +67,21 @@ struct SlotArgs {
   u32* error_count;    // optional (VERIFY): mismatches of this call
   u64* counter;        // context word: (workgroups done << 32) | mismatches so far; 0 between calls
   u64* probe;          // PROBE instantiation only: per-wave timestamps (tools/wave_timeline.py)
+  u32* fault;          // context fault word (kFault* bits), read by subspace_crc_ctx_check
 };
+
+// Context fault word: set by a kernel whose bounded wait gave up (a broken invariant: stale
+// state, or a call racing another on the same context). The kernel finishes instead of hanging
+// the GPU, and the host reports the call as failed (subspace_crc_ctx_check) instead of OK.
+constexpr u32 kFaultLookbackSpin = 1u;  // a look-back scan predecessor never published
+constexpr u32 kFaultTicket = 2u;        // a look-back scan ticket beyond the grid (stale ticket)
+constexpr u32 kFaultSlotRing = 4u;      // the slot finisher waited too long for a payload CRC
+constexpr u32 kFaultSlotRoom = 8u;      // a slot payload wave waited too long for ring room
+__device__ __forceinline__ void raise_fault(u32* fault, u32 bit) {
+  if (fault) __hip_atomic_fetch_or(fault, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// spin bounds: ~2^20 polls of s_sleep(8) (~0.2 s), far beyond any real wait
+constexpr u32 kSpinBound = 1u << 20;
 // Per-wave probe record of the uniform kernel's PROBE instantiation: realtime clock (100 MHz)
 // at entry, after the LDS fill + barrier, after the tile loop, at exit, after the table and
 // tile-0 loads were issued; then XCC_ID | tile count << 32; the clock before the last slot
@@ -96,6 +116,7 @@ struct HeadSeeds {
 };
 
 typedef __attribute__((address_space(3))) u32 lds_u32_t;
+typedef __attribute__((address_space(3))) u64 lds_u64_t;
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4_t;
 
 // v_readfirstlane as an unsigned dword (the builtin returns int: widening it directly to
@@ -114,6 +135,13 @@ __device__ __forceinline__ u64 front_slot(u32 b, u32 G, u32 wid) {
 
 __device__ __forceinline__ u32 lds_ld(u32 addr) { return *reinterpret_cast<const lds_u32_t*>((uintptr_t)addr); }
 __device__ __forceinline__ void lds_st(u32 addr, u32 v) { *reinterpret_cast<lds_u32_t*>((uintptr_t)addr) = v; }
+// one ds_read_b64 / ds_write_b64 (8-B aligned: single-copy atomic, so a tagged entry is
+// never seen half-written by another wave)
+__device__ __forceinline__ u64 lds_ld64(u32 addr) { return *reinterpret_cast<const volatile lds_u64_t*>((uintptr_t)addr); }
+__device__ __forceinline__ void lds_st64(u32 addr, u64 v) { *reinterpret_cast<lds_u64_t*>((uintptr_t)addr) = v; }
+__device__ __forceinline__ u32 lds_ld_volatile(u32 addr) {
+  return *reinterpret_cast<const volatile lds_u32_t*>((uintptr_t)addr);
+}
 __device__ __forceinline__ u32x4 lds_ld4(u32 addr) { return *reinterpret_cast<const lds_u32x4_t*>((uintptr_t)addr); }
 __device__ __forceinline__ void lds_st4(u32 addr, u32x4 v) { *reinterpret_cast<lds_u32x4_t*>((uintptr_t)addr) = v; }
 

@@ -61,18 +61,36 @@ __device__ inline u64 find_msg(const u64* __restrict__ tile_base, u64 count, u64
   return lo;
 }
 
+// Tiles of message (s, L): its extended length L + (s & 15) in 8 KiB tiles (0 if L = 0).
+__device__ __forceinline__ u64 ext_tiles(u64 s, u64 len) { return len ? (len + (s & 15) + 8191) >> 13 : 0; }
+
 __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, u32 ostride, const u64* __restrict__ lengths,
                                      u32 lstride, const u64* __restrict__ tile_base, u64 m, u64 tau) {
   const u64 nt = tile_base[m + 1] - tile_base[m];
   const u64 j = tau - tile_base[m];
   const u64 s = offsets[m * ostride];
+  const u64 L = lengths[m * lstride];
   const u32 mis = (u32)(s & 15);
-  const u64 rest = lengths[m * lstride] + mis - (j << 13);  // extended bytes from the tile start on
+  const u64 rest = L + mis - (j << 13);  // extended bytes from the tile start on
   TileDesc d;
   d.tile_start = (s & ~(u64)15) + (j << 13);
   d.after = (u32)(nt - 1 - j) | (j == 0 ? kFirstTile : 0u);
   d.len = (rest < 8192 ? (u32)rest : 8192u) | (mis << 16);
+  // Defence in depth: a tile that is not one of the message's own (only possible with an
+  // inconsistent tile_base, which the fault checks below already exclude) reads nothing: an
+  // empty buffer range loads zeros without touching memory.
+  if (j >= nt || j >= ext_tiles(s, L)) {
+    d.tile_start = s & ~(u64)15;
+    d.len = mis << 16;
+  }
   return d;
+}
+
+// A look-back scan of this call gave up (kFaultTicket / kFaultLookbackSpin): tile_base is not
+// to be trusted, so the kernels that index with it do nothing (the call reports the fault).
+__device__ __forceinline__ bool scan_faulted(const u32* fault) {
+  return fault && (__hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                   (kFaultTicket | kFaultLookbackSpin)) != 0u;
 }
 
 // Per tile (up to `capacity`): its descriptor. Sets *overflow if the batch has more tiles.
@@ -91,8 +109,9 @@ __global__ __launch_bounds__(256) void crc32_ragged_desc_kernel(const u64* __res
                                                                 const u64* __restrict__ tile_base, u64 count,
                                                                 u64 capacity, const u32* __restrict__ chunk_msg,
                                                                 TileDesc* __restrict__ desc, u32* __restrict__ overflow, u64* scan_status,
-                                                                u64 scan_words, u32* scan_ticket) {
+                                                                u64 scan_words, u32* scan_ticket, const u32* fault) {
   reset_scan_state(scan_status, scan_words, scan_ticket);  // the tile-count scan is done
+  if (scan_faulted(fault)) return;
   const u64 total = tile_base[count];
   const u64 limit = total < capacity ? total : capacity;
   const int lane = threadIdx.x & 63;
@@ -337,9 +356,10 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
                                                           const u32* __restrict__ overflow,
                                                           const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                           HeadSeeds seeds, u32* __restrict__ out,
-                                                          u32* __restrict__ tilecrc, u64 nkmax) {
+                                                          u32* __restrict__ tilecrc, u64 nkmax, const u32* fault) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
+  if (scan_faulted(fault)) return;  // workgroup-uniform, before any barrier
   // Precomputed descriptors unless the batch had more tiles than the workspace holds
   // (overlapping messages); then every tile is located by binary search.
   if (*overflow == 0u)
@@ -352,7 +372,7 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
 
 template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
                                                   const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds,
-                                                  u32*, u32*, u64);
+                                                  u32*, u32*, u64, const u32*);
 
 // Per message with tiles: its padded CRC = XOR of its tiles' values = P(t1 - 1) ^ P(t0 - 1)
 // (P = inclusive XOR prefix of the tile values in tile order, crc_combine.hip), or the XOR
@@ -364,8 +384,9 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
                                           const u32* __restrict__ local, const u32* __restrict__ segx, u32 nw, u32 nwb,
                                           const u32* __restrict__ overflow, const u32* __restrict__ gops,
                                           u32 final_xor, u32* __restrict__ out, u64* scan_status, u64 scan_words,
-                                          u32* scan_ticket) {
+                                          u32* scan_ticket, const u32* fault) {
   reset_scan_state(scan_status, scan_words, scan_ticket);  // the segment scan is done
+  if (scan_faulted(fault)) return;
   // the 13 inverse operators (6.5 KiB) staged in LDS: up to 104 dependent table lookups
   // per message read from global memory took 61 us for config C's 1 Mi messages (r01bu)
   __shared__ u32 inv[kNumInvOps * 128];

@@ -27,26 +27,33 @@
 //    Message i's payload is at base + i*stride, its MessagePrefix prefix_size bytes before.
 //    The checksum (client/checksum.h:29-37 over common/channel.h:527-542's spans) is
 //      ~crc_raw(~0, span0 || payload) = ~( Z_4096(crc_raw(~0, span0)) ^ crc_raw(0, payload) )
-//    with span0 = prefix[4, 48). The payload term is this kernel's message CRC from init 0.
-//    Per window of 32 tiles (64 messages, one per lane) each lane loads its message's 64-B
-//    prefix line -- issued with the window's first tile loads, so it lands with them -- and at
-//    the window's end computes crc_raw(~0, span0) (11 steps, flag bit set first for a
-//    publish, as SetHasChecksum() precedes the checksum: client/publisher.cc:664-675) and
-//    one Z_4096 opmul, XORs it into its ring slot and stores flag + checksum (publish) or
-//    the status (verify: client/client.cc:1346-1356; no kMessageHasChecksum -> unchecked).
-//    Mismatches are counted per workgroup and summed by one 64-bit atomic per workgroup
-//    that also counts finished workgroups; the last one writes the call's total.
+//    with span0 = prefix[4, 48). The payload term is the payload waves' message CRC from
+//    init 0. The workgroup has one more wave, the FINISHER: the 8 payload waves run exactly
+//    the plain kernel's stream (no prefix load, store or slot register in their loop) and
+//    leave each message CRC in an LDS ring, tagged with its tile index; the finisher loads
+//    the prefix lines of the messages the front is streaming (64 per group of 4 tiles, one
+//    per lane), computes crc_raw(~0, span0) (11 steps; for a publish with the
+//    kMessageHasChecksum bit set first, as SetHasChecksum() precedes the checksum:
+//    client/publisher.cc:664-675) and one Z_4096 opmul, waits for the tagged ring entries,
+//    and stores flag + checksum (publish) or the status (verify: client/client.cc:1346-1356;
+//    no kMessageHasChecksum -> unchecked). Every prefix load and slot store is in the
+//    finisher's own vmcnt stream, so no payload wave ever waits for one.
+//    Mismatches are summed by one 64-bit atomic per workgroup that also counts finished
+//    workgroups; the last one writes the call's total.
 #include "crc_device.h"
 
 
 namespace subspace_amd {
 
 template <int WG, bool SLOT, bool PROBE>
-__global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __restrict__ base, u64 stride, u64 count,
-                                                             const u32* __restrict__ gtab, const u32* __restrict__ gops,
-                                                             u32 init, u32 final_xor, u32* __restrict__ out,
-                                                             int order, u32* __restrict__ zero_word, SlotArgs sa) {
+__global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
+    const uint8_t* __restrict__ base, u64 stride, u64 count, const u32* __restrict__ gtab,
+    const u32* __restrict__ gops, u32 init, u32 final_xor, u32* __restrict__ out, int order,
+    u32* __restrict__ zero_word, SlotArgs sa) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
+  // WG / 64 payload waves; SLOT adds the finisher wave (wave index NPW)
+  constexpr int NPW = WG / 64;
+  constexpr int NT = SLOT ? WG + 64 : WG;
   const u32 sbase = (u32)(uintptr_t)smem;
   u64 pt[4] = {0, 0, 0, 0};  // PROBE: timestamps, stored at exit (no store inside the stream)
   if constexpr (PROBE) pt[0] = __builtin_amdgcn_s_memrealtime();
@@ -58,20 +65,24 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // Two 64-B lookup chains per line, joined by Z_64 (crc_device.h line_crc32_2chain): half
   // the dependent chain per tile for 8 more conflict-free lookups per line; config B 45.36 ->
   // 45.10 us (r02c17, slot_gap interleaved) and 45.4-45.8 -> 45.0-45.4 us (r02c18, sweep A/B,
-  // four pairs); config S publish 48.96 -> 48.70 us, verify 47.87 -> 47.62 (r02c20); bit-exact.
+  // four pairs); bit-exact.
   constexpr bool kTwoChain = true;  // (false: the one-chain line CRC, for A/B builds)
   // step tables, per-lane operators, Z_4096 and Z_64 (the two-chain line CRC's join)
-  LdsFill<WG, kTwoChain ? kUniOpSlots : kUniOpSlotsOneChain> fill;
+  LdsFill<NT, kTwoChain ? kUniOpSlots : kUniOpSlotsOneChain> fill;
   fill.load(gtab, gops);
 
   const int lane = threadIdx.x & 63;
   // wave-uniform (SGPR) wave index: keeps the tile loop a scalar loop, so hipcc's waitcnt
   // bookkeeping stays exact (a divergent loop makes it drain the prefetch every iteration)
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool finisher = SLOT && wid == NPW;
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
-  constexpr int kRing = SLOT ? kUniSlotRingResults : uni_ring_results(WG / 64);
-  const u32 ring = sbase + (SLOT ? kUniSlotRing : kUniRing) + (u32)wid * (4u * kRing);
+  constexpr int kRing = uni_ring_results(NPW);
+  const u32 ring = sbase + kUniRing + (u32)wid * (4u * kRing);
+  // SLOT: this wave's tagged result ring, and the finisher's progress word
+  const u32 sring = sbase + kUniSlotRing + (u32)wid * kSlotRingBytesPerWave;
+  const u32 sprog = sbase + uniform_slot_progress(NPW);
   const u32 lop = sbase + kLdsOps + 4u * (u32)(31 - (lane & 31));  // this lane's operator slot
   const int l = lane & 31, h = lane >> 5;
   const u64 ntiles = (count + 1) >> 1;
@@ -83,12 +94,13 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // its wpb consecutive tiles, w = b*wpb + wid.
   // Order 1 ("region"): workgroup b owns the contiguous tiles [b*per, (b+1)*per), its waves
   // interleave inside it: tau = b*per + k*wpb + wid.
-  constexpr u64 wpb = WG / 64;
+  // (The slot kernel's finisher replays order 0's mapping: the host launches SLOT with order 0.)
+  constexpr u64 wpb = NPW;
   const u64 nw = (u64)gridDim.x * wpb;
   u64 t0, tstep, tend;
   // order 3 needs whole XCD groups: 8 | G and 16 | (G/8)*wpb; otherwise it is order 0
   if (order == 3 && ((gridDim.x & 7u) || ((((u64)gridDim.x >> 3) * wpb) & 15u))) order = 0;
-  if (order == 0) {
+  if (SLOT || order == 0) {
     t0 = front_slot(blockIdx.x, gridDim.x, (u32)wid);
     tstep = nw;
     tend = ntiles;
@@ -115,7 +127,8 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // control scalar (a 64-bit compare needs VALU temporaries, which hipcc may place in a
   // buffer register still being loaded, forcing a vmcnt drain at the loop head).
   // (32-bit division: every tile count here is < 2^32, as count < 2^33 messages)
-  const u32 nk = t0 < tend ? ((u32)(tend - t0) + (u32)tstep - 1u) / (u32)tstep : 0u;
+  // The finisher wave has no tiles: it runs through the prologue and the empty loop.
+  const u32 nk = (!finisher && t0 < tend) ? ((u32)(tend - t0) + (u32)tstep - 1u) / (u32)tstep : 0u;
   const u32 s_init = (l == 0) ? init : 0u;
 
   // Tile k's lines. Past the wave's last tile it re-reads that tile, and the missing odd
@@ -140,7 +153,8 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     if constexpr (kTwoChain) return line_crc32_2chain(d, s_init, lc0, lc1, z64);
     else return line_crc32(d, s_init, lc0, lc1);
   };
-  // Message CRCs of tile k into ring slots 2*(k - kf) + h (kf = first tile of the window).
+  // Message CRCs of tile k: into ring slots 2*(k - kf) + h (kf = first tile of the window);
+  // SLOT: into the tagged ring entry 2*(k mod kSlotRingRounds) + h, as CRC | k << 32.
   auto tile_result = [&](u32 crc, u32 k, u32 kf) {
     u32 v = lane_shift(lop, crc);
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
@@ -148,71 +162,29 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-    if (l == 31) lds_st(ring + 4u * (2u * (k - kf) + (u32)h), v ^ final_xor);
-  };
-  // SLOT: the current window's prefix lines (lane j: message j of the window), their span-0
-  // term P = Z_4096(crc_raw(~0, span0)), stored checksum S, flags word F, the flag as found.
-  u32x4 Q[4];
-  u32 P = 0, S = 0, F = 0, mism = 0;
-  bool HAS = false;
-  const bool calc = sa.mode == 0u;
-  // message of lane j in the window of tiles kf.. (clamped like load_tile for the loads)
-  auto win_msg = [&](u32 kf, bool clamp) {
-    const u32 t = kf + ((u32)lane >> 1);
-    const u32 kk = !clamp ? t : (t < nk ? t : (nk ? nk - 1 : 0u));
-    u64 msg = (nk || !clamp) ? 2 * (t0 + (u64)kk * tstep) + (u64)(lane & 1) : 0;
-    if (clamp) msg = msg < count ? msg : msg - 1;
-    return msg;
-  };
-  auto load_prefix = [&](u32 kf) {
-    const u32x4* q = reinterpret_cast<const u32x4*>(base + win_msg(kf, true) * stride - sa.prefix_size);
-#pragma unroll
-    for (int i = 0; i < 4; i++) Q[i] = q[i];
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // After the drain that follows window 0's prefix loads: every loaded prefix word counts as
-  // used here. Words the checksum never reads (bytes 0-3, the checksum area's tail) would
-  // otherwise leave their registers free while the loads are in flight, and hipcc reused such
-  // a register in tile 0's compute -- which then waited for the prefix loads and for tile 1's,
-  // issued before them (config S publish 50.2 -> 49.6 us, verify 49.2 -> 48.4, r02c5). The
-  // same hint after the loop's drains ran 8.7 us slower (r02c4): only here.
-  auto prefix_landed = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; i++) asm volatile("" ::"v"(Q[i]));
-  };
-  auto prefix_pass = [&]() {
-    u32 w[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) w[i] = Q[i >> 2][i & 3];
-    HAS = (w[8] & 4u) != 0u;  // kMessageHasChecksum in MessagePrefix::flags (common/channel.h:62-70)
-    F = calc ? (w[8] | 4u) : w[8];
-    w[8] = F;
-    u32 hh = 0xFFFFFFFFu;
-#pragma unroll
-    for (int i = 1; i < 12; i++) hh = step4(hh ^ w[i], lc0, lc1);  // span 0 = prefix bytes [4, 48)
-    P = opmul(sbase, kUniSlotOpZ4096, hh);
-    S = w[12];  // the stored checksum (first 4 B of the checksum area, prefix + 48)
-  };
-  // Finish the window's messages: lane j takes ring slot j (its payload CRC, complemented)
-  // and XORs in its span-0 term; then stores flag + checksum, or the status.
-  auto slot_flush = [&](u32 kf, u32 nt) {
-    const u64 msg = win_msg(kf, false);
-    const bool valid = ((u32)lane >> 1) < nt && msg < count;
-    const u32 r = lds_ld(ring + 4u * (u32)lane) ^ P;
-    u32* pw = reinterpret_cast<u32*>(const_cast<uint8_t*>(base) + msg * stride - sa.prefix_size);
-    if (calc) {
-      if (valid) {
-        pw[8] = F;   // SetHasChecksum()
-        pw[12] = r;  // *reinterpret_cast<uint32_t*>(checksum.data()) = ~crc (client/checksum.h:36)
-        if (sa.status) sa.status[msg] = 0u;
-        if (sa.crc_out) sa.crc_out[msg] = r;
-      }
+    if constexpr (SLOT) {
+      if (l == 31)
+        lds_st64(sring + 16u * (k & (u32)(kSlotRingRounds - 1)) + 8u * (u32)h, ((u64)k << 32) | (u64)(v ^ final_xor));
     } else {
-      const u32 st = !HAS ? 2u : (r == S ? 0u : 1u);  // client/checksum.h:46
-      if (valid && sa.status) sa.status[msg] = st;
-      mism += (u32)__builtin_popcountll(__ballot(valid && st == 1u));
+      if (l == 31) lds_st(ring + 4u * (2u * (k - kf) + (u32)h), v ^ final_xor);
     }
-    wave_lds_sync();
+  };
+  // SLOT: before writing tiles k .. k+kSlotCheckRounds-1, the ring entries they replace
+  // (tiles k - kSlotRingRounds ..) must have been consumed by the finisher. It trails the
+  // slowest payload wave by a group of 4 tiles, so this wait is for waves that run more than
+  // kSlotRingRounds - kSlotCheckRounds - 4 tiles ahead of their slowest sibling.
+  // (bounded: a finisher that never advances raises kFaultSlotRoom instead of hanging the GPU,
+  // and the wave waits no more in this launch)
+  bool gave_up = false;
+  auto ring_room = [&](u32 k) {
+    for (u32 spins = 0; !gave_up && rfl(lds_ld_volatile(sprog)) + (u32)(kSlotRingRounds - kSlotCheckRounds) < k;
+         spins++) {
+      if (spins == kSpinBound) {
+        if (lane == 0) raise_fault(sa.fault, kFaultSlotRoom);
+        gave_up = true;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
   };
 
   // Store the ring's results of tiles kf .. kf+nt-1 (messages 2*tau, 2*tau+1 of each).
@@ -234,6 +206,12 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   u32x4 A[8], B[8];
   load_tile(A, 0);
   fill.store(sbase);
+  if constexpr (SLOT) {
+    // no ring entry may carry a tag before its tile is written; the progress word starts at 0
+    constexpr u32 kEntries = (u32)NPW * kSlotRingBytesPerWave / 8u;
+    for (u32 i = threadIdx.x; i < kEntries; i += NT) lds_st64(sbase + kUniSlotRing + 8u * i, ~0ull);
+    if (threadIdx.x == 0) lds_st(sprog, 0u);
+  }
   __syncthreads();
   // Wait for tile 0 right here (the loop's first drain is then a no-op). Waves without tiles
   // run through the loop without iterations rather than returning early: the early return
@@ -252,53 +230,20 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // profiles/r01/ceiling.md), and tile k+1's latency still hides behind tile k's compute.
   // A full ring is stored right after the next tile's loads are issued, so the stores
   // retire during that tile's compute instead of stalling the next drain (crc_long.hip).
-  // SLOT: a window's prefix lines are loaded with its first tile's loads (window 0's with
-  // tile 1's, below); the window ends right after a drain, before the next tile's loads,
-  // where its span-0 terms are computed and its messages finished and stored, and the next
-  // window's prefix lines are loaded.
-  // (Computing the span-0 terms right after the window's first drain instead -- so that only
-  // the stores remain at the end -- ran 62 vs 50 us at config S in an interleaved A/B, r02l.)
+  // SLOT: the same loop; the window check waits for ring room instead of storing.
+  constexpr u32 kWin = SLOT ? (u32)kSlotCheckRounds : (u32)(kRing / 2);
   u32 k = 0, kf = 0;
-  // SLOT: window 0's prefix lines go out with tile 1's loads, not with tile 0's: 4 MiB of
-  // scattered 64-B reads in the kernel's first flood delayed every wave's tile 0 by 1.6 us
-  // (tools/wave_timeline.py --mode publish, r02ai; config S publish 49.65 -> 49.42 us, verify
-  // 48.67 -> 48.45 us, tools/session_slotab.sh r02ak). The pair is peeled so that the wait for
-  // tile 0 counts the prefix loads exactly (inside the loop, a conditional load would make
-  // hipcc's merged count wait for the next tile's loads before computing the current one).
-  if constexpr (SLOT) {
-    if (k + 2 < nk) {
-      load_tile(B, 1);
-      load_prefix(0);
-      tile_result(line_crc(A), 0, 0);
-      drain_before_issue();
-      prefix_landed();
-      load_tile(A, 2);
-      tile_result(line_crc(B), 1, 0);
-      k = 2;
-    } else {
-      load_prefix(0);
-    }
-  }
-  // SLOT: the loop stops before the wave's last pair, which follows it: the last window's
-  // span-0 terms are computed while the wave's last tile is in flight
-  for (; SLOT ? k + 2 < nk : k + 1 < nk; k += 2) {
+  for (; k + 1 < nk; k += 2) {
     drain_before_issue();
-    if constexpr (SLOT) {
-      if (k - kf == (u32)(kRing / 2)) {
-        prefix_pass();
-        wave_lds_sync();
-        slot_flush(kf, kRing / 2);
-        load_prefix(k);
-        kf = k;
-      }
-      load_tile(B, k + 1);
-    } else {
-      load_tile(B, k + 1);
-      if (k - kf == (u32)(kRing / 2)) {
+    load_tile(B, k + 1);
+    if (k - kf == kWin) {
+      if constexpr (SLOT) {
+        ring_room(k);
+      } else {
         wave_lds_sync();
         flush(kf, kRing / 2);
-        kf = k;
       }
+      kf = k;
     }
     tile_result(line_crc(A), k, kf);
     drain_before_issue();
@@ -306,35 +251,10 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     tile_result(line_crc(B), k + 1, kf);
   }
   if constexpr (PROBE) pt[2] = __builtin_amdgcn_s_memrealtime();
-  bool pdone = false;  // SLOT: the current window's span-0 terms are computed
-  if constexpr (SLOT) {
-    if (k + 1 < nk) {  // the last pair: tile k loaded, tile k+1 the wave's last
-      drain_before_issue();
-      if (k - kf == (u32)(kRing / 2)) {
-        prefix_pass();
-        wave_lds_sync();
-        slot_flush(kf, kRing / 2);
-        load_prefix(k);
-        kf = k;
-      }
-      load_tile(B, k + 1);
-      if (k != kf) {  // the window's prefix lines landed a tile ago: overlap with tile k+1's loads
-        prefix_pass();
-        pdone = true;
-      }
-      tile_result(line_crc(A), k, kf);
-      drain_before_issue();
-      tile_result(line_crc(B), k + 1, kf);
-      k += 2;
-    }
-  }
   if (k < nk) {  // odd last tile, already loaded
-    if (k - kf == (u32)(kRing / 2)) {
+    if (k - kf == kWin) {
       if constexpr (SLOT) {
-        prefix_pass();
-        wave_lds_sync();
-        slot_flush(kf, kRing / 2);
-        load_prefix(k);
+        ring_room(k);
       } else {
         wave_lds_sync();
         flush(kf, kRing / 2);
@@ -344,25 +264,93 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
     tile_result(line_crc(A), k, kf);
   }
   wave_lds_sync();
-  u64 pt_flush = 0;
   if constexpr (SLOT) {
-    if (!pdone) prefix_pass();
-    if constexpr (PROBE) pt_flush = __builtin_amdgcn_s_memrealtime();
-    slot_flush(kf, nk > kf ? nk - kf : 0u);
-    // the call's mismatch count: one 64-bit atomic per workgroup adds (1 << 32) | its count;
-    // the workgroup that sees G - 1 finished before it writes the total and resets the word
-    if (!calc && sa.error_count) {
-      const u32 mring = sbase + kUniSlotRing + (u32)wid * (4u * kRing);
-      if (lane == 0) lds_st(mring, mism);
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        u32 n = 0;
+    if (finisher) {
+      // Group g = tiles 4g .. 4g+3 of every payload wave: lane j takes tile 4g + (j >> 4) of
+      // payload wave (j >> 1) & 7, message half j & 1 -- 64 messages, one per lane.
+      static_assert(NPW == 8, "the finisher's lane map assumes 8 payload waves");
+      const u32 fw = ((u32)lane >> 1) & 7u, fr = (u32)lane >> 4, fh = (u32)lane & 1u;
+      const u64 ft0 = front_slot(blockIdx.x, gridDim.x, fw);
+      const u32 fnk = ft0 < ntiles ? ((u32)(ntiles - ft0) + (u32)nw - 1u) / (u32)nw : 0u;
+      const u64 w0 = front_slot(blockIdx.x, gridDim.x, 0u);  // wave 0 has the most tiles
+      const u32 nk0 = w0 < ntiles ? ((u32)(ntiles - w0) + (u32)nw - 1u) / (u32)nw : 0u;
+      const u32 ngroups = (nk0 + 3u) >> 2;
+      const u32 fring = sbase + kUniSlotRing + fw * kSlotRingBytesPerWave + 8u * fh;
+      const bool calc = sa.mode == 0u;
+      auto gtile = [&](u32 g) { return 4u * g + fr; };
+      auto gmsg = [&](u32 g) { return 2 * (ft0 + (u64)gtile(g) * nw) + (u64)fh; };
+      auto gvalid = [&](u32 g) { return gtile(g) < fnk && gmsg(g) < count; };
+      u32x4 Q[4];
+      auto load_prefix = [&](u32 g) {
+        const u64 m = gvalid(g) ? gmsg(g) : 0;
+        const u32x4* q = reinterpret_cast<const u32x4*>(base + m * stride - sa.prefix_size);
 #pragma unroll
-        for (int q = 0; q < WG / 64; q++) n += lds_ld(sbase + kUniSlotRing + (u32)q * (4u * kRing));
-        const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(sa.counter), (1ull << 32) | (u64)n);
-        if ((u32)(old >> 32) == gridDim.x - 1u) {
-          *sa.error_count = (u32)old + n;
-          __hip_atomic_store(sa.counter, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 0; i < 4; i++) Q[i] = q[i];
+      };
+      u32 mism = 0;
+      // group 0's prefix lines go out once wave 0's tile 0 is in its ring (the first flood
+      // has landed), not with it
+      for (u32 spins = 0; nk0 != 0u && (u32)(lds_ld64(sbase + kUniSlotRing) >> 32) != 0u && spins < kSpinBound; spins++)
+        __builtin_amdgcn_s_sleep(8);
+      if (ngroups) load_prefix(0);
+      for (u32 g = 0; g < ngroups; g++) {
+        // span-0 term of the group's messages: P = Z_4096(crc_raw(~0, prefix[4, 48)))
+        u32 w[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = Q[i >> 2][i & 3];
+        const bool has = (w[8] & 4u) != 0u;  // kMessageHasChecksum (common/channel.h:62-70)
+        const u32 F = calc ? (w[8] | 4u) : w[8];
+        w[8] = F;
+        u32 hh = 0xFFFFFFFFu;
+#pragma unroll
+        for (int i = 1; i < 12; i++) hh = step4(hh ^ w[i], lc0, lc1);
+        const u32 P = opmul(sbase, kUniSlotOpZ4096, hh);
+        const u32 S = w[12];  // the stored checksum (first 4 B of the checksum area, prefix + 48)
+        const bool valid = gvalid(g);
+        const u64 msg = gmsg(g);
+        // wait for the group's tagged payload CRCs
+        const u32 ea = fring + 16u * (gtile(g) & (u32)(kSlotRingRounds - 1));
+        u64 e;
+        for (u32 spins = 0;; spins++) {
+          e = lds_ld64(ea);
+          if (gave_up || __ballot(valid && (u32)(e >> 32) != gtile(g)) == 0) break;
+          if (spins == kSpinBound) {  // never in a correct call: report, do not hang (nor wait again)
+            if (lane == 0) raise_fault(sa.fault, kFaultSlotRing);
+            gave_up = true;
+          }
+          __builtin_amdgcn_s_sleep(8);
+        }
+        // the entries are in registers: their ring slots may be reused
+        if (lane == 0) lds_st(sprog, 4u * g + 4u);
+        if (g + 1 < ngroups) load_prefix(g + 1);  // the front is now streaming group g+1
+        const u32 r = (u32)e ^ P;
+        u32* pw = reinterpret_cast<u32*>(const_cast<uint8_t*>(base) + msg * stride - sa.prefix_size);
+        if (calc) {
+          if (valid) {
+            pw[8] = F;   // SetHasChecksum()
+            pw[12] = r;  // *reinterpret_cast<uint32_t*>(checksum.data()) = ~crc (client/checksum.h:36)
+            if (sa.status) sa.status[msg] = 0u;
+            if (sa.crc_out) sa.crc_out[msg] = r;
+          }
+        } else {
+          const u32 st = !has ? 2u : (r == S ? 0u : 1u);  // client/checksum.h:46
+          if (valid && sa.status) sa.status[msg] = st;
+          mism += (u32)__builtin_popcountll(__ballot(valid && st == 1u));
+        }
+      }
+      if (sa.error_count && lane == 0) {
+        if (calc) {
+          // a publish has no mismatches: the count is 0 (include/subspace_crc.h)
+          if (blockIdx.x == 0) *sa.error_count = 0u;
+        } else {
+          // the call's mismatch count: one 64-bit atomic per workgroup adds (1 << 32) | its
+          // count; the workgroup that sees G - 1 finished before it writes the total and
+          // resets the word
+          const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(sa.counter), (1ull << 32) | (u64)mism);
+          if ((u32)(old >> 32) == gridDim.x - 1u) {
+            *sa.error_count = (u32)old + mism;
+            __hip_atomic_store(sa.counter, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         }
       }
     }
@@ -373,12 +361,14 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __re
   // here, at the end, so the call needs no separate memset
   if (zero_word != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0u;
   if constexpr (PROBE) {
-    pt[3] = __builtin_amdgcn_s_memrealtime();
-    u64* r = sa.probe + ((u64)blockIdx.x * wpb + (u64)wid) * kProbeWords;
-    const u64 xcc = (u64)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-    const u64 v = lane == 0 ? pt[0] : lane == 1 ? pt[1] : lane == 2 ? pt[2] : lane == 3 ? pt[3]
-                : lane == 4 ? pt_args : lane == 5 ? (xcc | ((u64)nk << 32)) : lane == 6 ? pt_flush : pt_landed;
-    if (lane < 8) r[lane] = v;
+    if (!finisher) {
+      pt[3] = __builtin_amdgcn_s_memrealtime();
+      u64* r = sa.probe + ((u64)blockIdx.x * wpb + (u64)wid) * kProbeWords;
+      const u64 xcc = (u64)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+      const u64 v = lane == 0 ? pt[0] : lane == 1 ? pt[1] : lane == 2 ? pt[2] : lane == 3 ? pt[3]
+                  : lane == 4 ? pt_args : lane == 5 ? (xcc | ((u64)nk << 32)) : lane == 6 ? 0ull : pt_landed;
+      if (lane < 8) r[lane] = v;
+    }
   }
 }
 

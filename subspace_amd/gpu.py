@@ -20,15 +20,18 @@ POLY_CASTAGNOLI = 0x82F63B78  # CRC-32C: -msse4.2 reference builds (SubspaceCRC3
 SLOT_CALCULATE = 0  # publisher: set kMessageHasChecksum, store the 3-span checksum in the prefix
 SLOT_VERIFY = 1     # subscriber: check the stored checksum of slots that carry the flag
 SLOT_OK, SLOT_MISMATCH, SLOT_UNCHECKED = 0, 1, 2
+EFAULT = -5  # SUBSPACE_CRC_EFAULT: a kernel of an earlier call gave up a bounded wait
 
 
 class CrcError(RuntimeError):
-    pass
+    def __init__(self, msg: str, code: int = 0):
+        super().__init__(msg)
+        self.code = code
 
 
 def _check(rc: int, what: str) -> None:
     if rc != 0:
-        raise CrcError(f"{what} failed ({rc}): {_lib.last_error()}")
+        raise CrcError(f"{what} failed ({rc}): {_lib.last_error()}", rc)
 
 
 def _ptr(t) -> int:
@@ -69,6 +72,11 @@ class CrcContext:
 
     def __exit__(self, *exc):
         self.close()
+
+    def check(self, stream=None) -> None:
+        """Synchronise ``stream`` and raise CrcError (code EFAULT) if a kernel of an earlier
+        call on this context gave up a bounded wait (subspace_crc_ctx_check)."""
+        _check(self._lib.subspace_crc_ctx_check(self._h, _stream_ptr(stream)), "subspace_crc_ctx_check")
 
     def reserve(self, max_messages: int, max_tiles: int) -> None:
         _check(self._lib.subspace_crc_ctx_reserve(self._h, max_messages, max_tiles), "subspace_crc_ctx_reserve")

@@ -329,7 +329,7 @@ def _corrupt(host, po, ps, cs, sizes, seed):
     return kinds
 
 
-@pytest.mark.parametrize("count", [1, 2, 3, 63, 4097, 65537, 140001])
+@pytest.mark.parametrize("count", [1, 2, 3, 63, 4097, 65537, 140001, 300001])
 @pytest.mark.parametrize("cs", [4, 20])
 def test_fused_slot_kernel_publish_and_verify(gpu_ctx, oracle, count, cs):
     """The fused slot kernel (contiguous 4 KiB slots, metadata_size 0: payload CRC, span-0
@@ -438,3 +438,24 @@ def test_fused_slot_verify_graph_replay(gpu_ctx):
         g.replay()
         torch.cuda.synchronize()
         assert int(err.item()) == 3
+
+
+@pytest.mark.parametrize("fused", [1, 0])
+def test_calculate_zeroes_error_count(gpu_ctx, fused):
+    """A publish (CALCULATE) has no mismatches: the error count it is given reads 0 afterwards,
+    through the fused slot kernel and the two-kernel path alike (include/subspace_crc.h:
+    'set to the number of SUBSPACE_CRC_SLOT_MISMATCH slots of this call')."""
+    from subspace_amd import _lib
+    lib = _lib.load()
+    count, cs, ms = 3001, 4, 0
+    sizes = np.full(count, 4096, dtype=np.uint64)
+    host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=606)
+    dev = torch.from_numpy(host).to(DEV)
+    err = torch.full((1,), 777, dtype=torch.int32, device=DEV)
+    assert lib.subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", fused) == 0
+    try:
+        gpu_ctx.crc32_slots_strided(dev, stride, count, message_size=4096, mode=gpu.SLOT_CALCULATE, error_count=err)
+        torch.cuda.synchronize()
+    finally:
+        lib.subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", 1)
+    assert int(err.item()) == 0

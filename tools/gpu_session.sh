@@ -57,6 +57,20 @@ for s in $STEPS; do
       timeout -k 10 600 python tools/bench_configs.py --configs C,Cu,D,E,S > "$OUT/configs.log" 2>&1
       rc=$?
       if [ $rc -ne 0 ]; then echo "step configs rc=$rc (stop)" >> "$OUT/status.txt"; exit $rc; fi ;;
+    slottest)  # the slot, fault and config-S tests only (a kernel change's first check)
+      timeout -k 10 900 python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread \
+        tests/test_gpu_fault.py tests/test_gpu_slots.py tests/test_gpu_configs.py -k "fault or slot or Slot or S_ or stream" \
+        > "$OUT/pytest_slot.log" 2>&1
+      rc=$?
+      if [ $rc -ne 0 ]; then echo "step slottest rc=$rc (stop)" >> "$OUT/status.txt"; exit $rc; fi ;;
+    slotgap)  # config S kernels vs the plain uniform kernel over the same buffers, interleaved
+      timeout -k 10 300 python tools/slot_gap.py 5 > "$OUT/slot_gap.jsonl" 2> "$OUT/slot_gap.err"
+      stop_if_fault $? slotgap ;;
+    timeline)  # per-wave timelines: config B, config S payloads, publish, verify
+      for m in uniform uniform4160 publish verify; do
+        timeout -k 10 300 python tools/wave_timeline.py --mode $m --launches 20 > "$OUT/timeline_$m.jsonl" 2> "$OUT/timeline_$m.err"
+        stop_if_fault $? "timeline_$m"
+      done ;;
     *)
       echo "unknown step $s" >> "$OUT/status.txt" ;;
   esac
