@@ -378,10 +378,12 @@ class Workload:
                                stream=streams[i % len(streams)])
 
     def check(self, dist):
-        """(bit-exact vs the fixture on rank 0, gather ms). Collective when world > 1: the
-        4-byte CRCs of every rank are all_gathered to global order and the whole list is
-        compared with the fixture (B: each rank's batch 0 is a distinct id set, so at
-        world 1 it is exactly config B)."""
+        """(bit-exact vs the fixture on rank 0, gather timing). Collective when world > 1: the
+        4-byte CRCs of every rank are all_gathered (RCCL over xGMI) and put in global order on
+        the device; HIP events on the current stream time exactly that (`gather_ms`, the device
+        gather: the collective plus the on-device interleave; at world 1 one device copy). The
+        D2H copy and the host hash check are timed apart (`d2h_check_ms`). B: each rank's
+        batch 0 is a distinct id set, so at world 1 it is exactly config B."""
         import torch
         from subspace_amd import shard
         if self.name == "B":
@@ -391,16 +393,19 @@ class Workload:
         if self.world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        tg = time.perf_counter()
-        if self.world > 1 and self.name == "C":
-            full = shard.gather_ragged_crcs(self.outs[0][:self.nmsg], self.bounds, self.rank, self.world, dist)
-        elif self.world > 1:
-            full = shard.gather_crcs(self.outs[0], E_COUNT, self.rank, self.world, dist)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        if self.name == "C":
+            full = shard.gather_ragged_crcs_device(self.outs[0][:self.nmsg], self.bounds, self.world, dist)
         else:
-            full = self.outs[0][:self.nmsg].cpu().numpy().view(np.uint32)
-        gather_ms = (time.perf_counter() - tg) * 1e3
-        ok = digest(full) == GOLD[self.name]["sha256_le_u32"] if full is not None else None
-        return ok, gather_ms
+            full = shard.gather_crcs_device(self.outs[0], E_COUNT, self.world, dist)
+        ev[1].record()
+        torch.cuda.synchronize()
+        gather_ms = ev[0].elapsed_time(ev[1])
+        tc = time.perf_counter()
+        ok = digest(full.cpu().numpy().view(np.uint32)) == GOLD[self.name]["sha256_le_u32"] if self.rank == 0 else None
+        return ok, {"gather_ms": round(gather_ms, 4), "d2h_check_ms": round((time.perf_counter() - tc) * 1e3, 3),
+                    "gather_bytes": int(full.numel()) * 4}
 
     def free(self):
         self.bufs, self.outs = [], []
@@ -429,7 +434,8 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, re
     """W untimed warm-up steps (after settle launches: at least `settle` - W of them and at
     least `settle_s` seconds of them), then EXACTLY `steps` steps between barrier +
     synchronize on both sides. Returns (max-over-ranks seconds, HIP-event span of the region
-    / steps in ms, sampled per-launch ms or None, settle launches run)."""
+    / steps in ms, sampled per-launch ms or None, settle launches run, this rank's own
+    seconds)."""
     import torch
     stream = streams[0]
     n_settle, t_settle = 0, time.perf_counter()
@@ -466,7 +472,7 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, re
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = own = time.perf_counter() - t0
     if region_marks:
         region_marks.pause()
     if world > 1:
@@ -475,7 +481,7 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, re
         elapsed = float(t.item())
     avg_ms = region[0].elapsed_time(region[1]) / steps
     sampled = float(np.mean([a.elapsed_time(b) for a, b in ev.values()])) if ev else None
-    return elapsed, avg_ms, sampled, n_settle + warmup
+    return elapsed, avg_ms, sampled, n_settle + warmup, own
 
 
 # ------------------------------------------------------------------------------ secondary configs
@@ -666,20 +672,27 @@ def dry_run_cpu(args, world, rank) -> int:
         step()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = own = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     tl = torch.from_numpy(local[:len(msgs)].view(np.int32).copy())
     tg = time.perf_counter()
-    if world > 1 and wl == "C":
-        full = shard.gather_ragged_crcs(tl, bounds, rank, world, dist)
-    elif world > 1 and wl == "E":
-        full = shard.gather_crcs(tl, count, rank, world, dist)
+    # the same gather helpers as the GPU run (here on CPU tensors over gloo)
+    if wl == "C":
+        full = shard.gather_ragged_crcs_device(tl, bounds, world, dist).numpy().view(np.uint32)
+    elif wl == "E":
+        full = shard.gather_crcs_device(tl, count, world, dist).numpy().view(np.uint32)
     else:
         full = local[:len(msgs)]
     gather_ms = (time.perf_counter() - tg) * 1e3
+    me = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": "cpu", "pid": os.getpid(),
+          "step_ms": round(own / args.steps * 1e3, 4)}
+    everyone = [me]
+    if world > 1:
+        everyone = [None] * world
+        dist.all_gather_object(everyone, me)
     if rank == 0:
         total = (step_bytes * world if wl == "B" else GOLD[key]["total_bytes"]) * args.steps
         value = total / elapsed / 2**30
@@ -695,6 +708,10 @@ def dry_run_cpu(args, world, rank) -> int:
                        "gather_ms": round(gather_ms, 3)},
             "per_gpu_value": round(value / world, 3),
             "bitexact_vs_golden": digest(full) == GOLD[key]["sha256_le_u32"] if full is not None else None,
+            "ranks": everyone,
+            "rank_step_ms": {"min": min(r["step_ms"] for r in everyone), "max": max(r["step_ms"] for r in everyone)},
+            "rccl_world": dist.get_world_size() if world > 1 else 1,
+            "backend": dist.get_backend() if world > 1 else None,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -744,12 +761,24 @@ def main():
     streams = [stream] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
     for s2 in streams[1:]:
         s2.wait_stream(stream)
-    elapsed, avg_kern_ms, sampled_ms, settle = run_timed(wl, args.steps, args.warmup, args.settle, streams, world,
-                                                         dist, args.event_every,
-                                                         RoctxRegion(args.roctx_region and rank == 0),
-                                                         args.settle_s if args.settle > 0 else 0.0)
+    elapsed, avg_kern_ms, sampled_ms, settle, own_s = run_timed(wl, args.steps, args.warmup, args.settle, streams,
+                                                                world, dist, args.event_every,
+                                                                RoctxRegion(args.roctx_region and rank == 0),
+                                                                args.settle_s if args.settle > 0 else 0.0)
     settle = max(0, settle - args.warmup)
-    bitexact, gather_ms = wl.check(dist)
+    bitexact, gather = wl.check(dist)
+    gather_ms = gather["gather_ms"] if gather else None
+    # every rank's identity and timing, so the line shows that N distinct GPUs ran
+    props = torch.cuda.get_device_properties(gpu_index)
+    me = {"rank": rank, "local_rank": local, "device": torch.cuda.current_device(),
+          "pci": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
+          "uuid": str(getattr(props, "uuid", "")), "step_ms": round(own_s / args.steps * 1e3, 4),
+          "launch_ms_event": round(avg_kern_ms, 4)}
+    if world > 1:
+        everyone = [None] * world
+        dist.all_gather_object(everyone, me)
+    else:
+        everyone = [me]
     step_bytes, total_step_bytes, nmsg = wl.step_bytes, wl.total_bytes, wl.nmsg
     bounds = getattr(wl, "bounds", None)
 
@@ -764,7 +793,7 @@ def main():
                 one = Workload(args.workload, ctx, dev, 1, 0)
                 torch.cuda.synchronize()
                 solo_steps = max(1, min(args.steps, 200 if args.workload == "B" else 20))
-                el1, avg1, _, _ = run_timed(one, solo_steps, min(args.warmup, 3), 0, [stream], 1, None)
+                el1, avg1, _, _, _ = run_timed(one, solo_steps, min(args.warmup, 3), 0, [stream], 1, None)
                 ok1, _ = one.check(None)
                 solo = {"value": round(one.total_bytes * solo_steps / el1 / 2**30, 2), "steps": solo_steps,
                         "ms_per_step": round(el1 / solo_steps * 1e3, 4), "bitexact_vs_golden": ok1,
@@ -828,15 +857,17 @@ def main():
                         "messages_rank0": nmsg, "bytes_total": total_step_bytes,
                         "parallelism": f"contiguous byte-balanced shards x{world}, RCCL all_gather of CRCs "
                                        "(timed separately)",
-                        "gather_ms": round(gather_ms, 3) if gather_ms is not None else None}
+                        "gather": gather,
+                        "value_incl_gather": round(total_bytes / (elapsed + args.steps * gather_ms * 1e-3) / 2**30, 2)
+                        if gather_ms is not None else None}
             scaling = "strong"
         else:
             workload = {"workload": "E: 8 Mi x 4 KiB payloads per step, round-robin over the GPUs, one CRC32 each",
                         "messages_total": E_COUNT, "messages_per_gpu": nmsg, "message_bytes": MSG_BYTES,
                         "parallelism": f"round-robin message shards x{world}, RCCL all_gather of CRCs "
                                        "(timed separately)",
-                        "gather_ms": round(gather_ms, 3) if gather_ms is not None else None,
-                        # the same rate with one gather of every step's CRCs to rank 0 added per step
+                        "gather": gather,
+                        # the same rate with one device gather of every step's CRCs added per step
                         "value_incl_gather": round(total_bytes / (elapsed + args.steps * gather_ms * 1e-3) / 2**30, 2)
                         if gather_ms is not None else None}
             scaling = "strong"
@@ -871,6 +902,13 @@ def main():
                                              "consecutive launches overlap when 2)",
                          "sampled_launch_ms": round(sampled_ms, 4) if sampled_ms else None},
         }
+        steps_ms = [r["step_ms"] for r in everyone]
+        line["ranks"] = everyone
+        line["rank_step_ms"] = {"min": min(steps_ms), "max": max(steps_ms)}
+        line["distinct_gpus"] = len({r["pci"] + r["uuid"] for r in everyone})
+        if world > 1:
+            line["rccl_world"] = dist.get_world_size()
+            line["backend"] = dist.get_backend()
         if solo is not None:
             line["single_gpu"] = solo
             line["efficiency"] = round(value / (world * solo["value"]), 4) if "value" in solo else None

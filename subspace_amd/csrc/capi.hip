@@ -229,8 +229,7 @@ int use_workspace(subspace_crc_ctx* c, hipStream_t st) {
 const char* fault_text(u32 f) {
   if (f & kFaultTicket) return "a look-back scan ticket was beyond its grid (stale scan state)";
   if (f & kFaultLookbackSpin) return "a look-back scan predecessor never published (stale scan state)";
-  if (f & kFaultSlotRing) return "the fused slot kernel's finisher never received a payload CRC";
-  if (f & kFaultSlotRoom) return "a fused slot payload wave never got ring room";
+  if (f & kFaultSlotRing) return "a fused slot kernel finishing wave never received a payload CRC";
   return "unknown fault";
 }
 
@@ -786,15 +785,18 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
   // payload CRC, the span-0 term and the flag/checksum store or status in one kernel
   if (!dev_message_sizes && message_size == 4096 && metadata_size == 0 && slot_stride % 16 == 0 &&
       ((uintptr_t)(buf + prefix_size) % 16) == 0 && c->fused_slots) {
-    // 8 payload waves + the finisher wave per workgroup, tile order 0 (the finisher replays it)
-    const int blocks = grid_for(c, (count + 1) / 2, 512 / 64);
+    // 8 waves per workgroup, tile order 0 (the finishing waves replay it), and at most
+    // kSlotRingRounds tiles per wave (a workgroup is one ring window): more workgroups than
+    // CUs for channels above 256 x 8 x 32 tiles
+    const u64 tiles = (count + 1) / 2;
+    const u64 blocks = std::max<u64>(grid_for(c, tiles, 512 / 64), ceil_div(tiles, 8ull * kSlotRingRounds));
     SlotArgs sa{prefix_size, mode, dev_status, dev_crc_out, dev_error_count,
                 c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters), c->probe, c->d_fault};
     if (c->probe)  // experiment hook: the timestamp-recording instantiation
-      crc32_uniform4k_kernel<512, true, true><<<blocks, 512 + 64, uniform_slot_lds_bytes(8), st>>>(
+      crc32_uniform4k_kernel<512, true, true><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
           buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, 0, nullptr, sa);
     else
-      crc32_uniform4k_kernel<512, true, false><<<blocks, 512 + 64, uniform_slot_lds_bytes(8), st>>>(
+      crc32_uniform4k_kernel<512, true, false><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
           buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, 0, nullptr, sa);
     HIP_TRY(hipGetLastError());
     return SUBSPACE_CRC_OK;

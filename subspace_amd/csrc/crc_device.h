@@ -46,15 +46,16 @@ constexpr int uni_ring_results(int waves) { return kUniRing + (u32)waves * 1024u
 constexpr size_t uniform_lds_bytes(int waves) { return kUniRing + (size_t)waves * 4u * uni_ring_results(waves); }
 static_assert(uniform_lds_bytes(16) <= 160u * 1024u && uniform_lds_bytes(8) <= 160u * 1024u,
               "uniform kernel LDS exceeds 160 KiB");
-// Slot variant (crc_uniform.hip, SLOT = true): the payload waves' results go to per-wave rings
-// of kSlotRingRounds tiles (2 tagged 8-B entries per tile: CRC | tile index << 32), read by the
-// workgroup's finisher wave; then the finisher's progress word (tiles consumed).
+// Slot variant (crc_uniform.hip, SLOT = true): each wave's results go to a ring of
+// kSlotRingRounds tiles (2 tagged 8-B entries per tile: CRC | tile index << 32; a workgroup is
+// one ring window: the host gives no wave more tiles), read after the tile loop by the
+// workgroup's kSlotFinishers finishing waves; then the workgroup's mismatch word.
 constexpr u32 kUniSlotRing = kUniRing;
 constexpr int kSlotRingRounds = 32;
-constexpr int kSlotCheckRounds = 16;  // payload waves check the finisher's progress every 16 tiles
+constexpr int kSlotFinishers = 4;  // waves 0-3: the older wave of each SIMD pair
 constexpr u32 kSlotRingBytesPerWave = 2u * 8u * kSlotRingRounds;
-constexpr u32 uniform_slot_progress(int waves) { return kUniSlotRing + (u32)waves * kSlotRingBytesPerWave; }
-constexpr size_t uniform_slot_lds_bytes(int waves) { return uniform_slot_progress(waves) + 16u; }
+constexpr u32 uniform_slot_mism_word(int waves) { return kUniSlotRing + (u32)waves * kSlotRingBytesPerWave; }
+constexpr size_t uniform_slot_lds_bytes(int waves) { return uniform_slot_mism_word(waves) + 16u; }
 static_assert(uniform_slot_lds_bytes(8) <= 160u * 1024u, "slot kernel LDS exceeds 160 KiB");
 
 // Fused slot checksums of the uniform 4 KiB kernel: the message-slot layout of
@@ -75,8 +76,7 @@ struct SlotArgs {
 // the GPU, and the host reports the call as failed (subspace_crc_ctx_check) instead of OK.
 constexpr u32 kFaultLookbackSpin = 1u;  // a look-back scan predecessor never published
 constexpr u32 kFaultTicket = 2u;        // a look-back scan ticket beyond the grid (stale ticket)
-constexpr u32 kFaultSlotRing = 4u;      // the slot finisher waited too long for a payload CRC
-constexpr u32 kFaultSlotRoom = 8u;      // a slot payload wave waited too long for ring room
+constexpr u32 kFaultSlotRing = 4u;      // a slot finishing wave waited too long for a payload CRC
 __device__ __forceinline__ void raise_fault(u32* fault, u32 bit) {
   if (fault) __hip_atomic_fetch_or(fault, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -84,8 +84,9 @@ __device__ __forceinline__ void raise_fault(u32* fault, u32 bit) {
 constexpr u32 kSpinBound = 1u << 20;
 // Per-wave probe record of the uniform kernel's PROBE instantiation: realtime clock (100 MHz)
 // at entry, after the LDS fill + barrier, after the tile loop, at exit, after the table and
-// tile-0 loads were issued; then XCC_ID | tile count << 32; the clock before the last slot
-// flush (slot instantiation, else 0) and when the wave's first tile had landed.
+// tile-0 loads were issued; then XCC_ID | tile count << 32; the wave's HW_ID register (wave
+// slot [3:0], SIMD [5:4], CU [11:8], SE [14:13]) | the low 32 bits of the clock when a slot
+// finishing wave began (else 0) << 32; when the wave's first tile had landed.
 constexpr int kProbeWords = 8;
 
 // Ragged-kernel layout: tables, the same line-shift operators, then opmul slots Z_4096 and

@@ -27,33 +27,38 @@
 //    Message i's payload is at base + i*stride, its MessagePrefix prefix_size bytes before.
 //    The checksum (client/checksum.h:29-37 over common/channel.h:527-542's spans) is
 //      ~crc_raw(~0, span0 || payload) = ~( Z_4096(crc_raw(~0, span0)) ^ crc_raw(0, payload) )
-//    with span0 = prefix[4, 48). The payload term is the payload waves' message CRC from
-//    init 0. The workgroup has one more wave, the FINISHER: the 8 payload waves run exactly
-//    the plain kernel's stream (no prefix load, store or slot register in their loop) and
-//    leave each message CRC in an LDS ring, tagged with its tile index; the finisher loads
-//    the prefix lines of the messages the front is streaming (64 per group of 4 tiles, one
-//    per lane), computes crc_raw(~0, span0) (11 steps; for a publish with the
-//    kMessageHasChecksum bit set first, as SetHasChecksum() precedes the checksum:
-//    client/publisher.cc:664-675) and one Z_4096 opmul, waits for the tagged ring entries,
-//    and stores flag + checksum (publish) or the status (verify: client/client.cc:1346-1356;
-//    no kMessageHasChecksum -> unchecked). Every prefix load and slot store is in the
-//    finisher's own vmcnt stream, so no payload wave ever waits for one.
-//    Mismatches are summed by one 64-bit atomic per workgroup that also counts finished
-//    workgroups; the last one writes the call's total.
+//    with span0 = prefix[4, 48). The payload term is the message CRC from init 0. The waves
+//    run exactly the plain kernel's stream -- no prefix load, slot store or slot register in
+//    the tile loop -- and leave each message CRC in an LDS ring, tagged with its tile index.
+//    Every workgroup is one ring window (<= kSlotRingRounds tiles per wave; the host launches
+//    more workgroups for longer channels). After its tiles, each of waves 0-3 -- the older
+//    wave of each SIMD pair, which runs ~1.3 us ahead of its partner --
+//    finishes a quarter of the workgroup's messages: it loads their prefix lines (one per
+//    lane), computes crc_raw(~0, span0) (11 steps; for a publish with the kMessageHasChecksum
+//    bit set first, as SetHasChecksum() precedes the checksum: client/publisher.cc:664-675) and
+//    one Z_4096 opmul, waits for the tagged ring entries of waves 4-7, and stores flag +
+//    checksum (publish) or the status (verify: client/client.cc:1346-1356; no
+//    kMessageHasChecksum -> unchecked). Mismatches are summed per workgroup with one LDS
+//    atomic per finishing wave and over workgroups by one 64-bit global atomic per workgroup
+//    that also counts finished workgroups; the last one writes the call's total.
 #include "crc_device.h"
 
+// Timing-only investigation builds of the slot finishing (tools/ubench/build_slot_variants.sh
+// passes -DSUBSPACE_SLOT_VARIANT=n; the product build is 0): 10 publish stores whole 32-B
+// sectors (prefix words 8-15); 12 no prefix stores; 13 no prefix loads (zeros).
+#ifndef SUBSPACE_SLOT_VARIANT
+#define SUBSPACE_SLOT_VARIANT 0
+#endif
 
 namespace subspace_amd {
 
 template <int WG, bool SLOT, bool PROBE>
-__global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
+__global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
     const uint8_t* __restrict__ base, u64 stride, u64 count, const u32* __restrict__ gtab,
     const u32* __restrict__ gops, u32 init, u32 final_xor, u32* __restrict__ out, int order,
     u32* __restrict__ zero_word, SlotArgs sa) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
-  // WG / 64 payload waves; SLOT adds the finisher wave (wave index NPW)
-  constexpr int NPW = WG / 64;
-  constexpr int NT = SLOT ? WG + 64 : WG;
+  constexpr int NPW = WG / 64;  // waves
   const u32 sbase = (u32)(uintptr_t)smem;
   u64 pt[4] = {0, 0, 0, 0};  // PROBE: timestamps, stored at exit (no store inside the stream)
   if constexpr (PROBE) pt[0] = __builtin_amdgcn_s_memrealtime();
@@ -68,21 +73,20 @@ __global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
   // four pairs); bit-exact.
   constexpr bool kTwoChain = true;  // (false: the one-chain line CRC, for A/B builds)
   // step tables, per-lane operators, Z_4096 and Z_64 (the two-chain line CRC's join)
-  LdsFill<NT, kTwoChain ? kUniOpSlots : kUniOpSlotsOneChain> fill;
+  LdsFill<WG, kTwoChain ? kUniOpSlots : kUniOpSlotsOneChain> fill;
   fill.load(gtab, gops);
 
   const int lane = threadIdx.x & 63;
   // wave-uniform (SGPR) wave index: keeps the tile loop a scalar loop, so hipcc's waitcnt
   // bookkeeping stays exact (a divergent loop makes it drain the prefetch every iteration)
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool finisher = SLOT && wid == NPW;
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
   constexpr int kRing = uni_ring_results(NPW);
   const u32 ring = sbase + kUniRing + (u32)wid * (4u * kRing);
-  // SLOT: this wave's tagged result ring, and the finisher's progress word
+  // SLOT: this wave's tagged result ring; the workgroup's mismatch word
   const u32 sring = sbase + kUniSlotRing + (u32)wid * kSlotRingBytesPerWave;
-  const u32 sprog = sbase + uniform_slot_progress(NPW);
+  const u32 smism = sbase + uniform_slot_mism_word(NPW);
   const u32 lop = sbase + kLdsOps + 4u * (u32)(31 - (lane & 31));  // this lane's operator slot
   const int l = lane & 31, h = lane >> 5;
   const u64 ntiles = (count + 1) >> 1;
@@ -94,7 +98,7 @@ __global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
   // its wpb consecutive tiles, w = b*wpb + wid.
   // Order 1 ("region"): workgroup b owns the contiguous tiles [b*per, (b+1)*per), its waves
   // interleave inside it: tau = b*per + k*wpb + wid.
-  // (The slot kernel's finisher replays order 0's mapping: the host launches SLOT with order 0.)
+  // (The slot finishing replays order 0's mapping: the host launches SLOT with order 0.)
   constexpr u64 wpb = NPW;
   const u64 nw = (u64)gridDim.x * wpb;
   u64 t0, tstep, tend;
@@ -127,8 +131,7 @@ __global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
   // control scalar (a 64-bit compare needs VALU temporaries, which hipcc may place in a
   // buffer register still being loaded, forcing a vmcnt drain at the loop head).
   // (32-bit division: every tile count here is < 2^32, as count < 2^33 messages)
-  // The finisher wave has no tiles: it runs through the prologue and the empty loop.
-  const u32 nk = (!finisher && t0 < tend) ? ((u32)(tend - t0) + (u32)tstep - 1u) / (u32)tstep : 0u;
+  const u32 nk = t0 < tend ? ((u32)(tend - t0) + (u32)tstep - 1u) / (u32)tstep : 0u;
   const u32 s_init = (l == 0) ? init : 0u;
 
   // Tile k's lines. Past the wave's last tile it re-reads that tile, and the missing odd
@@ -154,7 +157,7 @@ __global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
     else return line_crc32(d, s_init, lc0, lc1);
   };
   // Message CRCs of tile k: into ring slots 2*(k - kf) + h (kf = first tile of the window);
-  // SLOT: into the tagged ring entry 2*(k mod kSlotRingRounds) + h, as CRC | k << 32.
+  // SLOT: into the tagged ring entry 2*k + h (k < kSlotRingRounds), as CRC | k << 32.
   auto tile_result = [&](u32 crc, u32 k, u32 kf) {
     u32 v = lane_shift(lop, crc);
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
@@ -169,24 +172,6 @@ __global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
       if (l == 31) lds_st(ring + 4u * (2u * (k - kf) + (u32)h), v ^ final_xor);
     }
   };
-  // SLOT: before writing tiles k .. k+kSlotCheckRounds-1, the ring entries they replace
-  // (tiles k - kSlotRingRounds ..) must have been consumed by the finisher. It trails the
-  // slowest payload wave by a group of 4 tiles, so this wait is for waves that run more than
-  // kSlotRingRounds - kSlotCheckRounds - 4 tiles ahead of their slowest sibling.
-  // (bounded: a finisher that never advances raises kFaultSlotRoom instead of hanging the GPU,
-  // and the wave waits no more in this launch)
-  bool gave_up = false;
-  auto ring_room = [&](u32 k) {
-    for (u32 spins = 0; !gave_up && rfl(lds_ld_volatile(sprog)) + (u32)(kSlotRingRounds - kSlotCheckRounds) < k;
-         spins++) {
-      if (spins == kSpinBound) {
-        if (lane == 0) raise_fault(sa.fault, kFaultSlotRoom);
-        gave_up = true;
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
-  };
-
   // Store the ring's results of tiles kf .. kf+nt-1 (messages 2*tau, 2*tau+1 of each).
   auto flush = [&](u32 kf, u32 nt) {
 #pragma unroll
@@ -207,10 +192,10 @@ __global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
   load_tile(A, 0);
   fill.store(sbase);
   if constexpr (SLOT) {
-    // no ring entry may carry a tag before its tile is written; the progress word starts at 0
+    // no ring entry may carry a tag before its tile is written; the mismatch word starts at 0
     constexpr u32 kEntries = (u32)NPW * kSlotRingBytesPerWave / 8u;
-    for (u32 i = threadIdx.x; i < kEntries; i += NT) lds_st64(sbase + kUniSlotRing + 8u * i, ~0ull);
-    if (threadIdx.x == 0) lds_st(sprog, 0u);
+    for (u32 i = threadIdx.x; i < kEntries; i += WG) lds_st64(sbase + kUniSlotRing + 8u * i, ~0ull);
+    if (threadIdx.x == 0) lds_st(smism, 0u);
   }
   __syncthreads();
   // Wait for tile 0 right here (the loop's first drain is then a no-op). Waves without tiles
@@ -230,19 +215,15 @@ __global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
   // profiles/r01/ceiling.md), and tile k+1's latency still hides behind tile k's compute.
   // A full ring is stored right after the next tile's loads are issued, so the stores
   // retire during that tile's compute instead of stalling the next drain (crc_long.hip).
-  // SLOT: the same loop; the window check waits for ring room instead of storing.
-  constexpr u32 kWin = SLOT ? (u32)kSlotCheckRounds : (u32)(kRing / 2);
+  // SLOT: the same loop without the ring stores (a workgroup is one ring window).
+  constexpr u32 kWin = SLOT ? ~0u : (u32)(kRing / 2);
   u32 k = 0, kf = 0;
   for (; k + 1 < nk; k += 2) {
     drain_before_issue();
     load_tile(B, k + 1);
-    if (k - kf == kWin) {
-      if constexpr (SLOT) {
-        ring_room(k);
-      } else {
-        wave_lds_sync();
-        flush(kf, kRing / 2);
-      }
+    if (!SLOT && k - kf == kWin) {
+      wave_lds_sync();
+      flush(kf, kRing / 2);
       kf = k;
     }
     tile_result(line_crc(A), k, kf);
@@ -252,52 +233,48 @@ __global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
   }
   if constexpr (PROBE) pt[2] = __builtin_amdgcn_s_memrealtime();
   if (k < nk) {  // odd last tile, already loaded
-    if (k - kf == kWin) {
-      if constexpr (SLOT) {
-        ring_room(k);
-      } else {
-        wave_lds_sync();
-        flush(kf, kRing / 2);
-      }
+    if (!SLOT && k - kf == kWin) {
+      wave_lds_sync();
+      flush(kf, kRing / 2);
       kf = k;
     }
     tile_result(line_crc(A), k, kf);
   }
   wave_lds_sync();
+  u64 pt_finish = 0;
   if constexpr (SLOT) {
-    if (finisher) {
-      // Group g = tiles 4g .. 4g+3 of every payload wave: lane j takes tile 4g + (j >> 4) of
-      // payload wave (j >> 1) & 7, message half j & 1 -- 64 messages, one per lane.
-      static_assert(NPW == 8, "the finisher's lane map assumes 8 payload waves");
-      const u32 fw = ((u32)lane >> 1) & 7u, fr = (u32)lane >> 4, fh = (u32)lane & 1u;
+    if (wid < kSlotFinishers) {
+      if constexpr (PROBE) pt_finish = __builtin_amdgcn_s_memrealtime();
+      // Round r: message q = r * 64 * kSlotFinishers + 64 * wid + lane of the workgroup, i.e. tile
+      // q >> 4 of wave (q >> 1) & 7, half q & 1 (16 tiles per round, one message per lane).
+      static_assert(NPW == 8 && kSlotRingRounds == 2 * 16, "the finishing map assumes 8 waves, 2 rounds");
+      const u32 fw = ((u32)lane >> 1) & 7u, fh = (u32)lane & 1u;
       const u64 ft0 = front_slot(blockIdx.x, gridDim.x, fw);
       const u32 fnk = ft0 < ntiles ? ((u32)(ntiles - ft0) + (u32)nw - 1u) / (u32)nw : 0u;
       const u64 w0 = front_slot(blockIdx.x, gridDim.x, 0u);  // wave 0 has the most tiles
       const u32 nk0 = w0 < ntiles ? ((u32)(ntiles - w0) + (u32)nw - 1u) / (u32)nw : 0u;
-      const u32 ngroups = (nk0 + 3u) >> 2;
-      const u32 fring = sbase + kUniSlotRing + fw * kSlotRingBytesPerWave + 8u * fh;
       const bool calc = sa.mode == 0u;
-      auto gtile = [&](u32 g) { return 4u * g + fr; };
-      auto gmsg = [&](u32 g) { return 2 * (ft0 + (u64)gtile(g) * nw) + (u64)fh; };
-      auto gvalid = [&](u32 g) { return gtile(g) < fnk && gmsg(g) < count; };
-      u32x4 Q[4];
-      auto load_prefix = [&](u32 g) {
-        const u64 m = gvalid(g) ? gmsg(g) : 0;
+      auto ftile = [&](u32 r) { return 16u * r + 4u * (u32)wid + ((u32)lane >> 4); };
+      auto fmsg = [&](u32 r) { return 2 * (ft0 + (u64)ftile(r) * nw) + (u64)fh; };
+      auto fvalid = [&](u32 r) { return ftile(r) < fnk && fmsg(r) < count; };
+      // both rounds' prefix lines at once (64 B per lane and round)
+      u32x4 Q[2][4];
+#pragma unroll
+      for (u32 r = 0; r < 2; r++) {
+        const u64 m = fvalid(r) ? fmsg(r) : 0;
         const u32x4* q = reinterpret_cast<const u32x4*>(base + m * stride - sa.prefix_size);
 #pragma unroll
-        for (int i = 0; i < 4; i++) Q[i] = q[i];
-      };
+        for (int i = 0; i < 4; i++) Q[r][i] = SUBSPACE_SLOT_VARIANT == 13 ? u32x4{0, 0, 0, 0} : q[i];
+      }
       u32 mism = 0;
-      // group 0's prefix lines go out once wave 0's tile 0 is in its ring (the first flood
-      // has landed), not with it
-      for (u32 spins = 0; nk0 != 0u && (u32)(lds_ld64(sbase + kUniSlotRing) >> 32) != 0u && spins < kSpinBound; spins++)
-        __builtin_amdgcn_s_sleep(8);
-      if (ngroups) load_prefix(0);
-      for (u32 g = 0; g < ngroups; g++) {
-        // span-0 term of the group's messages: P = Z_4096(crc_raw(~0, prefix[4, 48)))
+      bool gave_up = false;
+#pragma unroll
+      for (u32 r = 0; r < 2; r++) {
+        if (16u * r >= nk0) break;  // wave-uniform
+        // span-0 term: P = Z_4096(crc_raw(~0, prefix[4, 48)))
         u32 w[16];
 #pragma unroll
-        for (int i = 0; i < 16; i++) w[i] = Q[i >> 2][i & 3];
+        for (int i = 0; i < 16; i++) w[i] = Q[r][i >> 2][i & 3];
         const bool has = (w[8] & 4u) != 0u;  // kMessageHasChecksum (common/channel.h:62-70)
         const u32 F = calc ? (w[8] | 4u) : w[8];
         w[8] = F;
@@ -306,34 +283,38 @@ __global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
         for (int i = 1; i < 12; i++) hh = step4(hh ^ w[i], lc0, lc1);
         const u32 P = opmul(sbase, kUniSlotOpZ4096, hh);
         const u32 S = w[12];  // the stored checksum (first 4 B of the checksum area, prefix + 48)
-        const bool valid = gvalid(g);
-        const u64 msg = gmsg(g);
-        // wait for the group's tagged payload CRCs
-        const u32 ea = fring + 16u * (gtile(g) & (u32)(kSlotRingRounds - 1));
+        const bool valid = fvalid(r);
+        const u64 msg = fmsg(r);
+        // the payload CRC, once its wave has written it (bounded: a broken invariant raises
+        // kFaultSlotRing instead of hanging the GPU, and the wave waits no more)
+        const u32 ea = sbase + kUniSlotRing + fw * kSlotRingBytesPerWave + 16u * ftile(r) + 8u * fh;
         u64 e;
         for (u32 spins = 0;; spins++) {
           e = lds_ld64(ea);
-          if (gave_up || __ballot(valid && (u32)(e >> 32) != gtile(g)) == 0) break;
-          if (spins == kSpinBound) {  // never in a correct call: report, do not hang (nor wait again)
+          if (gave_up || __ballot(valid && (u32)(e >> 32) != ftile(r)) == 0) break;
+          if (spins == kSpinBound) {
             if (lane == 0) raise_fault(sa.fault, kFaultSlotRing);
             gave_up = true;
           }
-          __builtin_amdgcn_s_sleep(8);
+          __builtin_amdgcn_s_sleep(2);
         }
-        // the entries are in registers: their ring slots may be reused
-        if (lane == 0) lds_st(sprog, 4u * g + 4u);
-        if (g + 1 < ngroups) load_prefix(g + 1);  // the front is now streaming group g+1
-        const u32 r = (u32)e ^ P;
+        const u32 res = (u32)e ^ P;
         u32* pw = reinterpret_cast<u32*>(const_cast<uint8_t*>(base) + msg * stride - sa.prefix_size);
         if (calc) {
+          if (valid && SUBSPACE_SLOT_VARIANT == 10) {
+            u32x4* p8 = reinterpret_cast<u32x4*>(pw + 8);
+            p8[0] = u32x4{F, w[9], w[10], w[11]};
+            p8[1] = u32x4{res, w[13], w[14], w[15]};
+          } else if (valid && SUBSPACE_SLOT_VARIANT != 12) {
+            pw[8] = F;     // SetHasChecksum()
+            pw[12] = res;  // *reinterpret_cast<uint32_t*>(checksum.data()) = ~crc (client/checksum.h:36)
+          }
           if (valid) {
-            pw[8] = F;   // SetHasChecksum()
-            pw[12] = r;  // *reinterpret_cast<uint32_t*>(checksum.data()) = ~crc (client/checksum.h:36)
             if (sa.status) sa.status[msg] = 0u;
-            if (sa.crc_out) sa.crc_out[msg] = r;
+            if (sa.crc_out) sa.crc_out[msg] = res;
           }
         } else {
-          const u32 st = !has ? 2u : (r == S ? 0u : 1u);  // client/checksum.h:46
+          const u32 st = !has ? 2u : (res == S ? 0u : 1u);  // client/checksum.h:46
           if (valid && sa.status) sa.status[msg] = st;
           mism += (u32)__builtin_popcountll(__ballot(valid && st == 1u));
         }
@@ -341,15 +322,21 @@ __global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
       if (sa.error_count && lane == 0) {
         if (calc) {
           // a publish has no mismatches: the count is 0 (include/subspace_crc.h)
-          if (blockIdx.x == 0) *sa.error_count = 0u;
+          if (blockIdx.x == 0 && wid == 0) *sa.error_count = 0u;
         } else {
-          // the call's mismatch count: one 64-bit atomic per workgroup adds (1 << 32) | its
-          // count; the workgroup that sees G - 1 finished before it writes the total and
-          // resets the word
-          const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(sa.counter), (1ull << 32) | (u64)mism);
-          if ((u32)(old >> 32) == gridDim.x - 1u) {
-            *sa.error_count = (u32)old + mism;
-            __hip_atomic_store(sa.counter, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // the workgroup's count: one LDS atomic per finishing wave, (1 << 24) | its count
+          // (< 2^24: at most 512 messages per workgroup); the last of them adds the total and
+          // one finished workgroup, (1 << 32) | count, to the call's word; the workgroup that
+          // sees G - 1 finished before it writes the call's total and resets the word
+          const u32 o = __hip_atomic_fetch_add(reinterpret_cast<lds_u32_t*>((uintptr_t)smism), (1u << 24) | mism,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if ((o >> 24) == (u32)kSlotFinishers - 1u) {
+            const u32 n = (o + mism) & 0xFFFFFFu;
+            const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(sa.counter), (1ull << 32) | (u64)n);
+            if ((u32)(old >> 32) == gridDim.x - 1u) {
+              *sa.error_count = (u32)old + n;
+              __hip_atomic_store(sa.counter, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
           }
         }
       }
@@ -361,12 +348,13 @@ __global__ __launch_bounds__(SLOT ? WG + 64 : WG) void crc32_uniform4k_kernel(
   // here, at the end, so the call needs no separate memset
   if (zero_word != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0u;
   if constexpr (PROBE) {
-    if (!finisher) {
+    {
       pt[3] = __builtin_amdgcn_s_memrealtime();
       u64* r = sa.probe + ((u64)blockIdx.x * wpb + (u64)wid) * kProbeWords;
       const u64 xcc = (u64)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+      const u64 hwid = (u64)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID: wave slot, SIMD, CU, SE
       const u64 v = lane == 0 ? pt[0] : lane == 1 ? pt[1] : lane == 2 ? pt[2] : lane == 3 ? pt[3]
-                  : lane == 4 ? pt_args : lane == 5 ? (xcc | ((u64)nk << 32)) : lane == 6 ? 0ull : pt_landed;
+                  : lane == 4 ? pt_args : lane == 5 ? (xcc | ((u64)nk << 32)) : lane == 6 ? (hwid | (pt_finish << 32)) : pt_landed;
       if (lane < 8) r[lane] = v;
     }
   }

@@ -85,3 +85,34 @@ def gather_ragged_crcs(local, bounds, rank: int, world: int, dist, dst: int = 0)
     if rank != dst:
         return None
     return concat_ranges([p.cpu().numpy().view(np.uint32) for p in parts], bounds)
+
+
+# ---------------------------------------------------------------- device-resident gathers
+def gather_crcs_device(local, count: int, world: int, dist):
+    """all_gather the per-rank CRC tensors (padded to equal length) and interleave them into
+    global order ON THE DEVICE (every rank gets the full int32 tensor; no host copy). At
+    world 1 it is one device copy of the local results."""
+    import torch
+    per = (count + world - 1) // world
+    buf = torch.zeros(per, dtype=torch.int32, device=local.device)
+    buf[:min(local.numel(), per)] = local[:per]
+    if world == 1:
+        return buf[:count].clone()
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    # parts[r][j] is global message r + j*world: the (world, per) stack read column-major
+    return torch.stack(parts).t().contiguous().view(-1)[:count]
+
+
+def gather_ragged_crcs_device(local, bounds, world: int, dist):
+    """all_gather of a contiguous (ragged) split, padded to the largest shard, concatenated in
+    rank order on the device (every rank gets the full int32 tensor)."""
+    import torch
+    per = int(max(bounds[r + 1] - bounds[r] for r in range(world)))
+    buf = torch.zeros(max(per, 1), dtype=torch.int32, device=local.device)
+    buf[:local.numel()] = local
+    if world == 1:
+        return buf[:int(bounds[1])].clone()
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    return torch.cat([parts[r][:int(bounds[r + 1] - bounds[r])] for r in range(world)])

@@ -40,6 +40,11 @@ def test_dry_run_spawns_ranks_and_matches_fixture(world, workload):
     assert line["bitexact_vs_golden"] is True
     assert line["scaling"] == "strong"
     assert line["value"] > 0 and line["per_gpu_value"] == pytest.approx(line["value"] / world, rel=1e-2)
+    # the line is self-checking: the process group's size, the backend and one record per rank
+    assert line["rccl_world"] == world and line["backend"] == "gloo"
+    assert sorted(r["rank"] for r in line["ranks"]) == list(range(world))
+    assert len({r["pid"] for r in line["ranks"]}) == world  # N distinct rank processes
+    assert line["rank_step_ms"]["min"] <= line["rank_step_ms"]["max"]
 
 
 def test_dry_run_single_rank_default_workload():

@@ -30,7 +30,15 @@ def test_two_ranks_on_one_gpu(workload):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["single_gpu"]["bitexact_vs_golden"] is True
+    # self-checking fields: the process group's size and backend, one record per rank
+    assert d["rccl_world"] == 2 and d["backend"] == "gloo"
+    assert sorted(r["rank"] for r in d["ranks"]) == [0, 1]
+    assert d["distinct_gpus"] == 1  # both ranks rehearse on cuda:0 (a real N-GPU run shows N)
+    assert d["rank_step_ms"]["min"] <= d["rank_step_ms"]["max"]
     if workload == "E":
         assert d["bitexact_vs_golden"] is True and d["scaling"] == "strong"
-        assert d["config"]["gather_ms"] is not None
+        g = d["config"]["gather"]
+        # the gather is timed on the device (HIP events around the collective + on-device
+        # interleave); the D2H copy and host check are reported apart
+        assert g["gather_ms"] > 0 and g["d2h_check_ms"] > 0 and g["gather_bytes"] == 8 * 2**20 * 4
     assert d["efficiency"] > 0 and d["per_gpu_value"] == pytest.approx(d["value"] / 2, rel=1e-2)

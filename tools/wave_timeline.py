@@ -13,6 +13,7 @@ launch's last exit and the next launch's first entry. Clock: s_memrealtime, 100 
 import argparse
 import ctypes
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -91,11 +92,12 @@ def main():
     launch(bufs[0], out)
     lib.subspace_crc_testutil_probe(ctx._h, None)
     torch.cuda.synchronize()
-    if a.mode != "publish":
+    check = not os.environ.get("SLOT_GAP_NOCHECK")  # (timing-only builds compute nothing valid)
+    if a.mode != "publish" and check:
         assert torch.equal(out, ref), "PROBE instantiation results differ"
     if a.mode in ("uniform", "uniform4160"):
         lib.subspace_crc_testutil_probe(ctx._h, None)
-    assert int(errs.item()) == 0
+    assert int(errs.item()) == 0 or not check
     r = rec.cpu().numpy()[1:]  # launch 0 was overwritten by the check above
     if a.out:
         np.savez_compressed(a.out, rec=r)
@@ -110,8 +112,6 @@ def main():
             "entry_p50": pct(t[:, 0], 50), "entry_max": pct(t[:, 0], 100),
             "fill_p50": pct(t[:, 1] - t[:, 0], 50), "fill_max": pct(t[:, 1] - t[:, 0], 100),
             "issued_p50": pct(r[i, :, 4] * TICK_US - base, 50), "issued_max": pct(r[i, :, 4] * TICK_US - base, 100),
-            "slot_flush_p50": pct(r[i, :, 6] * TICK_US - base, 50) if r[i, :, 6].all() else None,
-            "slot_flush_max": pct(r[i, :, 6] * TICK_US - base, 100) if r[i, :, 6].all() else None,
             "tile0_landed_p50": pct(r[i, :, 7] * TICK_US - base, 50),
             "tile0_landed_max": pct(r[i, :, 7] * TICK_US - base, 100),
             "loop_end_p50": pct(t[:, 2], 50), "loop_end_max": pct(t[:, 2], 100),
@@ -138,6 +138,13 @@ def main():
     for name, col in (("entry", 0), ("issued", 4), ("tile0_landed", 7), ("exit", 3)):
         tt = np.stack([(r[i, :, col].astype(np.float64) - r[i, :, 0].min()) * TICK_US for i in range(r.shape[0])])
         med[f"{name}_by_wave_in_wg"] = [round(float(np.median(tt[:, wid == w])), 2) for w in range(8)]
+    # placement of wave w of a workgroup (HW_ID of launch 1): SIMD and wave slot, as counts
+    hw = r[0, :, 6].astype(np.int64)
+    simd, slot = (hw >> 4) & 3, hw & 15
+    med["simd_by_wave_in_wg"] = [dict(zip(*[x.tolist() for x in np.unique(simd[wid == w], return_counts=True)]))
+                                 for w in range(8)]
+    med["slot_by_wave_in_wg"] = [dict(zip(*[x.tolist() for x in np.unique(slot[wid == w], return_counts=True)]))
+                                 for w in range(8)]
     med["event_span_us_per_launch"] = round(span_ms * 1e3, 2)
     med["waves"] = waves
     med["tiles_per_wave"] = sorted(set(int(x) >> 32 for x in r[0, :, 5]))
