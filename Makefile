@@ -48,41 +48,53 @@ test-cpu: all
 	python -m pytest tests/ -x -q -m "not gpu"
 
 # ---- AddressSanitizer + UBSan build of the host code (CPU only; GPU sanitizers are not
-# available on the pool). The g++-compiled host sources (host CRC, split allocator) are
-# instrumented; the HIP objects are linked in unchanged (their host side is the C-ABI
-# argument checking, exercised through the same tests). Everything links against gcc's
-# runtime: python runs with it preloaded, ASan's leak checker off (CPython's own
+# available on the pool): the host sources (host CRC, split allocator) AND capi.hip's host
+# side (-Xarch_host: argument validation, workspace sizing, the chunked host-slot pipeline,
+# the host-address -> device-alias translation, the call scope and stream ordering) are
+# instrumented, all with ROCm's clang so one ASan runtime (clang's, shared) serves
+# everything; the other HIP objects (kernel launch stubs only) are linked in unchanged.
+# python runs with that runtime preloaded, ASan's leak checker off (CPython's own
 # allocations), every UBSan finding fatal.
 ASAN_DIR := build/asan
-ASAN_FLAGS := -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=all -g -O1
+ASAN_CXX := /opt/rocm/llvm/bin/clang++
+ASAN_CC := /opt/rocm/llvm/bin/clang
+ASAN_FLAGS := -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=all -g -O1 -shared-libsan
+ASAN_RT := $(shell $(ASAN_CXX) -print-file-name=libclang_rt.asan-x86_64.so)
 ASAN_LIB := $(ASAN_DIR)/libsubspace_crc.so
-ASAN_HOST_OBJS := $(patsubst $(CSRC)/%.cpp,$(ASAN_DIR)/%.o,$(CPP_SRCS))
+ASAN_HOST_OBJS := $(patsubst $(CSRC)/%.cpp,$(ASAN_DIR)/%.o,$(CPP_SRCS)) $(ASAN_DIR)/capi.o
 HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
+ASAN_HIP_OBJS := $(filter-out $(OBJDIR)/capi.o,$(HIP_OBJS))
 
 $(ASAN_DIR)/%.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p $(ASAN_DIR)
-	g++ -std=c++17 -fPIC -Wall $(ASAN_FLAGS) -c $< -o $@
+	$(ASAN_CXX) -std=c++17 -fPIC -Wall $(ASAN_FLAGS) -c $< -o $@
 
-$(ASAN_LIB): $(ASAN_HOST_OBJS) $(HIP_OBJS)
-	g++ -shared -fPIC $(ASAN_FLAGS) -o $@ $(ASAN_HOST_OBJS) $(HIP_OBJS) -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+$(ASAN_DIR)/capi.o: $(CSRC)/capi.hip $(HDRS)
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) $(HIPFLAGS) -g -Xarch_host -fsanitize=address,undefined -Xarch_host -fno-sanitize-recover=all \
+	    -Xarch_host -fno-omit-frame-pointer -c $< -o $@
+
+$(ASAN_LIB): $(ASAN_HOST_OBJS) $(ASAN_HIP_OBJS)
+	$(ASAN_CXX) -shared -fPIC $(ASAN_FLAGS) -o $@ $(ASAN_HOST_OBJS) $(ASAN_HIP_OBJS) -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,/opt/rocm/lib
 
 $(ASAN_DIR)/config_a: tools/config_a.cpp include/subspace/checksum.h $(ASAN_LIB)
-	g++ -std=c++17 $(ASAN_FLAGS) -Iinclude -o $@ tools/config_a.cpp -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN' -ldl
+	$(ASAN_CXX) -std=c++17 $(ASAN_FLAGS) -Iinclude -o $@ tools/config_a.cpp -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN' -ldl
 
 $(ASAN_DIR)/drain_demo: tools/drain_demo.cpp include/subspace/checksum.h include/subspace/checksum_batch.h include/subspace_crc.h $(ASAN_LIB)
-	g++ -std=c++17 -Wall $(ASAN_FLAGS) -Iinclude -o $@ tools/drain_demo.cpp -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN'
+	$(ASAN_CXX) -std=c++17 -Wall $(ASAN_FLAGS) -Iinclude -o $@ tools/drain_demo.cpp -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN'
 
 $(ASAN_DIR)/batch_gates: tests/c/batch_gates.cpp include/subspace/checksum.h include/subspace/checksum_batch.h include/subspace_crc.h $(ASAN_LIB)
-	g++ -std=c++17 -Wall $(ASAN_FLAGS) -Iinclude -o $@ tests/c/batch_gates.cpp -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN'
+	$(ASAN_CXX) -std=c++17 -Wall $(ASAN_FLAGS) -Iinclude -o $@ tests/c/batch_gates.cpp -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN'
 
 $(ASAN_DIR)/c_binding: tests/c/c_binding.c include/subspace_crc.h $(ASAN_LIB)
-	gcc -std=c11 -Wall -Wextra $(ASAN_FLAGS) -Iinclude -o $@ tests/c/c_binding.c -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN'
+	$(ASAN_CC) -std=c11 -Wall -Wextra $(ASAN_FLAGS) -Iinclude -o $@ tests/c/c_binding.c -L$(ASAN_DIR) -lsubspace_crc -Wl,-rpath,'$$ORIGIN'
 
 asan: $(ASAN_LIB) $(ASAN_DIR)/config_a $(ASAN_DIR)/drain_demo $(ASAN_DIR)/c_binding $(ASAN_DIR)/batch_gates
 
 asan-test: asan oracle
 	ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
-	LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $$(gcc -print-file-name=libubsan.so)" \
+	LD_PRELOAD="$(ASAN_RT)" \
 	SUBSPACE_CRC_PROBE_LIB=$(CURDIR)/$(ASAN_LIB) SUBSPACE_CRC_ASAN_DIR=$(CURDIR)/$(ASAN_DIR) \
 	python -m pytest tests/test_host_api.py tests/test_capi.py tests/test_split_alloc.py tests/test_c_binding.py tests/test_batch_gates.py -q -m "not gpu" -p no:cacheprovider
 

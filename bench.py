@@ -619,6 +619,58 @@ def slot_configs(ctx, dev, iters) -> dict:
                         ("publish: flag + checksum stored" if mode == gpu.SLOT_CALCULATE else
                          "verify: per-slot status + mismatch count"),
             "check": "verify passes all slots and 64 sampled stored checksums equal the host drop-in's"})
+    # S_list: the same channel drained as a device slot list in shuffled order (a subscriber's
+    # read order over several wrap-arounds): subspace_crc32_slots, verify
+    order = rng.permutation(n).astype(np.uint64)
+    base0 = np.uint64(bufs[0].data_ptr())
+    recs = np.stack([base0 + order * np.uint64(stride), base0 + order * np.uint64(stride) + np.uint64(ps),
+                     np.full(n, size, dtype=np.uint64)], axis=1)
+    d_recs = torch.from_numpy(np.ascontiguousarray(recs).view(np.int64)).to(dev)
+    errs.zero_()
+    ms = time_calls(lambda: ctx.crc32_slots(d_recs, max_message_size=size, checksum_size=cs, metadata_size=ms_,
+                                            mode=gpu.SLOT_VERIFY, status=status, error_count=errs), 50)
+    torch.cuda.synchronize()
+    ok = int(errs.item()) == 0 and bool((status == 0).all().item())
+    res["S_list_verify"] = config_line(nbytes, ms, ok, "subspace_crc32_slots (ragged kernel + slot finish)", {
+        "workload": "S_list: config S's 65,536 slots as a device slot list (subspace_crc_slot records) in "
+                    "shuffled order, verify",
+        "check": "every slot passes"})
+    del bufs, d_recs
+    torch.cuda.empty_cache()
+    # S_meta: 16 B of user metadata per slot (SetMetadataSize, client/options.h:375-391):
+    # ComputePrefixSize(4, 16) = 128, stride 4,224; spans 44 + 16 + 4,096 B
+    cs, ms_ = 4, 16
+    ps, stride = slots.compute_prefix_size(cs, ms_), slots.slot_stride(size, cs, ms_)
+    host = rng.integers(0, 256, stride * n, dtype=np.uint8)
+    host.reshape(n, stride)[:, :ps] = slots.make_prefixes(n, np.full(n, size, dtype=np.uint64), checksum_size=cs,
+                                                          metadata_size=ms_, seed=6)
+    bufs = [torch.from_numpy(host).to(dev) for _ in range(nbuf)]
+    nbytes = n * (size + 44 + ms_)
+    for mode, key in ((gpu.SLOT_CALCULATE, "S_meta_publish"), (gpu.SLOT_VERIFY, "S_meta_verify")):
+        i = [0]
+
+        def call():
+            b = bufs[i[0] % nbuf]
+            i[0] += 1
+            ctx.crc32_slots_strided(b, stride, n, message_size=size, checksum_size=cs, metadata_size=ms_, mode=mode,
+                                    status=status if mode == gpu.SLOT_VERIFY else None,
+                                    error_count=errs if mode == gpu.SLOT_VERIFY else None)
+        errs.zero_()
+        ms = time_calls(call, 200)
+        ok = None
+        if mode == gpu.SLOT_VERIFY:
+            torch.cuda.synchronize()
+            ok = int(errs.item()) == 0 and bool((status == 0).all().item())
+            chan = bufs[0].cpu().numpy()
+            for k in rng.choice(n, 64, replace=False):
+                pre = chan[k * stride:k * stride + ps]
+                pay = chan[k * stride + ps:k * stride + ps + size]
+                want = checksum.calculate_crc32_checksum(checksum.get_message_checksum_data(pre, pay, size, cs, ms_))
+                ok = ok and bytes(pre[48:52]) == want
+        res[key] = config_line(nbytes, ms, ok, "subspace_crc32_slots_strided", {
+            "workload": "S_meta: 65,536 slots (prefix 128 B with 16 B metadata + 4 KiB payload, stride 4,224), "
+                        "3-span checksum, " + ("publish" if mode == gpu.SLOT_CALCULATE else "verify"),
+            "check": "verify passes all slots and 64 sampled stored checksums equal the host drop-in's"})
     del bufs
     return res
 

@@ -19,14 +19,17 @@ M32 = 0xFFFFFFFF
 # `make asan-test` sets this: the compiled programs below are then AddressSanitizer + UBSan
 # builds linked against the sanitized library (Makefile "asan")
 ASAN_DIR = os.environ.get("SUBSPACE_CRC_ASAN_DIR")
-ASAN_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all", "-g"]
+ASAN_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all", "-g",
+              "-shared-libsan"]
+# the ASan build (Makefile asan-test) is ROCm's clang throughout: one sanitizer runtime
+CXX = "/opt/rocm/llvm/bin/clang++" if ASAN_DIR else "g++"
 
 
 def cxx_build(src, exe, *extra):
     """Compile and link a test program against the library (the sanitized one under asan)."""
     libdir = Path(ASAN_DIR) if ASAN_DIR else ROOT / "subspace_amd"
     flags = ASAN_FLAGS if ASAN_DIR else []
-    subprocess.run(["g++", "-std=c++17", "-O1", *flags, *extra, f"-I{ROOT / 'include'}", str(src), "-o", str(exe),
+    subprocess.run([CXX, "-std=c++17", "-O1", *flags, *extra, f"-I{ROOT / 'include'}", str(src), "-o", str(exe),
                     f"-L{libdir}", "-lsubspace_crc", f"-Wl,-rpath,{libdir}"], check=True)
 
 

@@ -1,0 +1,39 @@
+#!/bin/bash
+# Interleaved A/B of library builds on one GPU box, one process per run, after one discarded
+# warm-up process (a fresh box's first GPU process runs slower: DESIGN.md 4.0).
+#   bash tools/ab_session.sh <tag> <mode> <lib>...
+#   lib:  0 = the product library; N = tools/ubench/probes/libslotN.so
+#         (tools/ubench/build_variants.sh); anything else = a path (e.g. abtmp/lib_x.so from
+#         tools/ab_lib.sh). Repeat libs for an A B A B order.
+#   mode: slotgap -- tools/slot_gap.py: config S publish / verify vs the plain kernel over the
+#                    same buffers (timing only: variants may compute nothing valid)
+#         uniform -- tools/sweep_uniform.py: config B through the uniform kernel
+# Summaries: python tools/show_ab.py gpurun_out/<tag>
+set -u
+TAG=$1; MODE=$2; shift 2
+OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/$TAG
+mkdir -p $OUT
+run() {  # $1 = output stem, $2 = library path or ""
+  if [ "$MODE" = slotgap ]; then
+    SUBSPACE_CRC_PROBE_LIB=$2 SLOT_GAP_NOCHECK=1 timeout -k 10 200 python tools/slot_gap.py 3 > $OUT/$1.jsonl 2> $OUT/$1.err
+  else
+    SUBSPACE_CRC_PROBE_LIB=$2 timeout -k 10 200 python tools/sweep_uniform.py 65536 512 7 0 > $OUT/$1.jsonl 2> $OUT/$1.err
+  fi
+}
+run warm "" || exit $?
+i=0
+for v in "$@"; do
+  i=$((i + 1))
+  lib=""
+  if [ "$v" != 0 ]; then
+    case $v in
+      *[!0-9]*) lib=$v ;;
+      *) lib=$PWD/tools/ubench/probes/libslot$v.so ;;
+    esac
+  fi
+  run "run${i}_$(basename ${v%.so})" "$lib"
+  rc=$?
+  echo "run$i $v rc=$rc" >> $OUT/status.txt
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
+echo done >> $OUT/status.txt
