@@ -44,9 +44,8 @@
 #include "crc_device.h"
 
 // Timing-only investigation builds of the slot finishing (tools/ubench/build_variants.sh
-// passes -DSUBSPACE_SLOT_VARIANT=n; the product build is 0): 10 publish stores whole 32-B
-// sectors (prefix words 8-15); 12 no prefix stores; 13 no prefix loads (zeros); 16 publish
-// stores the whole 64-B prefix line; 17 nontemporal flag + checksum stores.
+// passes -DSUBSPACE_SLOT_VARIANT=n; the product build is 0): 12 no prefix stores; 13 no prefix
+// loads (zeros). The other variants measured in round 3 are in DESIGN.md 4.4.
 #ifndef SUBSPACE_SLOT_VARIANT
 #define SUBSPACE_SLOT_VARIANT 0
 #endif
@@ -302,20 +301,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
         const u32 res = (u32)e ^ P;
         u32* pw = reinterpret_cast<u32*>(const_cast<uint8_t*>(base) + msg * stride - sa.prefix_size);
         if (calc) {
-          if (valid && SUBSPACE_SLOT_VARIANT == 10) {
-            u32x4* p8 = reinterpret_cast<u32x4*>(pw + 8);
-            p8[0] = u32x4{F, w[9], w[10], w[11]};
-            p8[1] = u32x4{res, w[13], w[14], w[15]};
-          } else if (valid && SUBSPACE_SLOT_VARIANT == 16) {
-            u32x4* p0 = reinterpret_cast<u32x4*>(pw);
-            p0[0] = Q[r][0];
-            p0[1] = Q[r][1];
-            p0[2] = u32x4{F, w[9], w[10], w[11]};
-            p0[3] = u32x4{res, w[13], w[14], w[15]};
-          } else if (valid && SUBSPACE_SLOT_VARIANT == 17) {
-            __builtin_nontemporal_store(F, pw + 8);
-            __builtin_nontemporal_store(res, pw + 12);
-          } else if (valid && SUBSPACE_SLOT_VARIANT != 12) {
+          if (valid && SUBSPACE_SLOT_VARIANT != 12) {
             pw[8] = F;     // SetHasChecksum()
             pw[12] = res;  // *reinterpret_cast<uint32_t*>(checksum.data()) = ~crc (client/checksum.h:36)
           }
