@@ -267,3 +267,86 @@ def test_desc_window_search_matches_binary_search(seed):
         assert sorted(got) == list(range(min(total, capacity)))
         for tau, m in got.items():
             assert tb[m] <= tau < tb[m + 1], (capacity, tau, m)
+
+
+# ------------------------------------------------------------------ fused slot kernel
+def slot_grid(count, num_cus=256):
+    """capi.hip slots_strided_impl: 8-wave workgroups, one per CU up to the tile count, and
+    more workgroups when a wave would get more than kSlotRingRounds (32) tiles."""
+    tiles = (count + 1) // 2
+    return max(max(1, min(num_cus, (tiles + 7) // 8)), (tiles + 8 * 32 - 1) // (8 * 32))
+
+
+def slot_kernel_accesses(count, stride, prefix_size, num_cus=256):
+    """Every access of crc32_uniform4k_kernel<512, true, false> (crc_uniform.hip, SLOT) as
+    byte offsets from the first prefix (the channel buffer): payload tile loads (16 B each),
+    the finishing waves' prefix loads (16 B each, both rounds, issued unconditionally), their
+    flag/checksum stores (prefix words 8 and 12) and the LDS ring entries they read. Returns
+    (loads, stores_by_message, ring_reads, max tiles per wave)."""
+    G = slot_grid(count, num_cus)
+    ntiles = (count + 1) // 2
+    nw = 8 * G
+    lane = np.arange(64)
+    loads, stores, ring = [], {}, []
+    max_nk = 0
+    nk_of = lambda t0: (ntiles - t0 + nw - 1) // nw if t0 < ntiles else 0  # noqa: E731
+    for b in range(G):
+        for wid in range(8):
+            t0 = front_slot(b, G, wid)
+            nk = nk_of(t0)
+            max_nk = max(max_nk, nk)
+            for k in range(nk + 1):  # the prologue's tile 0 and every prefetch, clamped
+                kk = k if k < nk else (nk - 1 if nk else 0)
+                for h in (0, 1):
+                    msg = 2 * (t0 + kk * nw) + h if nk else 0
+                    msg = msg if msg < count else msg - 1
+                    base = prefix_size + msg * stride
+                    loads.append(base + (lane[:32, None] * 128 + 16 * np.arange(8)[None, :]).ravel())
+            if wid >= 4:
+                continue
+            fw, fh = (lane >> 1) & 7, lane & 1
+            ft0 = np.array([front_slot(b, G, int(w)) for w in fw])
+            fnk = np.array([nk_of(int(t)) for t in ft0])
+            nk0 = nk_of(front_slot(b, G, 0))
+            for r in (0, 1):
+                ftile = 16 * r + 4 * wid + (lane >> 4)
+                fmsg = 2 * (ft0 + ftile * nw) + fh
+                valid = (ftile < fnk) & (fmsg < count)
+                m = np.where(valid, fmsg, 0)
+                loads.append((m * stride)[:, None] + 16 * np.arange(4)[None, :])  # prefix line, 4 x 16 B
+                if 16 * r >= nk0:
+                    continue
+                ring.append(fw * 512 + 16 * ftile + 8 * fh)
+                for msg in fmsg[valid]:
+                    stores[int(msg)] = stores.get(int(msg), 0) + 1
+    return np.concatenate([x.ravel() for x in loads]), stores, np.concatenate(ring) if ring else np.zeros(0), max_nk
+
+
+@pytest.mark.parametrize("count,stride,prefix", [(1, 4160, 64), (2, 4160, 64), (3, 4160, 64), (63, 4160, 64),
+                                                 (4097, 4160, 64), (65536, 4160, 64), (65537, 4160, 64),
+                                                 (140001, 4160, 64), (300001, 4160, 64), (5003, 8256, 64),
+                                                 (5003, 8320, 128)])
+def test_slot_kernel_accesses_stay_in_the_channel(count, stride, prefix):
+    """Every vector load of the fused slot kernel is 16-B aligned (the buffer and stride are)
+    and lies inside the channel buffer [0, count * stride); every slot's flag and checksum are
+    stored exactly once, by one finishing wave; no wave has more tiles than its ring holds, and
+    every ring entry read lies in the 4 KiB ring area. (the product kernel
+    issues no load outside the buffer and no b128 load at a 4-B-aligned address.)"""
+    loads, stores, ring, max_nk = slot_kernel_accesses(count, stride, prefix)
+    assert (loads % 16 == 0).all()
+    assert loads.min() >= 0 and loads.max() + 16 <= count * stride
+    assert sorted(stores) == list(range(count)) and set(stores.values()) == {1}
+    assert max_nk <= 32
+    assert ring.size == 0 or (ring.min() >= 0 and ring.max() + 8 <= 8 * 512)
+
+
+def test_r02s3i_prefix_variant_was_in_bounds():
+    """The round-2 variant that faulted (r02s3i: three dwordx4 prefix loads per window at
+    prefix + 4, + 20, + 36) read inside each slot: its addresses were in bounds, so the fault
+    was not an out-of-range address -- the property it alone had is the 4-B-aligned b128 load
+    (DESIGN.md 4.4). Every product b128 load is 16-B aligned (test above)."""
+    stride, prefix = 4160, 64
+    for msg in (0, 1, 65535):
+        addrs = [msg * stride + off for off in (4, 20, 36)]
+        assert all(a % 16 == 4 for a in addrs)
+        assert all(msg * stride <= a and a + 16 <= msg * stride + prefix for a in addrs)
