@@ -19,6 +19,7 @@ namespace subspace_amd {
 template <int WG, bool SLOT, bool PROBE>
 __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int, u32*,
                                        SlotArgs);
+__global__ void crc32_uniform4k_dyn_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, u32*);
 
 struct TileDesc;
 __global__ void crc32_ragged_count_scan_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
@@ -529,6 +530,9 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_slot_lds_bytes(8));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_dyn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)uniform_dyn_lds_bytes(8));
   if (e == hipSuccess) e = hipMalloc(&c->d_slot_counter, kSlotCounters * sizeof(u64));
   if (e == hipSuccess) e = hipMemset(c->d_slot_counter, 0, kSlotCounters * sizeof(u64));
   if (e == hipSuccess) e = hipMalloc(&c->d_fault, 4 * sizeof(u32));
@@ -662,6 +666,13 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
       HIP_TRY(hipGetLastError());
       return SUBSPACE_CRC_OK;
     }
+    if (ord == 4) {  // experiment: order 0's tiles handed out by an LDS ticket per workgroup (512 threads)
+      crc32_uniform4k_dyn_kernel<<<grid_for(c, tiles, 8), 512, uniform_dyn_lds_bytes(8), st>>>(
+          b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, c->zero_word);
+      c->zero_word = nullptr;
+      HIP_TRY(hipGetLastError());
+      return SUBSPACE_CRC_OK;
+    }
 #define LAUNCH(WGV)                                                                                           \
   crc32_uniform4k_kernel<WGV, false, false><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(                             \
       b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, SlotArgs{})
@@ -783,7 +794,7 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
   auto* buf = static_cast<uint8_t*>(dev_buffer);
   // Fused path (crc_uniform.hip SLOT): 4 KiB payloads, 16-B aligned, no metadata span -- the
   // payload CRC, the span-0 term and the flag/checksum store or status in one kernel
-  if (!dev_message_sizes && message_size == 4096 && metadata_size == 0 && slot_stride % 16 == 0 &&
+  if (!dev_message_sizes && message_size == 4096 && (u32)metadata_size <= kSlotFusedMaxMeta && slot_stride % 16 == 0 &&
       ((uintptr_t)(buf + prefix_size) % 16) == 0 && c->fused_slots) {
     // 8 waves per workgroup, tile order 0 (the finishing waves replay it), and at most
     // kSlotRingRounds tiles per wave (a workgroup is one ring window): more workgroups than
@@ -791,7 +802,8 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
     const u64 tiles = (count + 1) / 2;
     const u64 blocks = std::max<u64>(grid_for(c, tiles, 512 / 64), ceil_div(tiles, 8ull * kSlotRingRounds));
     SlotArgs sa{prefix_size, mode, dev_status, dev_crc_out, dev_error_count,
-                c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters), c->probe, c->d_fault};
+                c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters), c->probe, c->d_fault,
+                (u32)checksum_size, (u32)metadata_size};
     if (c->probe)  // experiment hook: the timestamp-recording instantiation
       crc32_uniform4k_kernel<512, true, true><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
           buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, 0, nullptr, sa);
@@ -1133,7 +1145,7 @@ uint64_t subspace_crc_testutil_probe_waves(subspace_crc_ctx* c, uint64_t count) 
 int subspace_crc_testutil_tune(subspace_crc_ctx* c, int uniform_wg, int uniform_blocks, int uniform_order) {
   if (!c) return SUBSPACE_CRC_EINVAL;
   if (uniform_wg != 256 && uniform_wg != 512 && uniform_wg != 768 && uniform_wg != 1024) return SUBSPACE_CRC_EINVAL;
-  if (uniform_order < 0 || uniform_order > 3) return SUBSPACE_CRC_EINVAL;
+  if (uniform_order < 0 || uniform_order > 4) return SUBSPACE_CRC_EINVAL;
   c->uniform_wg = uniform_wg;
   c->uniform_blocks = uniform_blocks;
   c->uniform_order = uniform_order;

@@ -42,8 +42,11 @@ def publish_strided(ctx, host, stride, count, cs, ms, sizes=None, message_size=0
     return dev, status.cpu().numpy()
 
 
-@pytest.mark.parametrize("cs,ms", [(4, 0), (4, 16), (20, 32), (8, 5)])
+@pytest.mark.parametrize("cs,ms", [(4, 0), (4, 16), (20, 32), (8, 5), (5, 7), (6, 64), (7, 61), (4, 65), (30, 1)])
 def test_publish_uniform_4k(gpu_ctx, oracle, cs, ms):
+    """Contiguous 4 KiB slots, publish byte-identical to the oracle. metadata_size <= 64 goes
+    through the fused slot kernel (span 1 folded in by the finishing waves, at every byte
+    alignment of 48 + checksum_size); 65 through the payload kernel + slot finish kernel."""
     count = 1500
     sizes = np.full(count, 4096, dtype=np.uint64)
     host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=cs * 100 + ms)
@@ -459,3 +462,28 @@ def test_calculate_zeroes_error_count(gpu_ctx, fused):
     finally:
         lib.subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", 1)
     assert int(err.item()) == 0
+
+
+@pytest.mark.parametrize("cs,ms", [(4, 16), (5, 7), (6, 64), (4, 65)])
+def test_verify_metadata_channels(gpu_ctx, oracle, cs, ms):
+    """Verify statuses and the mismatch count of channels with user metadata equal the oracle's
+    after corruptions (metadata bytes included), fused (ms <= 64) and two-kernel (65) alike."""
+    count = 3001
+    sizes = np.full(count, 4096, dtype=np.uint64)
+    host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=cs * 1000 + ms)
+    po, yo = offsets(count, stride, ps)
+    oracle.publish_slots(host, po, yo, sizes, cs, ms)
+    rng = np.random.default_rng(ms)
+    for i in rng.choice(count, 40, replace=False):  # metadata, span 0 and payload bytes
+        k = int(rng.integers(0, 3))
+        at = [48 + cs + int(rng.integers(0, ms)), 4 + int(rng.integers(0, 44)), ps + int(rng.integers(0, 4096))][k]
+        host[int(po[i]) + at] ^= 0x10
+    want = oracle.verify_slots(host, po, yo, sizes, cs, ms)
+    dev = torch.from_numpy(host).to(DEV)
+    st = torch.full((count,), 7, dtype=torch.int32, device=DEV)
+    err = torch.full((1,), 12345, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_slots_strided(dev, stride, count, message_size=4096, checksum_size=cs, metadata_size=ms,
+                                mode=gpu.SLOT_VERIFY, status=st, error_count=err)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy().view(np.uint32), want)
+    assert int(err.item()) == int((want == 1).sum()) > 0

@@ -277,12 +277,14 @@ def slot_grid(count, num_cus=256):
     return max(max(1, min(num_cus, (tiles + 7) // 8)), (tiles + 8 * 32 - 1) // (8 * 32))
 
 
-def slot_kernel_accesses(count, stride, prefix_size, num_cus=256):
+def slot_kernel_accesses(count, stride, prefix_size, num_cus=256, cs=4, ms=0):
     """Every access of crc32_uniform4k_kernel<512, true, false> (crc_uniform.hip, SLOT) as
     byte offsets from the first prefix (the channel buffer): payload tile loads (16 B each),
     the finishing waves' prefix loads (16 B each, both rounds, issued unconditionally), their
     flag/checksum stores (prefix words 8 and 12) and the LDS ring entries they read. Returns
-    (loads, stores_by_message, ring_reads, max tiles per wave)."""
+    (loads, stores_by_message, ring_reads, max tiles per wave). With metadata (ms > 0) the
+    finishing waves also read span 1 as dwords: the one holding byte 48 + cs and the next
+    (sh + ms + 3) / 4 - 1, each index clamped to the last (18 loads, crc_uniform.hip)."""
     G = slot_grid(count, num_cus)
     ntiles = (count + 1) // 2
     nw = 8 * G
@@ -314,6 +316,14 @@ def slot_kernel_accesses(count, stride, prefix_size, num_cus=256):
                 valid = (ftile < fnk) & (fmsg < count)
                 m = np.where(valid, fmsg, 0)
                 loads.append((m * stride)[:, None] + 16 * np.arange(4)[None, :])  # prefix line, 4 x 16 B
+                if ms and 16 * r < nk0:
+                    o1 = 48 + cs
+                    nwords = ((o1 & 3) + ms + 3) >> 2
+                    j = np.minimum(np.arange(18), nwords - 1)
+                    span1 = (m * stride)[:, None] + (o1 & ~3) + 4 * j[None, :]
+                    assert (span1 % 4 == 0).all()
+                    # dword loads: 4 B each, model them as 16-B-aligned blocks for the range check
+                    loads.append(span1 & ~15)
                 if 16 * r >= nk0:
                     continue
                 ring.append(fw * 512 + 16 * ftile + 8 * fh)
@@ -322,17 +332,19 @@ def slot_kernel_accesses(count, stride, prefix_size, num_cus=256):
     return np.concatenate([x.ravel() for x in loads]), stores, np.concatenate(ring) if ring else np.zeros(0), max_nk
 
 
-@pytest.mark.parametrize("count,stride,prefix", [(1, 4160, 64), (2, 4160, 64), (3, 4160, 64), (63, 4160, 64),
-                                                 (4097, 4160, 64), (65536, 4160, 64), (65537, 4160, 64),
-                                                 (140001, 4160, 64), (300001, 4160, 64), (5003, 8256, 64),
-                                                 (5003, 8320, 128)])
-def test_slot_kernel_accesses_stay_in_the_channel(count, stride, prefix):
+@pytest.mark.parametrize("count,stride,prefix,cs,ms", [
+    (1, 4160, 64, 4, 0), (2, 4160, 64, 4, 0), (3, 4160, 64, 4, 0), (63, 4160, 64, 4, 0), (4097, 4160, 64, 4, 0),
+    (65536, 4160, 64, 4, 0), (65537, 4160, 64, 4, 0), (140001, 4160, 64, 4, 0), (300001, 4160, 64, 4, 0),
+    (5003, 8256, 64, 4, 0), (5003, 8320, 128, 20, 0), (3001, 4224, 128, 4, 16), (3001, 4160, 64, 5, 7),
+    (3001, 4224, 128, 6, 64), (3001, 4224, 128, 7, 61), (1, 4224, 128, 4, 16)])
+def test_slot_kernel_accesses_stay_in_the_channel(count, stride, prefix, cs, ms):
     """Every vector load of the fused slot kernel is 16-B aligned (the buffer and stride are)
     and lies inside the channel buffer [0, count * stride); every slot's flag and checksum are
     stored exactly once, by one finishing wave; no wave has more tiles than its ring holds, and
     every ring entry read lies in the 4 KiB ring area. (the product kernel
     issues no load outside the buffer and no b128 load at a 4-B-aligned address.)"""
-    loads, stores, ring, max_nk = slot_kernel_accesses(count, stride, prefix)
+    assert prefix == ((48 + cs + ms + 63) & ~63)  # ComputePrefixSize
+    loads, stores, ring, max_nk = slot_kernel_accesses(count, stride, prefix, cs=cs, ms=ms)
     assert (loads % 16 == 0).all()
     assert loads.min() >= 0 and loads.max() + 16 <= count * stride
     assert sorted(stores) == list(range(count)) and set(stores.values()) == {1}
