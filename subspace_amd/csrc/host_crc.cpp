@@ -184,8 +184,13 @@ __attribute__((target("sse4.2"))) uint32_t crc32c_sse42(uint32_t crc, const uint
   return c32;
 }
 
-bool have_sse42() {
-  static const bool ok = __builtin_cpu_supports("sse4.2");
+// The crc32 instruction path of SubspaceCRC32C: the CPU's SSE4.2 alone decides (not the
+// folding paths' PCLMULQDQ), unless SUBSPACE_CRC_HOST_ISA=table asks for tables only.
+bool use_crc32_insn() {
+  static const bool ok = [] {
+    const char* e = std::getenv("SUBSPACE_CRC_HOST_ISA");
+    return __builtin_cpu_supports("sse4.2") && !(e && !std::strcmp(e, "table"));
+  }();
   return ok;
 }
 
@@ -237,7 +242,7 @@ extern "C" uint32_t SubspaceCRC32C(uint32_t crc, const uint8_t* data, size_t len
     data += body;
     length -= body;
   }
-  if (have_sse42() && host_isa() > 0) return crc32c_sse42(crc, data, length);
+  if (use_crc32_insn()) return crc32c_sse42(crc, data, length);
 #endif
   return crc_slice16(slice16c(), crc, data, length);
 }
