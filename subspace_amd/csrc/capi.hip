@@ -19,7 +19,6 @@ namespace subspace_amd {
 template <int WG, bool SLOT, bool PROBE>
 __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int, u32*,
                                        SlotArgs);
-__global__ void crc32_uniform4k_dyn_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, u32*);
 
 struct TileDesc;
 __global__ void crc32_ragged_count_scan_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
@@ -530,9 +529,6 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_slot_lds_bytes(8));
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_dyn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)uniform_dyn_lds_bytes(8));
   if (e == hipSuccess) e = hipMalloc(&c->d_slot_counter, kSlotCounters * sizeof(u64));
   if (e == hipSuccess) e = hipMemset(c->d_slot_counter, 0, kSlotCounters * sizeof(u64));
   if (e == hipSuccess) e = hipMalloc(&c->d_fault, 4 * sizeof(u32));
@@ -662,13 +658,6 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
       sa.probe = c->probe;
       crc32_uniform4k_kernel<512, false, true><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), st>>>(
           b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, sa);
-      c->zero_word = nullptr;
-      HIP_TRY(hipGetLastError());
-      return SUBSPACE_CRC_OK;
-    }
-    if (ord == 4) {  // experiment: order 0's tiles handed out by an LDS ticket per workgroup (512 threads)
-      crc32_uniform4k_dyn_kernel<<<grid_for(c, tiles, 8), 512, uniform_dyn_lds_bytes(8), st>>>(
-          b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, c->zero_word);
       c->zero_word = nullptr;
       HIP_TRY(hipGetLastError());
       return SUBSPACE_CRC_OK;
@@ -1137,7 +1126,10 @@ int subspace_crc_testutil_probe(subspace_crc_ctx* c, void* dev_words) {
 // The number of waves (records) the PROBE launch of a count-message batch has.
 uint64_t subspace_crc_testutil_probe_waves(subspace_crc_ctx* c, uint64_t count) {
   if (!c) return 0;
-  return (u64)grid_for(c, (count + 1) / 2, 8) * 8u;
+  // the larger of the uniform kernel's grid and the slot kernel's (more workgroups than CUs
+  // when a wave would get more than kSlotRingRounds tiles)
+  const u64 tiles = (count + 1) / 2;
+  return std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSlotRingRounds)) * 8u;
 }
 
 // Tuning hook for experiments (not part of the public header): uniform-kernel workgroup
@@ -1145,7 +1137,7 @@ uint64_t subspace_crc_testutil_probe_waves(subspace_crc_ctx* c, uint64_t count) 
 int subspace_crc_testutil_tune(subspace_crc_ctx* c, int uniform_wg, int uniform_blocks, int uniform_order) {
   if (!c) return SUBSPACE_CRC_EINVAL;
   if (uniform_wg != 256 && uniform_wg != 512 && uniform_wg != 768 && uniform_wg != 1024) return SUBSPACE_CRC_EINVAL;
-  if (uniform_order < 0 || uniform_order > 4) return SUBSPACE_CRC_EINVAL;
+  if (uniform_order < 0 || uniform_order > 3) return SUBSPACE_CRC_EINVAL;
   c->uniform_wg = uniform_wg;
   c->uniform_blocks = uniform_blocks;
   c->uniform_order = uniform_order;

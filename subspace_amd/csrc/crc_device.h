@@ -44,12 +44,6 @@ constexpr u32 kUniRing = kLdsOps + kUniOpSlots * 512u;
 // results per wave ring: 256 (128 tiles), or 128 where 16 waves' rings would not fit
 constexpr int uni_ring_results(int waves) { return kUniRing + (u32)waves * 1024u <= 160u * 1024u ? 256 : 128; }
 constexpr size_t uniform_lds_bytes(int waves) { return kUniRing + (size_t)waves * 4u * uni_ring_results(waves); }
-// dynamic tiles (crc32_uniform4k_dyn_kernel): after the rings, each wave's ring of tile indices
-// (one u32 per ring tile), then the workgroup's ticket word
-constexpr u32 uniform_dyn_tids(int waves) { return (u32)uniform_lds_bytes(waves); }
-constexpr u32 uniform_dyn_ticket(int waves) { return uniform_dyn_tids(waves) + (u32)waves * 2u * uni_ring_results(waves); }
-constexpr size_t uniform_dyn_lds_bytes(int waves) { return uniform_dyn_ticket(waves) + 16u; }
-static_assert(uniform_dyn_lds_bytes(8) <= 160u * 1024u, "dynamic uniform kernel LDS exceeds 160 KiB");
 static_assert(uniform_lds_bytes(16) <= 160u * 1024u && uniform_lds_bytes(8) <= 160u * 1024u,
               "uniform kernel LDS exceeds 160 KiB");
 // Slot variant (crc_uniform.hip, SLOT = true): each wave's results go to a ring of

@@ -52,12 +52,8 @@
 
 namespace subspace_amd {
 
-// DYN (crc32_uniform4k_dyn_kernel, tile order 4): the workgroup's tiles -- order 0's front
-// slots, tau = front_slot(b, G, j & 7) + (j >> 3) * nw for ticket j -- are handed out by an LDS
-// ticket counter instead of statically (each wave's first ticket is its own slot), so the wave
-// of a SIMD pair that runs ahead takes more of them.
-template <int WG, bool SLOT, bool PROBE, bool DYN>
-__device__ __forceinline__ void uniform4k_body(
+template <int WG, bool SLOT, bool PROBE>
+__global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
     const uint8_t* __restrict__ base, u64 stride, u64 count, const u32* __restrict__ gtab,
     const u32* __restrict__ gops, u32 init, u32 final_xor, u32* __restrict__ out, int order,
     u32* __restrict__ zero_word, SlotArgs sa) {
@@ -88,9 +84,6 @@ __device__ __forceinline__ void uniform4k_body(
   const u32 lc1 = lc0 + 0x10000u;
   constexpr int kRing = uni_ring_results(NPW);
   const u32 ring = sbase + kUniRing + (u32)wid * (4u * kRing);
-  // DYN: this wave's ring of tile indices (one per ring tile), the workgroup's ticket word
-  const u32 tring = sbase + uniform_dyn_tids(NPW) + (u32)wid * (2u * kRing);
-  const u32 tword = sbase + uniform_dyn_ticket(NPW);
   // SLOT: this wave's tagged result ring; the workgroup's mismatch word
   const u32 sring = sbase + kUniSlotRing + (u32)wid * kSlotRingBytesPerWave;
   const u32 smism = sbase + uniform_slot_mism_word(NPW);
@@ -198,9 +191,6 @@ __device__ __forceinline__ void uniform4k_body(
   u32x4 A[8], B[8];
   load_tile(A, 0);
   fill.store(sbase);
-  if constexpr (DYN) {
-    if (threadIdx.x == 0) lds_st(tword, (u32)NPW);  // tickets 0..NPW-1 are the waves' first tiles
-  }
   if constexpr (SLOT) {
     // no ring entry may carry a tag before its tile is written; the mismatch word starts at 0
     constexpr u32 kEntries = (u32)NPW * kSlotRingBytesPerWave / 8u;
@@ -229,77 +219,6 @@ __device__ __forceinline__ void uniform4k_body(
   constexpr u32 kWin = SLOT ? ~0u : (u32)(kRing / 2);
   u32 k = 0, kf = 0;
   u64 pt_finish = 0;  // PROBE, SLOT: when a finishing wave began
-  if constexpr (DYN) {
-    static_assert(NPW == 8 && !SLOT, "dynamic tiles: 8 waves, plain results");
-    // tickets of the workgroup: sum of its 8 front slots' tile counts (a prefix of j: in the
-    // last round only the lower front slots have a tile)
-    u32 J = 0;
-#pragma unroll
-    for (u32 w = 0; w < 8; w++) {
-      const u64 f = front_slot(blockIdx.x, gridDim.x, w);
-      J += f < ntiles ? ((u32)(ntiles - f) + (u32)nw - 1u) / (u32)nw : 0u;
-    }
-    auto tau_of = [&](u32 j) { return front_slot(blockIdx.x, gridDim.x, j & 7u) + (u64)(j >> 3) * nw; };
-    auto load_tau = [&](u32x4 (&d)[8], u64 tau) {
-      u64 msg = 2 * tau + (u64)h;
-      msg = msg < count ? msg : msg - 1;
-      const u32x4* q = reinterpret_cast<const u32x4*>(base + msg * stride + (u64)l * 128);
-#pragma unroll
-      for (int i = 0; i < 8; i++) d[i] = q[i];
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    auto take = [&]() {  // the next ticket (one LDS atomic, lane 0)
-      u32 v = 0;
-      if (lane == 0)
-        v = __hip_atomic_fetch_add(reinterpret_cast<lds_u32_t*>((uintptr_t)tword), 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-      return v;
-    };
-    auto flush_dyn = [&](u32 kf_, u32 nt) {
-#pragma unroll
-      for (int i = 0; i < kRing / 64; i++) {
-        const u32 slot = (u32)(i * 64 + lane);
-        const u32 t = slot >> 1;
-        const u64 msg = 2 * (u64)lds_ld(tring + 4u * t) + (u64)(slot & 1u);
-        if (t < nt && msg < count) out[msg] = lds_ld(ring + 4u * slot);
-      }
-      wave_lds_sync();
-    };
-    u32 jA = (u32)wid;
-    u64 tA = tau_of(jA);
-    if (jA < J) {
-      u32 jn = take();
-      for (;;) {
-        drain_before_issue();
-        const u32 jB = rfl(jn);
-        const bool vB = jB < J;
-        const u64 tB = vB ? tau_of(jB) : tA;  // past the last ticket: re-read A's tile
-        jn = take();
-        load_tau(B, tB);
-        if (k - kf == (u32)(kRing / 2)) {
-          wave_lds_sync();
-          flush_dyn(kf, kRing / 2);
-          kf = k;
-        }
-        tile_result(line_crc(A), k, kf);
-        if (lane == 0) lds_st(tring + 4u * (k - kf), (u32)tA);
-        k++;
-        if (!vB) break;
-        drain_before_issue();
-        jA = rfl(jn);
-        const bool vA = jA < J;
-        tA = vA ? tau_of(jA) : tB;
-        jn = take();
-        load_tau(A, tA);
-        tile_result(line_crc(B), k, kf);
-        if (lane == 0) lds_st(tring + 4u * (k - kf), (u32)tB);
-        k++;
-        if (!vA) break;
-      }
-    }
-    wave_lds_sync();
-    if (k > kf) flush_dyn(kf, k - kf);
-  } else {
   for (; k + 1 < nk; k += 2) {
     drain_before_issue();
     load_tile(B, k + 1);
@@ -441,7 +360,6 @@ __device__ __forceinline__ void uniform4k_body(
   } else {
     if (nk > kf) flush(kf, nk - kf);
   }
-  }  // !DYN
   // a word the caller's next kernel accumulates into (a slot batch's mismatch count): zeroed
   // here, at the end, so the call needs no separate memset
   if (zero_word != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0u;
@@ -456,23 +374,6 @@ __device__ __forceinline__ void uniform4k_body(
       if (lane < 8) r[lane] = v;
     }
   }
-}
-
-template <int WG, bool SLOT, bool PROBE>
-__global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(const uint8_t* __restrict__ base, u64 stride, u64 count,
-                                                             const u32* __restrict__ gtab, const u32* __restrict__ gops,
-                                                             u32 init, u32 final_xor, u32* __restrict__ out, int order,
-                                                             u32* __restrict__ zero_word, SlotArgs sa) {
-  uniform4k_body<WG, SLOT, PROBE, false>(base, stride, count, gtab, gops, init, final_xor, out, order, zero_word, sa);
-}
-
-// Tile order 4 (subspace_crc_testutil_tune): order 0's tiles handed out by an LDS ticket per workgroup.
-__global__ __launch_bounds__(512) void crc32_uniform4k_dyn_kernel(const uint8_t* __restrict__ base, u64 stride,
-                                                                  u64 count, const u32* __restrict__ gtab,
-                                                                  const u32* __restrict__ gops, u32 init, u32 final_xor,
-                                                                  u32* __restrict__ out, u32* __restrict__ zero_word) {
-  uniform4k_body<512, false, false, true>(base, stride, count, gtab, gops, init, final_xor, out, 0, zero_word,
-                                          SlotArgs{});
 }
 
 #define INST(WGV, SL, PR)                                                                                 \

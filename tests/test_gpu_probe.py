@@ -53,7 +53,10 @@ def test_probe_uniform_matches_product(gpu_ctx):
     assert torch.equal(out, ref)
     r = rec.cpu().numpy()
     _check_records(r, N // 2)
-    assert (r[:, 6] == 0).all()  # no slot flush in the plain kernel
+    assert ((r[:, 6] >> 32) == 0).all()  # no slot finishing in the plain kernel
+    hw = r[:, 6] & 0xFFFFFFFF  # HW_ID: waves w and w + 4 of a workgroup share a SIMD
+    simd = (hw >> 4) & 3
+    assert (simd.reshape(-1, 8)[:, :4] == simd.reshape(-1, 8)[:, 4:]).all()
 
 
 def test_probe_slots_matches_product(gpu_ctx):
@@ -79,4 +82,9 @@ def test_probe_slots_matches_product(gpu_ctx):
     assert torch.equal(a, b)  # identical prefixes written
     r = rec.cpu().numpy()
     _check_records(r, (n + 1) // 2)
-    assert (r[:, 6] >= r[:, 2]).all() and (r[:, 6] <= r[:, 3]).all()  # slot flush between loop end and exit
+    # waves 0-3 of each workgroup finish the slots, between their loop end and their exit
+    # (the record keeps the clock's low 32 bits)
+    fin = (r[:, 6] >> 32).reshape(-1, 8)
+    lo = lambda x: (x & 0xFFFFFFFF).reshape(-1, 8)  # noqa: E731
+    assert (fin[:, 4:] == 0).all()
+    assert ((fin[:, :4] - lo(r[:, 2])[:, :4]) % (1 << 32) <= (lo(r[:, 3])[:, :4] - lo(r[:, 2])[:, :4]) % (1 << 32)).all()
