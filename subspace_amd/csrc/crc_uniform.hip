@@ -291,7 +291,10 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
           constexpr u32 kW = kSlotFusedMaxMeta / 4 + 2;
           u32 W1[kW];
 #pragma unroll
-          for (u32 j = 0; j < kW; j++) W1[j] = p1[j < nwords ? j : nwords - 1u];
+          for (u32 j = 0; j < kW; j++) {  // only the words the span needs (a uniform bound)
+            W1[j] = 0u;
+            if (j < nwords) W1[j] = p1[j];
+          }
           u32 tail = 0;
 #pragma unroll
           for (u32 j = 0; j + 1 < kW; j++) {
