@@ -390,7 +390,7 @@ class Workload:
             if self.world > 1:
                 return None, None
             return digest(self.outs[0].cpu().numpy().view(np.uint32)) == GOLD["B"]["sha256_le_u32"], None
-        if self.world > 1:
+        if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -450,7 +450,7 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, re
     ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for i in range(0, steps, event_every)} if event_every > 0 else {}
     region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     if region_marks:
@@ -470,12 +470,12 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, re
         stream.wait_stream(s2)  # ... and the last event after every stream's last launch
     region[1].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     elapsed = own = time.perf_counter() - t0
     if region_marks:
         region_marks.pause()
-    if world > 1:
+    if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=stream.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -733,9 +733,9 @@ def dry_run_cpu(args, world, rank) -> int:
     tg = time.perf_counter()
     # the same gather helpers as the GPU run (here on CPU tensors over gloo)
     if wl == "C":
-        full = shard.gather_ragged_crcs_device(tl, bounds, world, dist).numpy().view(np.uint32)
+        full = shard.gather_ragged_crcs_device(tl, bounds, world, dist if world > 1 else None).numpy().view(np.uint32)
     elif wl == "E":
-        full = shard.gather_crcs_device(tl, count, world, dist).numpy().view(np.uint32)
+        full = shard.gather_crcs_device(tl, count, world, dist if world > 1 else None).numpy().view(np.uint32)
     else:
         full = local[:len(msgs)]
     gather_ms = (time.perf_counter() - tg) * 1e3
@@ -792,7 +792,11 @@ def main():
     gpu_index = 0 if args.rehearse_one_gpu else local
     if torch.cuda.device_count() <= gpu_index:
         die(f"LOCAL_RANK {local} but only {torch.cuda.device_count()} visible GPU(s)")
-    if world > 1:
+    # a launcher (torch.distributed.run) sets WORLD_SIZE: then the process group exists even at
+    # one rank, so the RCCL path (init, barriers, the max-over-ranks reduction, the gather)
+    # runs exactly as at N ranks; a plain `python bench.py` (the driver's N = 1) has none
+    dist_on = world > 1 or world_env is not None
+    if dist_on:
         torch.cuda.set_device(gpu_index)
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if args.rehearse_one_gpu:
@@ -813,12 +817,13 @@ def main():
     streams = [stream] + [torch.cuda.Stream() for _ in range(args.streams - 1)]
     for s2 in streams[1:]:
         s2.wait_stream(stream)
+    pg = dist if dist_on else None
     elapsed, avg_kern_ms, sampled_ms, settle, own_s = run_timed(wl, args.steps, args.warmup, args.settle, streams,
-                                                                world, dist, args.event_every,
+                                                                world, pg, args.event_every,
                                                                 RoctxRegion(args.roctx_region and rank == 0),
                                                                 args.settle_s if args.settle > 0 else 0.0)
     settle = max(0, settle - args.warmup)
-    bitexact, gather = wl.check(dist)
+    bitexact, gather = wl.check(pg)
     gather_ms = gather["gather_ms"] if gather else None
     # every rank's identity and timing, so the line shows that N distinct GPUs ran
     props = torch.cuda.get_device_properties(gpu_index)
@@ -826,7 +831,7 @@ def main():
           "pci": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
           "uuid": str(getattr(props, "uuid", "")), "step_ms": round(own_s / args.steps * 1e3, 4),
           "launch_ms_event": round(avg_kern_ms, 4)}
-    if world > 1:
+    if dist_on:
         everyone = [None] * world
         dist.all_gather_object(everyone, me)
     else:
@@ -958,7 +963,7 @@ def main():
         line["ranks"] = everyone
         line["rank_step_ms"] = {"min": min(steps_ms), "max": max(steps_ms)}
         line["distinct_gpus"] = len({r["pci"] + r["uuid"] for r in everyone})
-        if world > 1:
+        if dist_on:
             line["rccl_world"] = dist.get_world_size()
             line["backend"] = dist.get_backend()
         if solo is not None:
@@ -968,7 +973,7 @@ def main():
         line["cpu_baseline"] = cpu
         line["e2e_pcie"] = e2e
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
     ctx.close()
 

@@ -90,13 +90,13 @@ def gather_ragged_crcs(local, bounds, rank: int, world: int, dist, dst: int = 0)
 # ---------------------------------------------------------------- device-resident gathers
 def gather_crcs_device(local, count: int, world: int, dist):
     """all_gather the per-rank CRC tensors (padded to equal length) and interleave them into
-    global order ON THE DEVICE (every rank gets the full int32 tensor; no host copy). At
-    world 1 it is one device copy of the local results."""
+    global order ON THE DEVICE (every rank gets the full int32 tensor; no host copy). Without
+    a process group (dist None) it is one device copy of the local results."""
     import torch
     per = (count + world - 1) // world
     buf = torch.zeros(per, dtype=torch.int32, device=local.device)
     buf[:min(local.numel(), per)] = local[:per]
-    if world == 1:
+    if dist is None:
         return buf[:count].clone()
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf)
@@ -111,7 +111,7 @@ def gather_ragged_crcs_device(local, bounds, world: int, dist):
     per = int(max(bounds[r + 1] - bounds[r] for r in range(world)))
     buf = torch.zeros(max(per, 1), dtype=torch.int32, device=local.device)
     buf[:local.numel()] = local
-    if world == 1:
+    if dist is None:
         return buf[:int(bounds[1])].clone()
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf)

@@ -42,3 +42,28 @@ def test_two_ranks_on_one_gpu(workload):
         # interleave); the D2H copy and host check are reported apart
         assert g["gather_ms"] > 0 and g["d2h_check_ms"] > 0 and g["gather_bytes"] == 8 * 2**20 * 4
     assert d["efficiency"] > 0 and d["per_gpu_value"] == pytest.approx(d["value"] / 2, rel=1e-2)
+
+
+def test_rccl_path_one_rank():
+    """The RCCL branch of bench.py on the one-GPU box: launched by torch.distributed.run with
+    one rank, bench.py creates the "nccl" (RCCL) process group with device_id, times between
+    RCCL barriers with the max-over-ranks all_reduce, gathers the CRCs with an RCCL all_gather
+    (into global order on the device) and gathers every rank's record -- the code an N-GPU run
+    executes, with N = 1. Workload E: the whole 8 Mi x 4 KiB batch, checked against its fixture."""
+    import socket
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"),
+                        "--gpus", "1", "--workload", "E", "--steps", "3", "--warmup", "1", "--settle", "0"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["backend"] == "nccl" and d["rccl_world"] == 1 and d["n_gpus"] == 1
+    assert d["bitexact_vs_golden"] is True
+    assert d["config"]["gather"]["gather_ms"] > 0 and d["ranks"][0]["rank"] == 0
