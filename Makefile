@@ -8,7 +8,7 @@ CSRC := subspace_amd/csrc
 LIB := subspace_amd/libsubspace_crc.so
 OBJDIR := build/obj
 
-HIP_SRCS := $(CSRC)/crc_uniform.hip $(CSRC)/crc_ragged.hip $(CSRC)/crc_long.hip $(CSRC)/crc_combine.hip $(CSRC)/crc_slots.hip $(CSRC)/capi.hip $(CSRC)/testutil.hip
+HIP_SRCS := $(CSRC)/crc_uniform.hip $(CSRC)/crc_small.hip $(CSRC)/crc_ragged.hip $(CSRC)/crc_long.hip $(CSRC)/crc_combine.hip $(CSRC)/crc_slots.hip $(CSRC)/capi.hip $(CSRC)/testutil.hip
 CPP_SRCS := $(CSRC)/host_crc.cpp $(CSRC)/split_alloc.cpp
 HDRS := $(CSRC)/crc_device.h $(CSRC)/crc_math.h include/subspace_crc.h
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))

@@ -40,6 +40,8 @@ __global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* o
 template <int WG>
 __global__ void crc32_long_kernel(const uint8_t*, u64, u32, u32, const u32*, const u32*, u32, u32, u32*, u32);
 __global__ void crc32_long_final_kernel(const u32*, const u32*, u32, u32, u32, u32, u32*, u64*, u64, u32*);
+template <int WG, bool SLOT>
+__global__ void crc32_small_kernel(const u32*, const u32*, SmallArgs);
 
 }  // namespace subspace_amd
 
@@ -167,6 +169,7 @@ struct subspace_crc_ctx {
   u64* d_slot_counter = nullptr;
   u32 slot_counter_next = 0;
   bool fused_slots = true;        // contiguous 4 KiB slot batches take the fused uniform kernel
+  bool small_path = true;         // batches of messages <= 4 KiB take the small-message kernel (crc_small.hip)
   u64* probe = nullptr;           // experiment hook: per-wave timestamps (subspace_crc_testutil_probe)
   u32* d_fault = nullptr;         // fault word (crc_device.h kFault*): read and cleared by subspace_crc_ctx_check
   // One call at a time per context (a recursive mutex: the host-slot paths call the device
@@ -393,6 +396,67 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   return SUBSPACE_CRC_OK;
 }
 
+// Messages of at most max_len bytes fit one half-tile of the small-message kernel: 4,096 if
+// they start on 16-B boundaries, else 4,081 (the extended length adds offset & 15).
+bool small_fits(u64 max_len, bool aligned16) { return max_len <= (aligned16 ? kSmallMaxExt : kSmallMaxExt - 15); }
+
+// Small-message path (crc_small.hip): messages of at most 4 KiB two to a tile in one kernel
+// (the last workgroup computes any message longer than a half-tile). Same arguments and
+// results as ragged_run; with `slot` the kernel also finishes the slots (span terms, flag +
+// checksum or status, mismatch count) and `out` is unused.
+struct SmallSlot {
+  const u64* prefixes;
+  u32 pstride;
+  u64 pdelta;
+  u32 mode;
+  int32_t checksum_size, metadata_size;
+  u32 *status, *crc_out, *error_count;
+};
+int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 ostride, const u64* lengths,
+              u32 lstride, u64 count, u32 init, u32 final_xor, u32* out, hipStream_t st,
+              const SmallSlot* slot = nullptr) {
+  SmallArgs a{};
+  a.base = base;
+  a.offsets = offsets;
+  a.ostride = ostride;
+  a.lengths = lengths;
+  a.lstride = lstride;
+  a.count = count;
+  a.init = init;
+  a.final_xor = final_xor;
+  a.out = out;
+  a.rops = c->d_rops;
+  a.pow2 = c->d_pow2;
+  const unsigned blocks = (unsigned)grid_for(c, (count + 1) / 2, 8);
+  const size_t lds = small_lds_bytes() + 16;
+  if (slot) {
+    a.prefixes = slot->prefixes;
+    a.pstride = slot->pstride;
+    a.pdelta = slot->pdelta;
+    a.mode = slot->mode;
+    a.checksum_size = (u32)slot->checksum_size;
+    a.metadata_size = (u32)slot->metadata_size;
+    a.status = slot->status;
+    a.crc_out = slot->crc_out;
+    a.error_count = slot->error_count;
+    a.counter = c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters);
+    crc32_small_kernel<512, true><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
+  } else {
+    a.zero_word = c->zero_word;
+    c->zero_word = nullptr;
+    crc32_small_kernel<512, false><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
+  }
+  HIP_TRY(hipGetLastError());
+  return SUBSPACE_CRC_OK;
+}
+
+// The fused small-slot kernel finishes slots whose checksum and metadata areas are at most
+// kSlotFusedMaxMeta bytes each (its lanes without a slot read their spans from the 4 KiB
+// step table); others take the small kernel + crc32_slot_finish_kernel.
+bool small_slot_fused(int32_t checksum_size, int32_t metadata_size) {
+  return (u32)checksum_size <= kSlotFusedMaxMeta && (u32)metadata_size <= kSlotFusedMaxMeta;
+}
+
 int ensure_slot_ws(subspace_crc_ctx* c, u64 count) {
   if (count <= c->s_capacity) return SUBSPACE_CRC_OK;
   (void)hipFree(c->d_crc0);
@@ -469,7 +533,7 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   c->host_tab = make_tables(poly);
   c->zinv1 = inverse(z_one(c->host_tab));
 
-  std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kUniOpSlots * 128, 0u), rops(kRagOpWords, 0u);
+  std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kSmallOpSlots * 128, 0u), rops(kRagOpWords, 0u);
   for (int k = 0; k < 4; k++)
     for (int b = 0; b < 256; b++) tab[k * 256 + b] = c->host_tab.t[k][b];
 
@@ -502,9 +566,12 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   {  // Z_64 replicated 4x, the same table as the uniform kernel's slots 33..36
     std::copy(laneops.begin() + 128 * kUniSlotOpZ64, laneops.begin() + 128 * (kUniSlotOpZ64 + 4), rops.begin() + kRagZ64Words);
   }
-  // the ragged final kernel's padding inverses Z_{2^b}^{-1}, b = 0..12
+  // the ragged final kernel's padding inverses Z_{2^b}^{-1}, b = 0..12; the small-message
+  // kernel's (b = 0..11) after the uniform kernel's slots
   for (int b = 0; b < kNumInvOps; b++)
     nibble_tables(inverse(z_bytes(c->host_tab, 1ull << b)), &rops[kRagInvOps + 128 * b]);
+  std::copy(rops.begin() + kRagInvOps, rops.begin() + kRagInvOps + 128 * kSmallInvOps,
+            laneops.begin() + 128 * kSmallOpInv);
 
   hipError_t e = hipMalloc(&c->d_tab, tab.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_laneops, laneops.size() * 4);
@@ -540,6 +607,12 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_long_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)ragged_lds_bytes());
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)small_lds_bytes() + 16);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)small_lds_bytes() + 16);
   if (e != hipSuccess) {
     subspace_crc_ctx_destroy(c);
     return hip_fail(e, "context setup");
@@ -705,7 +778,10 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     c->scan_dirty = false;
     return SUBSPACE_CRC_OK;
   }
-  // Any other shape: materialise offsets/lengths and take the ragged path.
+  // Any other shape: materialise offsets/lengths (context workspace: ordered after the last
+  // workspace call first) and take the small-message or the ragged path.
+  int rc = use_workspace(c, st);
+  if (rc) return rc;
   if (count > c->u_capacity) {
     (void)hipFree(c->d_uoff);
     (void)hipFree(c->d_ulen);
@@ -718,6 +794,9 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
   uniform_offsets_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(stride, length, count, c->d_uoff,
                                                                            c->d_ulen);
   HIP_TRY(hipGetLastError());
+  if (small_fits(length, (stride % 16) == 0 && ((uintptr_t)dev_base % 16) == 0) && c->small_path && count > 1)
+    return small_run(c, static_cast<const uint8_t*>(dev_base), c->d_uoff, 1, c->d_ulen, 1, count, init, final_xor,
+                     dev_out, st);
   const u64 arena = stride * (count - 1) + length;
   return subspace_crc32_batch(c, dev_base, arena, c->d_uoff, c->d_ulen, count, init, flags, dev_out, stream);
 }
@@ -742,11 +821,21 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
   if (rc) return rc;
   rc = ensure_slot_ws(c, count);
   if (rc) return rc;
-  // payload CRCs from init 0 at absolute addresses (base 0; fields 1 and 2 of each record)
+  // payload CRCs from init 0 at absolute addresses (base 0; fields 1 and 2 of each record):
+  // slots of at most 4 KiB through the small-message kernel, larger ones the ragged path
   const u64* rec = reinterpret_cast<const u64*>(dev_slots);
-  const u64 cap = count * ((max_message_size + 15 + 8191) / 8192) + 1;
+  const bool small = max_message_size <= kSmallMaxExt && c->small_path;
+  if (small && small_slot_fused(checksum_size, metadata_size)) {  // one kernel, slots finished in it
+    const SmallSlot ss{rec, 3, 0, mode, checksum_size, metadata_size, dev_status, nullptr, dev_error_count};
+    return small_run(c, nullptr, rec + 1, 3, rec + 2, 3, count, 0u, 0u, nullptr, st, &ss);
+  }
   want_zeroed(c, dev_error_count);
-  rc = ragged_run(c, nullptr, cap, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st);
+  if (small) {
+    rc = small_run(c, nullptr, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st);
+  } else {
+    const u64 cap = count * ((max_message_size + 15 + 8191) / 8192) + 1;
+    rc = ragged_run(c, nullptr, cap, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st);
+  }
   const bool zeroed = was_zeroed(c, dev_error_count);
   if (rc) return rc;
   return slot_finish(c, rec, nullptr, 0, nullptr, 0, count, checksum_size, metadata_size, mode, dev_status,
@@ -811,8 +900,21 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
     slot_payload_offsets_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(slot_stride, prefix_size, count,
                                                                                 c->d_soff);
     HIP_TRY(hipGetLastError());
-    const u64 cap = (slot_stride * count + 15 * count) / 8192 + count + 1;
-    rc = ragged_run(c, buf, cap, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st);
+    const bool aligned = slot_stride % 16 == 0 && ((uintptr_t)(buf + prefix_size) % 16) == 0;
+    if (count > 1 && small_fits(slot_stride - prefix_size, aligned) && c->small_path) {
+      // slots of at most 4 KiB (a larger size, past its slot, still gets its CRC: the small
+      // kernel's last workgroup); the prefix of slot i is its payload offset - prefix_size
+      if (small_slot_fused(checksum_size, metadata_size)) {
+        was_zeroed(c, dev_error_count);  // the fused kernel writes the count itself
+        const SmallSlot ss{c->d_soff, 1, prefix_size, mode, checksum_size, metadata_size, dev_status, dev_crc_out,
+                           dev_error_count};
+        return small_run(c, buf, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, nullptr, st, &ss);
+      }
+      rc = small_run(c, buf, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st);
+    } else {
+      const u64 cap = (slot_stride * count + 15 * count) / 8192 + count + 1;
+      rc = ragged_run(c, buf, cap, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st);
+    }
   } else {
     rc = subspace_crc32_batch_uniform(c, buf + prefix_size, slot_stride, message_size, count, 0u, 0u, c->d_crc0,
                                       st);
@@ -1108,6 +1210,10 @@ int subspace_crc_testutil_set(subspace_crc_ctx* c, const char* key, int value) {
   }
   if (!std::strcmp(key, "fused_slots")) {
     c->fused_slots = value != 0;
+    return SUBSPACE_CRC_OK;
+  }
+  if (!std::strcmp(key, "small_path")) {  // 0: messages <= 4 KiB take the ragged path (A/B, parity)
+    c->small_path = value != 0;
     return SUBSPACE_CRC_OK;
   }
   return SUBSPACE_CRC_EINVAL;

@@ -109,6 +109,41 @@ constexpr int kRagOpWords = kRagInvOps + kNumInvOps * 128;
 constexpr size_t ragged_lds_bytes() { return kLdsOps + (size_t)kRagLdsOpWords * 4u; }
 static_assert(ragged_lds_bytes() <= 160u * 1024u, "ragged kernel LDS exceeds 160 KiB");
 
+// Small-message kernel layout (crc_small.hip): the uniform kernel's operator slots (line
+// shifts, Z_4096, Z_64 x4), then the padding inverses Z_{2^b}^{-1}, b = 0..11 (a message of
+// at most 4 KiB is padded by fewer than 4,096 bytes), then a 16-B word (the workgroup's
+// mismatch count). The device array d_laneops holds all kSmallOpSlots slots (the uniform kernel loads
+// the first kUniOpSlots).
+constexpr int kSmallOpInv = kUniOpSlots;
+constexpr int kSmallInvOps = 12;
+constexpr int kSmallOpSlots = kSmallOpInv + kSmallInvOps;
+constexpr u32 kSmallMaxExt = 4096;  // extended bytes (length + offset & 15) of one half-tile
+constexpr size_t small_lds_bytes() { return kLdsOps + (size_t)kSmallOpSlots * 512u; }
+static_assert(small_lds_bytes() <= 160u * 1024u, "small-message kernel LDS exceeds 160 KiB");
+
+// Small-message kernel arguments (crc_small.hip; one struct: read with scalar loads).
+struct SmallArgs {
+  const uint8_t* base;
+  const u64* offsets;   // message m's first byte: base + offsets[m * ostride]
+  const u64* lengths;   // its length: lengths[m * lstride]
+  const u64* prefixes;  // SLOT: its MessagePrefix at base + prefixes[m * pstride] - pdelta
+  u64 count;
+  u64 pdelta;
+  u32 ostride, lstride, pstride;
+  u32 init, final_xor;
+  u32 mode, checksum_size, metadata_size;  // SLOT: both sizes <= kSlotFusedMaxMeta (lanes
+                                           // without a slot read their spans from the 4 KiB
+                                           // step table)
+  u32* out;          // !SLOT: the CRC of every message
+  u32* status;       // SLOT, optional: per-slot status
+  u32* crc_out;      // SLOT, optional: the stored checksum (CALCULATE)
+  u32* error_count;  // SLOT, optional: this call's mismatches (0 for CALCULATE)
+  u64* counter;      // SLOT: context word, (workgroups done << 32) | mismatches; 0 between calls
+  u32* zero_word;    // !SLOT, optional: zeroed at the end (the next kernel's mismatch count)
+  const u32* rops;   // the ragged operator array (Z_8192; Z_4096^{-1}, the 13th padding inverse)
+  const u32* pow2;   // SLOT: Z_{2^k}, k < 64 (a long message's Z_L)
+};
+
 // Ragged path: tiles per wave of the descriptor kernel, = the chunk of the tile-count scan's
 // chunk index (chunk_msg[c] = the message holding tile c * kDescTilesPerWave).
 constexpr u64 kDescTilesPerWave = 256;
@@ -276,6 +311,32 @@ __device__ __forceinline__ u32 opmul(u32 sbase, int slot, u32 v) {
 #pragma unroll
   for (int k = 1; k < 8; k++) r ^= lds_ld(op + 64u * k + ((v >> (4 * k - 2)) & 0x3Cu));
   return r;
+}
+
+// Nibble operator read from global memory (operators not staged in LDS: the ragged kernel's
+// tile shifts for messages of 16 GiB and more; the small kernel's long-message path).
+__device__ __forceinline__ u32 opmul_global(const u32* __restrict__ op, u32 v) {
+  u32 r = op[v & 15u];
+#pragma unroll
+  for (int k = 1; k < 8; k++) r ^= op[16 * k + ((v >> (4 * k)) & 15u)];
+  return r;
+}
+
+// Keep the bytes of a 128-B line window at positions [lo, hi) (0 <= lo, hi <= 128).
+__device__ __forceinline__ void keep_bytes(u32x4 (&d)[8], u32 lo, u32 hi) {
+#pragma unroll
+  for (int b = 0; b < 8; b++) {
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+      const u32 p = 16u * b + 4u * x;
+      u32 keep = 0u;
+      if (p + 4u <= hi) keep = 0xFFFFFFFFu;
+      else if (p < hi) keep = 0xFFFFFFFFu >> (8u * (p + 4u - hi));
+      if (p + 4u <= lo) keep = 0u;
+      else if (p < lo) keep &= 0xFFFFFFFFu << (8u * (lo - p));
+      d[b][x] &= keep;
+    }
+  }
 }
 
 // Byte step with the k=3 step table (plain byte table): crc = (crc >> 8) ^ T[(crc ^ b) & 0xFF].

@@ -151,32 +151,6 @@ __global__ __launch_bounds__(256) void crc32_ragged_desc_kernel(const u64* __res
 
 // ------------------------------------------------------------------ main kernel
 
-// Nibble operator read from global memory (the tile-shift operators for 2^21 tiles and
-// more, which only messages of 16 GiB and more need; the padding inverses).
-__device__ __forceinline__ u32 opmul_global(const u32* __restrict__ op, u32 v) {
-  u32 r = op[v & 15u];
-#pragma unroll
-  for (int k = 1; k < 8; k++) r ^= op[16 * k + ((v >> (4 * k)) & 15u)];
-  return r;
-}
-
-// Keep the bytes of a 128-B line window at positions [lo, hi) (0 <= lo, hi <= 128).
-__device__ __forceinline__ void keep_bytes(u32x4 (&d)[8], u32 lo, u32 hi) {
-#pragma unroll
-  for (int b = 0; b < 8; b++) {
-#pragma unroll
-    for (int x = 0; x < 4; x++) {
-      const u32 p = 16u * b + 4u * x;
-      u32 keep = 0u;
-      if (p + 4u <= hi) keep = 0xFFFFFFFFu;
-      else if (p < hi) keep = 0xFFFFFFFFu >> (8u * (p + 4u - hi));
-      if (p + 4u <= lo) keep = 0u;
-      else if (p < lo) keep &= 0xFFFFFFFFu << (8u * (lo - p));
-      d[b][x] &= keep;
-    }
-  }
-}
-
 template <int WG, bool DESC>
 __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, const u64* __restrict__ offsets,
                                             u32 ostride, const u64* __restrict__ lengths, u32 lstride,

@@ -1,0 +1,403 @@
+// Small-message kernel: one CRC32 per message of at most 4 KiB, two messages per 8 KiB tile
+// -- the slot-list and per-slot-size paths (subspace_crc32_slots with max_message_size <=
+// 4096, subspace_crc32_slots_strided with per-slot sizes in slots of <= 4 KiB) and uniform
+// batches of messages shorter than 4 KiB. It replaces the ragged pipeline (tile-count scan,
+// descriptors, ragged kernel, segment scans, final kernel, slot finish: seven launches,
+// ~118 us for 65,536 slots of 4 KiB) with one kernel, because a message of at most one
+// half-tile needs neither a tile index nor a cross-tile combine.
+//
+// Decomposition:
+//  * Message m = bytes [s, s + L) of base (s = offsets[m*ostride], L = lengths[m*lstride]),
+//    mis = s & 15, extended length E = L + mis. With E <= 4096 it fills one half of a tile:
+//    lane l of half h owns the 128-B line [s0 + 128 l, +128) of message 2 tau + h, s0 = s -
+//    mis -- the uniform kernel's access shape (64 consecutive lines per load instruction when
+//    the two messages are adjacent) and the ragged kernel's alignment rule (whole 16-B
+//    blocks from the block holding s; the first mis bytes and the bytes from E on masked).
+//  * Waves sweep the tiles like the uniform kernel (order-0 front). A tile's two records
+//    are loaded one tile ahead of its lines (vector loads, retired in order with the line
+//    loads, as the ragged kernel's descriptors), so line addresses never wait on a record.
+//  * Every line load stays inside its message: block b of lane l is read from s0 +
+//    min(128 l + 16 b, last block), so the lanes past the end re-read the last block (one
+//    cache line) instead of branching around loads, and a half with nothing to read (no
+//    message, an empty one, or one too long for this kernel) reads a 16-B block of the step
+//    table. Loads never touch a 16-B block that holds no byte of the message.
+//  * Line 0 starts from seed = Z_mis^{-1}(init), every other line from 0, so each half gives
+//      V = crc_raw(seed, 0^mis || D || 0^p) = Z_p(crc_raw(init, D)),   p = 4096 - E;
+//    values are parked one tile per lane (lane k & 63 keeps tile k's two values and codes),
+//    and every 64 tiles each lane undoes the padding of its two messages with p's bits over
+//    the inverse operators Z_{2^b}^{-1}, b < 12 (LDS), and stores the CRCs.
+//  * SLOT: the message-slot checksum (client/checksum.h:29-47 over common/channel.h:527-542's
+//    spans) in the same flush, from init 0: with H = crc_raw(~0, span 0 || span 1) from the
+//    prefix (the flag set first for a publish, client/publisher.cc:664-675),
+//      Z_p(crc_raw(H, payload)) = Z_{p+L}(H) ^ V = Z_4096(Z_mis^{-1}(H)) ^ V,
+//    so the padding inverses that finish a plain CRC finish the checksum too; then flag +
+//    checksum are stored (publish) or compared (verify: client/client.cc:1346-1356), with no
+//    second kernel.
+//  * A message with E > 4096 (longer than the caller's max_message_size bound, or a 4 KiB
+//    payload that does not start on a 16-B boundary) is parked as such and computed by the
+//    wave's next flush, one at a time by the whole wave, in 8 KiB chunks (acc = Z_8192(acc) ^
+//    chunk, the last chunk's padding undone; SLOT: finished as Z_L(H) ^ crc_raw(0, payload)),
+//    behind a wave-uniform branch the common case never takes. No list, no second kernel, no
+//    code in the tile loop, and a batch of long messages still spreads over every wave.
+//  * SLOT verify: mismatches are summed per workgroup by one LDS atomic per wave and over
+//    workgroups by one relaxed 64-bit atomic per workgroup on a context counter word that also
+//    counts finished workgroups; the last one writes the call's total and resets the word
+//    (the fused uniform slot kernel's scheme: no fences, no memset).
+#include "crc_device.h"
+
+namespace subspace_amd {
+
+template <int WG, bool SLOT>
+__global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__ gtab, const u32* __restrict__ gops,
+                                                         SmallArgs a) {
+  extern __shared__ __attribute__((aligned(16))) u32 smem[];
+  constexpr int NPW = WG / 64;
+  const u32 sbase = (u32)(uintptr_t)smem;
+  const u32 smism = sbase + (u32)small_lds_bytes();  // SLOT: the workgroup's mismatch word
+  LdsFill<WG, kSmallOpSlots> fill;
+  fill.load(gtab, gops);
+
+  const int lane = threadIdx.x & 63;
+  const u32 wid = rfl(threadIdx.x >> 6);
+  const u32 l = (u32)lane & 31u, h = (u32)lane >> 5;
+  const u32 lc0 = sbase + (l << 2), lc1 = lc0 + 0x10000u;
+  const u32 lop = sbase + kLdsOps + 4u * (31u - l);  // this lane's line-shift operator
+  const u32 z64 = sbase + kLdsOps + 512u * (u32)kUniSlotOpZ64 + 4u * (u32)(lane & 3);
+  const u64 count = a.count;
+  const uint8_t* const base = a.base;
+  const u64 ntiles = (count + 1) >> 1;
+  const u64 nw = (u64)gridDim.x * NPW;
+  const u64 t0 = front_slot(blockIdx.x, gridDim.x, wid);
+  const u32 nk = t0 < ntiles ? (u32)((ntiles - t0 + nw - 1) / nw) : 0u;  // tiles tau = t0 + k*nw
+  const uint8_t* safe = reinterpret_cast<const uint8_t*>(gtab);  // 16 readable bytes
+  const bool calc = a.mode == 0u;
+
+  // this lane's message in tile k (present: k < nk and m < count)
+  auto msg_of = [&](u32 k) __attribute__((always_inline)) { return 2 * (t0 + (u64)k * nw) + (u64)h; };
+  // The record of this lane's half in tile k, clamped into the batch (every record load reads
+  // a real record; whether the half holds a message is decided from k and m when used).
+  auto fetch = [&](u32 k, u64& s, u64& L, u64& P) __attribute__((always_inline)) {
+    const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
+    u64 m = nk ? msg_of(kk) : 0;
+    m = m < count ? m : count - 1;
+    s = a.offsets[m * a.ostride];
+    L = a.lengths[m * a.lstride];
+    if constexpr (SLOT) P = a.prefixes[m * a.pstride];
+  };
+  // Extended bytes this kernel reads for tile k's half as a half-tile (0: nothing -- no
+  // message, an empty one, or one longer than a half-tile, computed apart: long_crc).
+  auto ext = [&](u32 k, u64 s, u64 L) __attribute__((always_inline)) -> u32 {
+    const u64 E = L + (s & 15u);
+    return (k < nk && msg_of(k) < count && L != 0 && E <= kSmallMaxExt) ? (u32)E : 0u;
+  };
+  auto load_lines = [&](u32x4 (&D)[8], u64 s, u32 E) __attribute__((always_inline)) {
+    const uint8_t* p0 = E ? base + (s & ~(u64)15) : safe;
+    const u32 lastb = E ? (E - 1u) & ~15u : 0u;  // the block holding the message's last byte
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const u32 off = 128u * l + 16u * (u32)b;
+      D[b] = *reinterpret_cast<const u32x4*>(p0 + (off < lastb ? off : lastb));
+    }
+    // keep the loads at this point, in order (hipcc otherwise sinks them into the compute)
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // Z_{2^b}^{-1} applied for the set bits of `bits` (b < nb <= 12; wave-uniform loop over the
+  // bits any lane has): Z_mis^{-1} and the padding inverses Z_p^{-1}
+  auto inv_bits = [&](u32 x, u32 bits, int nb) __attribute__((always_inline)) {
+    for (int b = 0; b < nb && __any(bits != 0u); b++) {
+      const u32 xm = opmul(sbase, kSmallOpInv + b, x);
+      x = (bits & 1u) ? xm : x;
+      bits >>= 1;
+    }
+    return x;
+  };
+
+  // SLOT: the prefix terms of a slot: H = crc_raw(~0, span 0 || span 1) with the flag word as
+  // stored (kMessageHasChecksum set first for a publish), the flag word F, the stored checksum
+  // S (prefix + 48) and whether the flag was set. Prefixes are 8-B aligned (the C ABI's rule):
+  // 8-B loads.
+  auto span_crc = [&](const uint8_t* pfx, u32& F, u32& S, bool& has) __attribute__((always_inline)) -> u32 {
+    const u64* q = reinterpret_cast<const u64*>(pfx);
+    u32 w[14];
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+      const u64 x = q[i];
+      w[2 * i] = (u32)x;
+      w[2 * i + 1] = (u32)(x >> 32);
+    }
+    has = (w[8] & 4u) != 0u;  // kMessageHasChecksum (common/channel.h:62-70)
+    F = calc ? (w[8] | 4u) : w[8];
+    w[8] = F;
+    S = w[12];
+    u32 hh = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 1; i < 12; i++) hh = step4(hh ^ w[i], lc0, lc1);
+    if (a.metadata_size) {  // wave-uniform: span 1 after the checksum area (crc_uniform.hip)
+      const u32 o1 = 48u + a.checksum_size, sh = o1 & 3u, ms = a.metadata_size;
+      const u32 nwords = (sh + ms + 3u) >> 2;
+      const u32* p1 = reinterpret_cast<const u32*>(pfx + (o1 & ~3u));
+      constexpr u32 kW = kSlotFusedMaxMeta / 4 + 2;
+      u32 W1[kW];
+#pragma unroll
+      for (u32 j = 0; j < kW; j++) {
+        W1[j] = 0u;
+        if (j < nwords) W1[j] = p1[j];
+      }
+      u32 tail = 0;
+#pragma unroll
+      for (u32 j = 0; j + 1 < kW; j++) {
+        const u32 x = __builtin_amdgcn_alignbyte(W1[j + 1], W1[j], sh);
+        if (j < (ms >> 2)) hh = step4(hh ^ x, lc0, lc1);
+        if (j == (ms >> 2)) tail = x;
+      }
+      for (u32 b = 0; b < (ms & 3u); b++) hh = step1(hh, (tail >> (8u * b)) & 0xFFu, lc1);
+    }
+    return hh;
+  };
+
+  // A message longer than a half-tile, by the whole wave (s, L, P wave-uniform): 8 KiB chunks
+  // as the ragged kernel's tiles (lines, line shifts, halves joined by Z_4096), acc =
+  // Z_8192(acc) ^ chunk, the last chunk's padding p = 8192 nt - E < 8192 undone (b < 12 from
+  // LDS, b = 12 from global memory). Returns crc_raw(init, D); SLOT: crc_raw(~0, spans || D),
+  // i.e. Z_L(H) ^ crc_raw(0, D) with L's bits over Z_{2^k} (global).
+  auto long_crc = [&](u64 s, u64 L, u64 P) __attribute__((always_inline)) -> u32 {
+    const u32 mis = (u32)s & 15u;
+    const u64 E = L + mis, nt = (E + 8191) >> 13;
+    const uint8_t* p0 = base + (s & ~(u64)15);
+    const u32 seed = inv_bits(a.init, mis, 4);
+    u32 acc = 0;
+    for (u64 j = 0; j < nt; j++) {
+      const u64 rest = E - (j << 13);
+      const u32 len = rest < 8192 ? (u32)rest : 8192u;
+      const u32 lastb = (len - 1u) & ~15u;
+      const uint8_t* pj = p0 + (j << 13);
+      u32x4 d[8];
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const u32 off = 128u * (u32)lane + 16u * (u32)b;
+        d[b] = *reinterpret_cast<const u32x4*>(pj + (off < lastb ? off : lastb));
+      }
+      const bool hd = j == 0 && mis != 0u && lane == 0;
+      if (__any(hd || len < 8192u)) {
+        const int v0 = (int)len - 128 * lane;
+        const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
+        keep_bytes(d, hd ? mis : 0u, hi);
+      }
+      const u32 crc = line_crc32_2chain(d, (j == 0 && lane == 0) ? seed : 0u, lc0, lc1, z64);
+      u32 v = lane_shift(lop, crc);  // lanes 0-31: bytes 0..4095 of the chunk, 32-63: the rest
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+      const u32 h0 = (u32)__builtin_amdgcn_readlane((int)v, 31), h1 = (u32)__builtin_amdgcn_readlane((int)v, 63);
+      const u32 c = opmul(sbase, kUniSlotOpZ4096, h0) ^ h1;
+      acc = j ? opmul_global(a.rops + kLaneOpWords + 128, acc) ^ c : c;  // Z_8192: the first tile shift
+    }
+    const u32 pad = (u32)((nt << 13) - E);
+    acc = inv_bits(acc, pad & 0xFFFu, kSmallInvOps);
+    if (pad & 0x1000u) acc = opmul_global(a.rops + kRagInvOps + 128 * 12, acc);
+    if constexpr (SLOT) {
+      u32 F, S;
+      bool has;
+      u32 R = span_crc(base + P - a.pdelta, F, S, has);
+      for (int b = 0; b < 64 && (L >> b); b++)
+        if ((L >> b) & 1u) R = opmul_global(a.pow2 + 128 * b, R);
+      acc ^= R;
+    }
+    return acc;
+  };
+
+  // SLOT: store flag + checksum (publish) or the status (verify) of slot m; counts mismatches
+  u32 mism = 0;
+  auto slot_store = [&](bool live, u64 m, const uint8_t* pfx, u32 F, u32 S, bool has, u32 R) __attribute__((always_inline)) {
+    const u32 res = ~R;  // *reinterpret_cast<uint32_t*>(checksum.data()) = ~crc (client/checksum.h:36)
+    if (calc) {
+      if (live) {
+        u32* pw = reinterpret_cast<u32*>(const_cast<uint8_t*>(pfx));
+        pw[8] = F;     // SetHasChecksum()
+        pw[12] = res;
+        if (a.status) a.status[m] = 0u;
+        if (a.crc_out) a.crc_out[m] = res;
+      }
+    } else {
+      const u32 st = !has ? 2u : (res == S ? 0u : 1u);  // client/checksum.h:46
+      if (live && a.status) a.status[m] = st;
+      mism += (u32)__builtin_popcountll(__ballot(live && st == 1u));
+    }
+  };
+
+  // Parked per lane: tile (k & 63)'s two values, codes and (SLOT) prefix offsets.
+  // Code: p = 4096 - E (bits 0-11) | mis << 12 for a half-tile message (value: Z_p(crc_raw(
+  // init, D))); kCodeLong for a longer one (computed by the flush: long_crc); kCodeEmpty for
+  // length 0 (CRC init ^ final_xor; a checksum over the spans only); kCodeSkip for no message.
+  constexpr u32 kCodeLong = 0x20000000u, kCodeEmpty = 0x40000000u, kCodeSkip = 0x80000000u;
+  u32 P0 = 0, P1 = 0, D0 = kCodeSkip, D1 = kCodeSkip;
+  u64 Q0 = 0, Q1 = 0;
+  auto rl64 = [](u64 x, int src) {
+    return ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(x >> 32), src) << 32) |
+           (u64)(u32)__builtin_amdgcn_readlane((int)(u32)x, src);
+  };
+  auto process = [&](const u32x4 (&cur)[8], u64 s, u64 L, u64 P, u32 k) __attribute__((always_inline)) {
+    const u32 mis = (u32)s & 15u;
+    const u32 E = ext(k, s, L);
+    u32x4 d[8];
+#pragma unroll
+    for (int b = 0; b < 8; b++) d[b] = cur[b];
+    // Head: line 0's first mis bytes precede the message. Tail: bytes from E on (the
+    // re-read last block included). Each lane keeps only its line's message bytes.
+    const bool head = E != 0u && mis != 0u && l == 0u;
+    if (__any(head || E < kSmallMaxExt)) {
+      const int v0 = (int)E - 128 * (int)l;
+      const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
+      keep_bytes(d, head ? mis : 0u, hi);
+    }
+    u32 seed = a.init;  // Z_mis^{-1}(init): after the mis masked bytes the state is init
+    if (seed != 0u && __any(head)) seed = inv_bits(seed, mis, 4);
+    const u32 crc = line_crc32_2chain(d, l == 0u ? seed : 0u, lc0, lc1, z64);
+    // line l of half h -> Z_{128*(31-l)}(line), XOR over each half (DPP): lanes 31, 63
+    u32 v = lane_shift(lop, crc);
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    const u64 m = msg_of(k);
+    const bool present = k < nk && m < count;
+    const bool over = present && L + mis > kSmallMaxExt;
+    const u32 code = !present ? kCodeSkip
+                   : over     ? kCodeLong
+                   : L == 0   ? kCodeEmpty
+                              : (kSmallMaxExt - E) | (mis << 12);
+    const bool mine = lane == (int)(k & 63u);
+    P0 = mine ? (u32)__builtin_amdgcn_readlane((int)v, 31) : P0;
+    P1 = mine ? (u32)__builtin_amdgcn_readlane((int)v, 63) : P1;
+    D0 = mine ? (u32)__builtin_amdgcn_readlane((int)code, 0) : D0;
+    D1 = mine ? (u32)__builtin_amdgcn_readlane((int)code, 32) : D1;
+    if constexpr (SLOT) {  // the prefix offsets of halves 0 and 1 (lanes 0 and 32)
+      const u64 q0 = rl64(P, 0), q1 = rl64(P, 32);
+      Q0 = mine ? q0 : Q0;
+      Q1 = mine ? q1 : Q1;
+    }
+  };
+  // Finish and store the parked tiles kf .. kf+nt-1 (lane i holds tile kf + i).
+  auto flush = [&](u32 kf, u32 nt) __attribute__((always_inline)) {
+    const bool valid = (u32)lane < nt;
+    const u64 tau = t0 + (u64)(kf + (u32)lane) * nw;
+    // rare: messages longer than a half-tile, one at a time by the whole wave (one copy of the
+    // code: a loop over both halves' lanes); the owner lane takes the finished value
+    u64 lng[2] = {__ballot(valid && D0 == kCodeLong), __ballot(valid && D1 == kCodeLong)};
+#pragma unroll 1
+    for (u32 hh = 0; hh < 2; hh++) {
+      u64 msk = lng[hh];
+      while (msk) {
+        const u32 src = (u32)__builtin_ctzll(msk);
+        msk &= msk - 1;
+        const u64 m = 2 * (t0 + (u64)(kf + src) * nw) + hh;
+        const u64 s = a.offsets[m * a.ostride], L = a.lengths[m * a.lstride];
+        const u64 P = SLOT ? a.prefixes[m * a.pstride] : 0;
+        const u32 r = long_crc(s, L, P);
+        if (lane == (int)src) {
+          if (hh) P1 = r;
+          else P0 = r;
+        }
+      }
+    }
+#pragma unroll
+    for (u32 hh = 0; hh < 2; hh++) {
+      const u32 v = hh ? P1 : P0;
+      const u32 code = valid ? (hh ? D1 : D0) : kCodeSkip;
+      const u64 m = 2 * tau + hh;
+      const bool half = code < kCodeLong;  // a half-tile message: Z_p undone here
+      if constexpr (SLOT) {
+        const bool live = code != kCodeSkip;
+        const uint8_t* pfx = live ? base + (hh ? Q1 : Q0) - a.pdelta : safe;  // (a read-only block)
+        u32 F, S;
+        bool has;
+        const u32 H = span_crc(pfx, F, S, has);
+        // Z_p(crc_raw(H, payload)) = Z_4096(Z_mis^{-1}(H)) ^ V, then Z_p undone
+        const u32 Hm = inv_bits(H, half ? (code >> 12) & 15u : 0u, 4);
+        const u32 X = opmul(sbase, kUniSlotOpZ4096, Hm) ^ v;
+        const u32 R = half ? inv_bits(X, code & 0xFFFu, kSmallInvOps) : (code == kCodeLong ? v : H);
+        slot_store(live, m, pfx, F, S, has, R);
+      } else {
+        u32 r = inv_bits(v, half ? code & 0xFFFu : 0u, kSmallInvOps);
+        if (code == kCodeEmpty) r = a.init;
+        if (code != kCodeSkip) a.out[m] = r ^ a.final_xor;
+      }
+    }
+  };
+
+  // Prologue: table loads, tile 0's and 1's records, tile 0's lines, then the LDS stores and
+  // the barrier (tile 0's latency hides behind the fill).
+  u64 sA, LA, PA = 0, sB, LB, PB = 0;
+  fetch(0, sA, LA, PA);
+  fetch(1, sB, LB, PB);
+  u32x4 A[8], B[8];
+  u64 sc = sA, Lc = LA, Pc = PA;
+  load_lines(A, sc, ext(0, sc, Lc));
+  fill.store(sbase);
+  if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
+  __syncthreads();
+
+  // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines; the
+  // parked tiles are finished whenever all 64 lanes hold one, right after the next tile's
+  // loads are issued (so the stores retire during that tile's compute), and at the end
+  // (crc_ragged.hip's loop, without descriptors).
+  u32 k = 0;
+  for (; k + 1 < nk; k += 2) {
+    drain_before_issue();  // tile k's lines and tile k+1's record
+    const u64 s1 = sB, L1 = LB, P1r = PB;
+    fetch(k + 2, sA, LA, PA);
+    load_lines(B, s1, ext(k + 1, s1, L1));
+    if (k && (k & 63u) == 0u) flush(k - 64u, 64u);
+    process(A, sc, Lc, Pc, k);
+    drain_before_issue();
+    const u64 s2 = sA, L2 = LA, P2r = PA;
+    fetch(k + 3, sB, LB, PB);
+    load_lines(A, s2, ext(k + 2, s2, L2));
+    process(B, s1, L1, P1r, k + 1);
+    sc = s2;
+    Lc = L2;
+    Pc = P2r;
+  }
+  if (k < nk) {
+    drain_before_issue();
+    if (k && (k & 63u) == 0u) flush(k - 64u, 64u);
+    process(A, sc, Lc, Pc, k);
+  }
+  if (nk) {
+    const u32 kf = (nk - 1u) & ~63u;  // the last window (1..64 tiles), not flushed yet
+    flush(kf, nk - kf);
+  }
+  if constexpr (SLOT) {
+    if (a.error_count && lane == 0) {
+      if (calc) {
+        if (blockIdx.x == 0 && wid == 0) *a.error_count = 0u;  // a publish has no mismatches
+      } else {
+        // the workgroup's count: one 64-bit LDS atomic per wave, (1 << 40) | its count; the
+        // last wave of the workgroup adds the total and one finished workgroup, (1 << 32) |
+        // count, to the call's word; the workgroup that sees G - 1 finished before it writes
+        // the call's total and resets the word
+        const u64 o = __hip_atomic_fetch_add(reinterpret_cast<lds_u64_t*>((uintptr_t)smism), (1ull << 40) | mism,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((u32)(o >> 40) == (u32)NPW - 1u) {
+          const u32 n = (u32)(o + mism);
+          const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(a.counter), (1ull << 32) | (u64)n);
+          if ((u32)(old >> 32) == gridDim.x - 1u) {
+            *a.error_count = (u32)old + n;
+            __hip_atomic_store(a.counter, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+    }
+  } else {
+    // a word the caller's next kernel accumulates into (a slot batch's mismatch count)
+    if (a.zero_word != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.zero_word = 0u;
+  }
+}
+
+template __global__ void crc32_small_kernel<512, false>(const u32*, const u32*, SmallArgs);
+template __global__ void crc32_small_kernel<512, true>(const u32*, const u32*, SmallArgs);
+
+}  // namespace subspace_amd

@@ -362,3 +362,67 @@ def test_r02s3i_prefix_variant_was_in_bounds():
         addrs = [msg * stride + off for off in (4, 20, 36)]
         assert all(a % 16 == 4 for a in addrs)
         assert all(msg * stride <= a and a + 16 <= msg * stride + prefix for a in addrs)
+
+
+# ------------------------------------------------------------------ small-message kernel
+def small_kernel_loads(starts, lengths, G):
+    """Replays crc32_small_kernel<512> (crc_small.hip): per wave (order-0 front, G workgroups x 8
+    waves) the tiles whose lines it loads -- the prologue's tile 0, then tiles k+1 and k+2 per
+    loop pair, clamped records past the wave's last tile -- and per half the 16-B blocks of
+    load_lines: s0 + min(128 l + 16 b, last block) for a half with E = L + (s & 15) in
+    [1, 4096] and L > 0, else the step table's block (None here). Yields (message or None,
+    block address or None); returns nothing else."""
+    count = len(starts)
+    ntiles = (count + 1) // 2
+    nw = 8 * G
+    for b in range(G):
+        for wid in range(8):
+            t0 = front_slot(b, G, wid)
+            nk = (ntiles - t0 + nw - 1) // nw if t0 < ntiles else 0
+            ks = [0]
+            k = 0
+            while k + 1 < nk:
+                ks += [k + 1, k + 2]
+                k += 2
+            for k in ks:
+                for h in (0, 1):
+                    m = 2 * (t0 + k * nw) + h
+                    present = k < nk and m < count
+                    kk = k if k < nk else max(nk - 1, 0)
+                    mr = min(2 * (t0 + kk * nw) + h if nk else 0, count - 1)  # the record read
+                    s, L = int(starts[mr]), int(lengths[mr])
+                    E = L + (s & 15)
+                    if not (present and L and E <= 4096):
+                        yield None, None
+                        continue
+                    assert mr == m
+                    lastb = (E - 1) & ~15
+                    for l in range(32):
+                        for blk in range(8):
+                            yield m, (s & ~15) + min(128 * l + 16 * blk, lastb)
+
+
+@pytest.mark.parametrize("seed,count,G", [(0, 1, 1), (1, 2, 1), (2, 3, 1), (3, 999, 63), (4, 5001, 256),
+                                          (5, 30001, 256)])
+def test_small_kernel_loads_stay_in_messages(seed, count, G):
+    """Every line load of the small-message kernel is a 16-B-aligned block holding at least one
+    byte of its own message (no load outside the caller's messages; messages at any offset &
+    15, empty ones, and ones over a half-tile, which read only the step table), and every byte
+    of every message it computes is loaded."""
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(0, 4097, count)
+    lengths[rng.random(count) < 0.05] = rng.integers(4097, 9000)
+    starts = np.cumsum(np.concatenate([[0], lengths[:-1] + rng.integers(0, 40, count - 1)])) + 7
+    covered = {}
+    for m, addr in small_kernel_loads(starts, lengths, G):
+        if m is None:
+            continue
+        s, e = int(starts[m]), int(starts[m] + lengths[m])
+        assert addr % 16 == 0 and addr + 16 > s and addr < e, (m, s, e, addr)
+        if count <= 5001:
+            covered.setdefault(m, set()).update(range(max(addr, s), min(addr + 16, e)))
+    if count <= 5001:
+        for m in range(count):
+            s, L = int(starts[m]), int(lengths[m])
+            if L and L + (s & 15) <= 4096:
+                assert covered.get(m) == set(range(s, s + L)), m

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/../.."
 mkdir -p tools/ubench/probes/obj
 for n in "$@"; do
   objs=""
-  for f in crc_uniform crc_ragged crc_long crc_combine crc_slots capi testutil; do
+  for f in crc_uniform crc_small crc_ragged crc_long crc_combine crc_slots capi testutil; do
     o=tools/ubench/probes/obj/${f}_v$n.o
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -DSUBSPACE_SLOT_VARIANT=$n -c subspace_amd/csrc/$f.hip -o $o &
     objs="$objs $o"
