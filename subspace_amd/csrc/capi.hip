@@ -301,6 +301,10 @@ int ensure_ragged_ws(subspace_crc_ctx* c, u64 messages, u64 tiles) {
     c->scan_b_words = ceil_div(tile_geom(c, c->desc_capacity).nseg, kScanTile);
     HIP_TRY(hipMalloc(&c->d_scan_state, (1 + c->scan_a_words + c->scan_b_words) * sizeof(u64)));
     HIP_TRY(hipMemset(c->d_scan_state, 0, (1 + c->scan_a_words + c->scan_b_words) * sizeof(u64)));
+    // hipMemset runs on the null stream, which does not order non-blocking streams (the
+    // host-slot pipeline's compute stream, a caller's): finish it before any scan can start
+    // (a scan that ran first read a recycled allocation's stale ticket, r03ac)
+    HIP_TRY(hipDeviceSynchronize());
     c->scan_dirty = false;
   }
   if (!c->d_overflow) HIP_TRY(hipMalloc(&c->d_overflow, 16));
@@ -427,7 +431,10 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
   a.out = out;
   a.rops = c->d_rops;
   a.pow2 = c->d_pow2;
-  const unsigned blocks = (unsigned)grid_for(c, (count + 1) / 2, 8);
+  // one workgroup per CU, more for batches that would give a wave more than 64 tiles
+  const u64 tiles = (count + 1) / 2;
+  const unsigned blocks =
+      (unsigned)std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSmallMaxTilesPerWave));
   const size_t lds = small_lds_bytes() + 16;
   if (slot) {
     a.prefixes = slot->prefixes;
@@ -601,6 +608,8 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess) e = hipMalloc(&c->d_fault, 4 * sizeof(u32));
   if (e == hipSuccess) e = hipMemset(c->d_fault, 0, 4 * sizeof(u32));
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ws_done, hipEventDisableTiming);
+  // the zeroed words above must be zero before a kernel on a non-blocking stream reads them
+  if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_ragged_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)ragged_lds_bytes());

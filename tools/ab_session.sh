@@ -8,6 +8,8 @@
 #   mode: slotgap -- tools/slot_gap.py: config S publish / verify vs the plain kernel over the
 #                    same buffers (timing only: variants may compute nothing valid)
 #         uniform -- tools/sweep_uniform.py: config B through the uniform kernel
+#         slotlist -- tools/slot_list_order.py: config S verified strided (fused uniform) and
+#                     as an ordered / shuffled slot list (small-message kernel)
 # Summaries: python tools/show_ab.py gpurun_out/<tag>
 set -u
 TAG=$1; MODE=$2; shift 2
@@ -16,6 +18,8 @@ mkdir -p $OUT
 run() {  # $1 = output stem, $2 = library path or ""
   if [ "$MODE" = slotgap ]; then
     SUBSPACE_CRC_PROBE_LIB=$2 SLOT_GAP_NOCHECK=1 timeout -k 10 200 python tools/slot_gap.py 3 > $OUT/$1.jsonl 2> $OUT/$1.err
+  elif [ "$MODE" = slotlist ]; then
+    SUBSPACE_CRC_PROBE_LIB=$2 timeout -k 10 200 python tools/slot_list_order.py 3 > $OUT/$1.jsonl 2> $OUT/$1.err
   else
     SUBSPACE_CRC_PROBE_LIB=$2 timeout -k 10 200 python tools/sweep_uniform.py 65536 512 7 0 > $OUT/$1.jsonl 2> $OUT/$1.err
   fi
