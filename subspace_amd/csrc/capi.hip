@@ -431,10 +431,7 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
   a.out = out;
   a.rops = c->d_rops;
   a.pow2 = c->d_pow2;
-  // one workgroup per CU, more for batches that would give a wave more than 64 tiles
-  const u64 tiles = (count + 1) / 2;
-  const unsigned blocks =
-      (unsigned)std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSmallMaxTilesPerWave));
+  const unsigned blocks = (unsigned)grid_for(c, (count + 1) / 2, 8);  // persistent: one per CU at most
   const size_t lds = small_lds_bytes() + 16;
   if (slot) {
     a.prefixes = slot->prefixes;

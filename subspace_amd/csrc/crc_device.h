@@ -118,7 +118,6 @@ constexpr int kSmallOpInv = kUniOpSlots;
 constexpr int kSmallInvOps = 12;
 constexpr int kSmallOpSlots = kSmallOpInv + kSmallInvOps;
 constexpr u32 kSmallMaxExt = 4096;  // extended bytes (length + offset & 15) of one half-tile
-constexpr u32 kSmallMaxTilesPerWave = 64;  // one parked tile per lane: the grid gives no wave more
 constexpr size_t small_lds_bytes() { return kLdsOps + (size_t)kSmallOpSlots * 512u; }
 static_assert(small_lds_bytes() <= 160u * 1024u, "small-message kernel LDS exceeds 160 KiB");
 

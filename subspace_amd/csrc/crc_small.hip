@@ -23,9 +23,8 @@
 //    table. Loads never touch a 16-B block that holds no byte of the message.
 //  * Line 0 starts from seed = Z_mis^{-1}(init), every other line from 0, so each half gives
 //      V = crc_raw(seed, 0^mis || D || 0^p) = Z_p(crc_raw(init, D)),   p = 4096 - E;
-//    values are parked one tile per lane (lane k keeps tile k's two values and codes: a wave
-//    has at most kSmallMaxTilesPerWave = 64 tiles, the host sizes the grid for that), and
-//    after the tile loop each lane undoes the padding of its two messages with p's bits over
+//    values are parked one tile per lane (lane k & 63 keeps tile k's two values and codes),
+//    and every 64 tiles each lane undoes the padding of its two messages with p's bits over
 //    the inverse operators Z_{2^b}^{-1}, b < 12 (LDS), and stores the CRCs.
 //  * SLOT: the message-slot checksum (client/checksum.h:29-47 over common/channel.h:527-542's
 //    spans) in the same flush, from init 0: with H = crc_raw(~0, span 0 || span 1) from the
@@ -45,13 +44,6 @@
 //    counts finished workgroups; the last one writes the call's total and resets the word
 //    (the fused uniform slot kernel's scheme: no fences, no memset).
 #include "crc_device.h"
-
-// Timing-only A/B builds (tools/ab_lib.sh SRC=crc_small -DSUBSPACE_SMALL_VARIANT=n; the product
-// build is 0): 1 puts the 64-tile flush back inside the tile loop (never taken with the
-// product grid: it measures the code's presence alone).
-#ifndef SUBSPACE_SMALL_VARIANT
-#define SUBSPACE_SMALL_VARIANT 0
-#endif
 
 namespace subspace_amd {
 
@@ -277,7 +269,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
                    : over     ? kCodeLong
                    : L == 0   ? kCodeEmpty
                               : (kSmallMaxExt - E) | (mis << 12);
-    const bool mine = lane == (int)k;
+    const bool mine = lane == (int)(k & 63u);
     P0 = mine ? (u32)__builtin_amdgcn_readlane((int)v, 31) : P0;
     P1 = mine ? (u32)__builtin_amdgcn_readlane((int)v, 63) : P1;
     D0 = mine ? (u32)__builtin_amdgcn_readlane((int)code, 0) : D0;
@@ -348,18 +340,19 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
   __syncthreads();
 
-  // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines
-  // (crc_ragged.hip's loop, without descriptors). A wave has at most 64 tiles (the host
-  // launches more workgroups for longer batches), one per lane, so the parked tiles are
-  // finished once, after the loop: the loop holds nothing but the stream (finishing code in
-  // it cost ~10 us per 65,536-message launch, as in the uniform kernel).
+  // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines; the
+  // parked tiles are finished whenever all 64 lanes hold one, right after the next tile's
+  // loads are issued (so the stores retire during that tile's compute), and at the end
+  // (crc_ragged.hip's loop, without descriptors). (A grid giving no wave more than 64 tiles,
+  // with the flush only after the loop, ran 2.8 us slower per 65,536-slot list in an
+  // interleaved A/B, r03af: hipcc's code for the loop changed)
   u32 k = 0;
   for (; k + 1 < nk; k += 2) {
     drain_before_issue();  // tile k's lines and tile k+1's record
     const u64 s1 = sB, L1 = LB, P1r = PB;
     fetch(k + 2, sA, LA, PA);
     load_lines(B, s1, ext(k + 1, s1, L1));
-    if (SUBSPACE_SMALL_VARIANT == 1 && k && (k & 63u) == 0u) flush(k - 64u, 64u);
+    if (k && (k & 63u) == 0u) flush(k - 64u, 64u);
     process(A, sc, Lc, Pc, k);
     drain_before_issue();
     const u64 s2 = sA, L2 = LA, P2r = PA;
@@ -372,9 +365,13 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   }
   if (k < nk) {
     drain_before_issue();
+    if (k && (k & 63u) == 0u) flush(k - 64u, 64u);
     process(A, sc, Lc, Pc, k);
   }
-  if (nk) flush(0u, nk);
+  if (nk) {
+    const u32 kf = (nk - 1u) & ~63u;  // the last window (1..64 tiles), not flushed yet
+    flush(kf, nk - kf);
+  }
   if constexpr (SLOT) {
     if (a.error_count && lane == 0) {
       if (calc) {

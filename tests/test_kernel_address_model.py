@@ -379,7 +379,6 @@ def small_kernel_loads(starts, lengths, G):
         for wid in range(8):
             t0 = front_slot(b, G, wid)
             nk = (ntiles - t0 + nw - 1) // nw if t0 < ntiles else 0
-            assert nk <= 64  # one parked tile per lane (kSmallMaxTilesPerWave)
             ks = [0]
             k = 0
             while k + 1 < nk:
@@ -428,17 +427,3 @@ def test_small_kernel_loads_stay_in_messages(seed, count, G):
             if L and L + (s & 15) <= 4096:
                 assert covered.get(m) == set(range(s, s + L)), m
 
-
-def small_grid(count, num_cus=256):
-    """capi.hip small_run: one 8-wave workgroup per CU up to the tile count, more when a wave
-    would get more than 64 tiles (kSmallMaxTilesPerWave: one parked tile per lane)."""
-    tiles = (count + 1) // 2
-    return max(max(1, min(num_cus, (tiles + 7) // 8)), (tiles + 8 * 64 - 1) // (8 * 64))
-
-
-@pytest.mark.parametrize("count", [1, 2, 3, 16383, 65536, 65537, 262145, 1 << 20, (1 << 31) + 5, (1 << 32) - 1])
-def test_small_grid_gives_no_wave_more_than_64_tiles(count):
-    G = small_grid(count)
-    ntiles, nw = (count + 1) // 2, 8 * G
-    assert (ntiles + nw - 1) // nw <= 64  # the most tiles any wave gets (front slot 0)
-    assert G < 2**32
