@@ -823,18 +823,20 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
   if (!dev_slots) return fail(SUBSPACE_CRC_EINVAL, "null device pointer");
   if (count >= (1ull << 32)) return fail(SUBSPACE_CRC_EINVAL, "count %llu exceeds 2^32-1", (unsigned long long)count);
   HIP_TRY(hipSetDevice(c->device));
-  rc = use_workspace(c, st);
-  if (rc) return rc;
-  rc = ensure_slot_ws(c, count);
-  if (rc) return rc;
   // payload CRCs from init 0 at absolute addresses (base 0; fields 1 and 2 of each record):
   // slots of at most 4 KiB through the small-message kernel, larger ones the ragged path
   const u64* rec = reinterpret_cast<const u64*>(dev_slots);
   const bool small = max_message_size <= kSmallMaxExt && c->small_path;
-  if (small && small_slot_fused(checksum_size, metadata_size)) {  // one kernel, slots finished in it
+  if (small && small_slot_fused(checksum_size, metadata_size)) {
+    // one kernel, the slots finished in it; no context workspace (the counter ring, as the
+    // fused uniform slot kernel)
     const SmallSlot ss{rec, 3, 0, mode, checksum_size, metadata_size, dev_status, nullptr, dev_error_count};
     return small_run(c, nullptr, rec + 1, 3, rec + 2, 3, count, 0u, 0u, nullptr, st, &ss);
   }
+  rc = use_workspace(c, st);
+  if (rc) return rc;
+  rc = ensure_slot_ws(c, count);
+  if (rc) return rc;
   want_zeroed(c, dev_error_count);
   if (small) {
     rc = small_run(c, nullptr, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st);

@@ -155,3 +155,53 @@ def test_slot_list_all_long_then_none(gpu_ctx, oracle):
     arena, po, yo = oracle_arena(pre, pay, pay_off, 2001, ps)
     oracle.publish_slots(arena, po, yo, sizes, cs, ms)
     assert np.array_equal(got_pre, arena[:len(pre)])
+
+
+def test_small_paths_graph_capture(gpu_ctx, oracle):
+    """The fused small-slot kernel (no context workspace: a counter word of the ring) and a
+    small uniform batch (offsets materialised once beforehand) captured into a HIP graph and
+    replayed; a payload byte flipped between replays must flip exactly that slot's status and
+    the mismatch count (the captured counter word is back at 0 after every replay)."""
+    count, cs, ms = 2001, 4, 16
+    pre, pay, pay_off, sizes, order, ps = build_slot_list(count, 99, cs, ms, 4096)
+    got_pre, _, _ = run_slot_list(gpu_ctx, pre, pay, pay_off, sizes, order, ps, cs, ms, 4096, gpu.SLOT_CALCULATE)
+    d_pre = torch.from_numpy(got_pre.copy()).to(DEV)
+    d_pay = torch.from_numpy(pay.copy()).to(DEV)
+    rec = slots.slot_records(d_pre.data_ptr() + order.astype(np.uint64) * np.uint64(ps),
+                             d_pay.data_ptr() + pay_off[order], sizes[order])
+    d_rec = torch.from_numpy(rec.view(np.int64)).to(DEV)
+    status = torch.full((count,), 7, dtype=torch.int32, device=DEV)
+    err = torch.full((1,), 12345, dtype=torch.int32, device=DEV)
+    n, L, stride = 999, 777, 781
+    ubuf = torch.empty(stride * (n - 1) + L, dtype=torch.uint8, device=DEV)
+    gpu.fill_uniform(ubuf, stride, L, n, seed=0x5A14)
+    uout = torch.zeros(n, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_uniform(ubuf, stride, L, n, uout)  # allocates the materialised offsets
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            gpu_ctx.crc32_slots(d_rec, max_message_size=4096, checksum_size=cs, metadata_size=ms,
+                                mode=gpu.SLOT_VERIFY, status=status, error_count=err)
+            gpu_ctx.crc32_uniform(ubuf, stride, L, n, uout)
+    torch.cuda.synchronize()
+    want_u = expected_uniform(oracle, n, L, 0x5A14)
+    victim = int(np.nonzero(sizes > 0)[0][3])  # a slot with a payload (slot order)
+    pos = int(order.tolist().index(victim))    # its record
+    for flipped in (False, True, False):
+        if flipped:
+            d_pay[int(pay_off[victim])] ^= 0x40
+        elif d_pay[int(pay_off[victim])].item() != pay[int(pay_off[victim])]:
+            d_pay[int(pay_off[victim])] ^= 0x40
+        uout.zero_()
+        err.fill_(12345)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        st = status.cpu().numpy().view(np.uint32)
+        assert int(err.item()) == (1 if flipped else 0)
+        assert st[pos] == (1 if flipped else 0) and int((st != 0).sum()) == (1 if flipped else 0)
+        assert np.array_equal(uout.cpu().numpy().view(np.uint32), want_u)
+    gpu_ctx.check()
