@@ -118,7 +118,10 @@ constexpr int kSmallOpInv = kUniOpSlots;
 constexpr int kSmallInvOps = 12;
 constexpr int kSmallOpSlots = kSmallOpInv + kSmallInvOps;
 constexpr u32 kSmallMaxExt = 4096;  // extended bytes (length + offset & 15) of one half-tile
-constexpr size_t small_lds_bytes() { return kLdsOps + (size_t)kSmallOpSlots * 512u; }
+constexpr u32 kSmallRing = kLdsOps + (u32)kSmallOpSlots * 512u;  // per-wave result rings
+constexpr u32 kSmallRingTiles = 32;                               // tiles per ring window
+constexpr u32 kSmallRingBytesPerWave = kSmallRingTiles * 2u * 8u;  // (value | code << 32) per message
+constexpr size_t small_lds_bytes() { return kSmallRing + 8u * kSmallRingBytesPerWave; }
 static_assert(small_lds_bytes() <= 160u * 1024u, "small-message kernel LDS exceeds 160 KiB");
 
 // Small-message kernel arguments (crc_small.hip; one struct: read with scalar loads).

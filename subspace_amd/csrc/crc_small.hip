@@ -23,9 +23,9 @@
 //    table. Loads never touch a 16-B block that holds no byte of the message.
 //  * Line 0 starts from seed = Z_mis^{-1}(init), every other line from 0, so each half gives
 //      V = crc_raw(seed, 0^mis || D || 0^p) = Z_p(crc_raw(init, D)),   p = 4096 - E;
-//    values are parked one tile per lane (lane k & 63 keeps tile k's two values and codes),
-//    and every 64 tiles each lane undoes the padding of its two messages with p's bits over
-//    the inverse operators Z_{2^b}^{-1}, b < 12 (LDS), and stores the CRCs.
+//    each message's value and code are parked in a per-wave LDS ring (32 tiles), and every 32
+//    tiles each lane takes one message of the ring, undoes its padding with p's bits over the
+//    inverse operators Z_{2^b}^{-1}, b < 12 (LDS), and stores the CRC.
 //  * SLOT: the message-slot checksum (client/checksum.h:29-47 over common/channel.h:527-542's
 //    spans) in the same flush, from init 0: with H = crc_raw(~0, span 0 || span 1) from the
 //    prefix (the flag set first for a publish, client/publisher.cc:664-675),
@@ -45,7 +45,9 @@
 //    (the fused uniform slot kernel's scheme: no fences, no memset).
 #include "crc_device.h"
 
+
 namespace subspace_amd {
+
 
 template <int WG, bool SLOT>
 __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__ gtab, const u32* __restrict__ gops,
@@ -60,6 +62,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   const int lane = threadIdx.x & 63;
   const u32 wid = rfl(threadIdx.x >> 6);
   const u32 l = (u32)lane & 31u, h = (u32)lane >> 5;
+  const u32 sring = sbase + kSmallRing + wid * kSmallRingBytesPerWave;  // this wave's result ring
   const u32 lc0 = sbase + (l << 2), lc1 = lc0 + 0x10000u;
   const u32 lop = sbase + kLdsOps + 4u * (31u - l);  // this lane's line-shift operator
   const u32 z64 = sbase + kLdsOps + 512u * (u32)kUniSlotOpZ64 + 4u * (u32)(lane & 3);
@@ -76,13 +79,12 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   auto msg_of = [&](u32 k) __attribute__((always_inline)) { return 2 * (t0 + (u64)k * nw) + (u64)h; };
   // The record of this lane's half in tile k, clamped into the batch (every record load reads
   // a real record; whether the half holds a message is decided from k and m when used).
-  auto fetch = [&](u32 k, u64& s, u64& L, u64& P) __attribute__((always_inline)) {
+  auto fetch = [&](u32 k, u64& s, u64& L) __attribute__((always_inline)) {
     const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
     u64 m = nk ? msg_of(kk) : 0;
     m = m < count ? m : count - 1;
     s = a.offsets[m * a.ostride];
     L = a.lengths[m * a.lstride];
-    if constexpr (SLOT) P = a.prefixes[m * a.pstride];
   };
   // Extended bytes this kernel reads for tile k's half as a half-tile (0: nothing -- no
   // message, an empty one, or one longer than a half-tile, computed apart: long_crc).
@@ -227,18 +229,12 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
   };
 
-  // Parked per lane: tile (k & 63)'s two values, codes and (SLOT) prefix offsets.
+  // Each message's value and code are parked in the wave's LDS ring, entry 2 (k & 31) + h.
   // Code: p = 4096 - E (bits 0-11) | mis << 12 for a half-tile message (value: Z_p(crc_raw(
   // init, D))); kCodeLong for a longer one (computed by the flush: long_crc); kCodeEmpty for
   // length 0 (CRC init ^ final_xor; a checksum over the spans only); kCodeSkip for no message.
   constexpr u32 kCodeLong = 0x20000000u, kCodeEmpty = 0x40000000u, kCodeSkip = 0x80000000u;
-  u32 P0 = 0, P1 = 0, D0 = kCodeSkip, D1 = kCodeSkip;
-  u64 Q0 = 0, Q1 = 0;
-  auto rl64 = [](u64 x, int src) {
-    return ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(x >> 32), src) << 32) |
-           (u64)(u32)__builtin_amdgcn_readlane((int)(u32)x, src);
-  };
-  auto process = [&](const u32x4 (&cur)[8], u64 s, u64 L, u64 P, u32 k) __attribute__((always_inline)) {
+  auto process = [&](const u32x4 (&cur)[8], u64 s, u64 L, u32 k) __attribute__((always_inline)) {
     const u32 mis = (u32)s & 15u;
     const u32 E = ext(k, s, L);
     u32x4 d[8];
@@ -269,107 +265,93 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
                    : over     ? kCodeLong
                    : L == 0   ? kCodeEmpty
                               : (kSmallMaxExt - E) | (mis << 12);
-    const bool mine = lane == (int)(k & 63u);
-    P0 = mine ? (u32)__builtin_amdgcn_readlane((int)v, 31) : P0;
-    P1 = mine ? (u32)__builtin_amdgcn_readlane((int)v, 63) : P1;
-    D0 = mine ? (u32)__builtin_amdgcn_readlane((int)code, 0) : D0;
-    D1 = mine ? (u32)__builtin_amdgcn_readlane((int)code, 32) : D1;
-    if constexpr (SLOT) {  // the prefix offsets of halves 0 and 1 (lanes 0 and 32)
-      const u64 q0 = rl64(P, 0), q1 = rl64(P, 32);
-      Q0 = mine ? q0 : Q0;
-      Q1 = mine ? q1 : Q1;
-    }
+    // lane 31 of each half: its message's value and code, one 8-B LDS store
+    if (l == 31u) lds_st64(sring + 8u * (2u * (k & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
   };
-  // Finish and store the parked tiles kf .. kf+nt-1 (lane i holds tile kf + i).
+  // Finish and store the ring's tiles kf .. kf+nt-1 (nt <= 32): lane i takes message i of the
+  // window, i.e. tile kf + i/2, half i & 1 (its value and code from the ring; a slot's prefix
+  // offset from its record again).
   auto flush = [&](u32 kf, u32 nt) __attribute__((always_inline)) {
-    const bool valid = (u32)lane < nt;
-    const u64 tau = t0 + (u64)(kf + (u32)lane) * nw;
-    // rare: messages longer than a half-tile, one at a time by the whole wave (one copy of the
-    // code: a loop over both halves' lanes); the owner lane takes the finished value
-    u64 lng[2] = {__ballot(valid && D0 == kCodeLong), __ballot(valid && D1 == kCodeLong)};
-#pragma unroll 1
-    for (u32 hh = 0; hh < 2; hh++) {
-      u64 msk = lng[hh];
-      while (msk) {
-        const u32 src = (u32)__builtin_ctzll(msk);
-        msk &= msk - 1;
-        const u64 m = 2 * (t0 + (u64)(kf + src) * nw) + hh;
-        const u64 s = a.offsets[m * a.ostride], L = a.lengths[m * a.lstride];
-        const u64 P = SLOT ? a.prefixes[m * a.pstride] : 0;
-        const u32 r = long_crc(s, L, P);
-        if (lane == (int)src) {
-          if (hh) P1 = r;
-          else P0 = r;
-        }
-      }
+    wave_lds_sync();
+    const u32 hh = (u32)lane & 1u, ti = (u32)lane >> 1;
+    const bool valid = ti < nt;
+    const u64 e = lds_ld64(sring + 8u * (u32)lane);
+    u32 v = (u32)e;
+    const u32 code = valid ? (u32)(e >> 32) : kCodeSkip;
+    const u64 m = 2 * (t0 + (u64)(kf + ti) * nw) + hh;
+    const u64 mc = code != kCodeSkip ? m : 0;  // (a real record for every lane)
+    // rare: messages longer than a half-tile, one at a time by the whole wave
+    u64 msk = __ballot(code == kCodeLong);
+    while (msk) {
+      const u32 src = (u32)__builtin_ctzll(msk);
+      msk &= msk - 1;
+      const u64 ms = 2 * (t0 + (u64)(kf + (src >> 1)) * nw) + (src & 1u);
+      const u64 s = a.offsets[ms * a.ostride], L = a.lengths[ms * a.lstride];
+      const u64 P = SLOT ? a.prefixes[ms * a.pstride] : 0;
+      const u32 r = long_crc(s, L, P);
+      v = lane == (int)src ? r : v;
     }
-#pragma unroll
-    for (u32 hh = 0; hh < 2; hh++) {
-      const u32 v = hh ? P1 : P0;
-      const u32 code = valid ? (hh ? D1 : D0) : kCodeSkip;
-      const u64 m = 2 * tau + hh;
-      const bool half = code < kCodeLong;  // a half-tile message: Z_p undone here
-      if constexpr (SLOT) {
-        const bool live = code != kCodeSkip;
-        const uint8_t* pfx = live ? base + (hh ? Q1 : Q0) - a.pdelta : safe;  // (a read-only block)
-        u32 F, S;
-        bool has;
-        const u32 H = span_crc(pfx, F, S, has);
-        // Z_p(crc_raw(H, payload)) = Z_4096(Z_mis^{-1}(H)) ^ V, then Z_p undone
-        const u32 Hm = inv_bits(H, half ? (code >> 12) & 15u : 0u, 4);
-        const u32 X = opmul(sbase, kUniSlotOpZ4096, Hm) ^ v;
-        const u32 R = half ? inv_bits(X, code & 0xFFFu, kSmallInvOps) : (code == kCodeLong ? v : H);
-        slot_store(live, m, pfx, F, S, has, R);
-      } else {
-        u32 r = inv_bits(v, half ? code & 0xFFFu : 0u, kSmallInvOps);
-        if (code == kCodeEmpty) r = a.init;
-        if (code != kCodeSkip) a.out[m] = r ^ a.final_xor;
-      }
+    const bool half = code < kCodeLong;  // a half-tile message: Z_p undone here
+    if constexpr (SLOT) {
+      const bool live = code != kCodeSkip;
+      const uint8_t* pfx = live ? base + a.prefixes[mc * a.pstride] - a.pdelta : safe;  // (a read-only block)
+      u32 F, S;
+      bool has;
+      const u32 H = span_crc(pfx, F, S, has);
+      // Z_p(crc_raw(H, payload)) = Z_4096(Z_mis^{-1}(H)) ^ V, then Z_p undone
+      const u32 Hm = inv_bits(H, half ? (code >> 12) & 15u : 0u, 4);
+      const u32 X = opmul(sbase, kUniSlotOpZ4096, Hm) ^ v;
+      const u32 R = half ? inv_bits(X, code & 0xFFFu, kSmallInvOps) : (code == kCodeLong ? v : H);
+      slot_store(live, m, pfx, F, S, has, R);
+    } else {
+      u32 r = inv_bits(v, half ? code & 0xFFFu : 0u, kSmallInvOps);
+      if (code == kCodeEmpty) r = a.init;
+      if (code != kCodeSkip) a.out[m] = r ^ a.final_xor;
     }
+    wave_lds_sync();
   };
+  constexpr u32 kWinMask = kSmallRingTiles - 1u;
 
   // Prologue: table loads, tile 0's and 1's records, tile 0's lines, then the LDS stores and
   // the barrier (tile 0's latency hides behind the fill).
-  u64 sA, LA, PA = 0, sB, LB, PB = 0;
-  fetch(0, sA, LA, PA);
-  fetch(1, sB, LB, PB);
+  u64 sA, LA, sB, LB;
+  fetch(0, sA, LA);
+  fetch(1, sB, LB);
   u32x4 A[8], B[8];
-  u64 sc = sA, Lc = LA, Pc = PA;
+  u64 sc = sA, Lc = LA;
   load_lines(A, sc, ext(0, sc, Lc));
   fill.store(sbase);
   if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
   __syncthreads();
 
   // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines; the
-  // parked tiles are finished whenever all 64 lanes hold one, right after the next tile's
-  // loads are issued (so the stores retire during that tile's compute), and at the end
-  // (crc_ragged.hip's loop, without descriptors). (A grid giving no wave more than 64 tiles,
-  // with the flush only after the loop, ran 2.8 us slower per 65,536-slot list in an
-  // interleaved A/B, r03af: hipcc's code for the loop changed)
+  // ring is finished whenever it holds 32 tiles, right after the next tile's loads are issued
+  // (so the stores retire during that tile's compute), and at the end (crc_ragged.hip's loop,
+  // without descriptors). Nothing else lives across the loop (register-parked
+  // values, 64-tile windows and a flush only after the loop each measured slower).
   u32 k = 0;
   for (; k + 1 < nk; k += 2) {
     drain_before_issue();  // tile k's lines and tile k+1's record
-    const u64 s1 = sB, L1 = LB, P1r = PB;
-    fetch(k + 2, sA, LA, PA);
+    const u64 s1 = sB, L1 = LB;
+    fetch(k + 2, sA, LA);
     load_lines(B, s1, ext(k + 1, s1, L1));
-    if (k && (k & 63u) == 0u) flush(k - 64u, 64u);
-    process(A, sc, Lc, Pc, k);
+    if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
+    process(A, sc, Lc, k);
     drain_before_issue();
-    const u64 s2 = sA, L2 = LA, P2r = PA;
-    fetch(k + 3, sB, LB, PB);
+    const u64 s2 = sA, L2 = LA;
+    fetch(k + 3, sB, LB);
     load_lines(A, s2, ext(k + 2, s2, L2));
-    process(B, s1, L1, P1r, k + 1);
+    process(B, s1, L1, k + 1);
     sc = s2;
     Lc = L2;
-    Pc = P2r;
   }
   if (k < nk) {
     drain_before_issue();
-    if (k && (k & 63u) == 0u) flush(k - 64u, 64u);
-    process(A, sc, Lc, Pc, k);
+    if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
+    process(A, sc, Lc, k);
   }
   if (nk) {
-    const u32 kf = (nk - 1u) & ~63u;  // the last window (1..64 tiles), not flushed yet
+    const u32 kf = (nk - 1u) & ~kWinMask;  // the last window, not flushed yet
     flush(kf, nk - kf);
   }
   if constexpr (SLOT) {
