@@ -19,7 +19,7 @@ run() {  # $1 = output stem, $2 = library path or ""
   if [ "$MODE" = slotgap ]; then
     SUBSPACE_CRC_PROBE_LIB=$2 SLOT_GAP_NOCHECK=1 timeout -k 10 200 python tools/slot_gap.py 3 > $OUT/$1.jsonl 2> $OUT/$1.err
   elif [ "$MODE" = slotlist ]; then
-    SUBSPACE_CRC_PROBE_LIB=$2 timeout -k 10 200 python tools/slot_list_order.py 3 > $OUT/$1.jsonl 2> $OUT/$1.err
+    SUBSPACE_CRC_PROBE_LIB=$2 SLOT_LIST_NOCHECK=1 timeout -k 10 200 python tools/slot_list_order.py 3 > $OUT/$1.jsonl 2> $OUT/$1.err
   else
     SUBSPACE_CRC_PROBE_LIB=$2 timeout -k 10 200 python tools/sweep_uniform.py 65536 512 7 0 > $OUT/$1.jsonl 2> $OUT/$1.err
   fi
