@@ -45,9 +45,7 @@
 //    (the fused uniform slot kernel's scheme: no fences, no memset).
 #include "crc_device.h"
 
-
 namespace subspace_amd {
-
 
 template <int WG, bool SLOT>
 __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__ gtab, const u32* __restrict__ gops,
@@ -366,7 +364,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
         const u64 o = __hip_atomic_fetch_add(reinterpret_cast<lds_u64_t*>((uintptr_t)smism), (1ull << 40) | mism,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if ((u32)(o >> 40) == (u32)NPW - 1u) {
-          const u32 n = (u32)(o + mism);
+          const u32 n = (u32)((o & ((1ull << 40) - 1)) + mism);  // the workgroup's mismatches
           const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(a.counter), (1ull << 32) | (u64)n);
           if ((u32)(old >> 32) == gridDim.x - 1u) {
             *a.error_count = (u32)old + n;
