@@ -430,6 +430,34 @@ class RoctxRegion:
             self.lib.roctxProfilerPause(0)
 
 
+SETTLE_CAP_S = 20.0
+
+
+def launch_rate_steady(blocks, window_s=1.0, tol=0.003):
+    """True when the last window_s seconds of (seconds, launches) blocks have a steady launch
+    rate: the newer half's mean time per launch is not below the older half's by more than tol
+    (still speeding up = not steady)."""
+    win = []
+    for blk in reversed(blocks):
+        win.append(blk)
+        if sum(x for x, _ in win) >= window_s:
+            break
+    total = sum(x for x, _ in win)
+    if total < window_s:
+        return False
+    newer, acc = [], 0.0
+    for blk in win:
+        if acc >= total / 2:
+            break
+        acc += blk[0]
+        newer.append(blk)
+    older = win[len(newer):]
+    if not older:
+        return False
+    per = lambda b: sum(x for x, _ in b) / sum(n for _, n in b)  # noqa: E731
+    return per(newer) >= per(older) * (1.0 - tol)
+
+
 def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, region_marks=None, settle_s=0.0):
     """W untimed warm-up steps (after settle launches: at least `settle` - W of them and at
     least `settle_s` seconds of them), then EXACTLY `steps` steps between barrier +
@@ -439,11 +467,20 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, re
     import torch
     stream = streams[0]
     n_settle, t_settle = 0, time.perf_counter()
-    while n_settle < max(0, settle - warmup) or time.perf_counter() - t_settle < settle_s:
+    # ... and, up to SETTLE_CAP_S, until the launch rate is steady: the mean time per launch of
+    # the last 0.5 s within 0.3 % of the 0.5 s before. VRAM freed to the driver (by this or an
+    # earlier process, e.g. a test run's 118 GB config-C buffer) is wiped in the background for
+    # several seconds, and every HBM-bound kernel runs 2-4 % slower meanwhile (DESIGN.md 6,
+    # tools/s_launches.py, r03s4-r03s6)
+    blocks = []  # (seconds, launches) per block of back-to-back launches
+    while (n_settle < max(0, settle - warmup) or time.perf_counter() - t_settle < settle_s or
+           (settle_s > 0 and not launch_rate_steady(blocks) and time.perf_counter() - t_settle < SETTLE_CAP_S)):
+        t_blk = time.perf_counter()
         for _ in range(50):  # back to back; the clock is read with a sync every 50 launches
             wl.step(n_settle, streams)
             n_settle += 1
         torch.cuda.synchronize()
+        blocks.append((time.perf_counter() - t_blk, 50))
     for i in range(warmup):
         wl.step(i, streams)
     torch.cuda.synchronize()
@@ -566,12 +603,15 @@ def secondary_configs(ctx, dev, names, iters) -> dict:
         elif name == "S":
             res.update(slot_configs(ctx, dev, iters))
 
+    # No torch.cuda.empty_cache() between configs: VRAM given back to the driver is wiped in the
+    # background for seconds (every HBM-bound kernel ~2-4 % slower meanwhile: config S after
+    # config C's 118 GB free measured 67-68 % instead of 69-71 %, r03s4-r03s6), so the configs
+    # reuse the caching allocator's blocks instead
     for name in names:
         try:
             one_config(name)
         except Exception as e:  # a secondary config must never cost the headline line
             res[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
-        torch.cuda.empty_cache()
     return res
 
 
@@ -636,7 +676,6 @@ def slot_configs(ctx, dev, iters) -> dict:
                     "shuffled order, verify",
         "check": "every slot passes"})
     del bufs, d_recs
-    torch.cuda.empty_cache()
     # S_meta: 16 B of user metadata per slot (SetMetadataSize, client/options.h:375-391):
     # ComputePrefixSize(4, 16) = 128, stride 4,224; spans 44 + 16 + 4,096 B
     cs, ms_ = 4, 16
@@ -844,8 +883,7 @@ def main():
     solo = None
     if world > 1 and not args.no_solo:
         if rank == 0:
-            wl.free()
-            torch.cuda.empty_cache()
+            wl.free()  # (no empty_cache: a driver free's background wipe would slow the solo leg)
             try:
                 one = Workload(args.workload, ctx, dev, 1, 0)
                 torch.cuda.synchronize()
@@ -861,8 +899,7 @@ def main():
                 solo = {"error": f"{type(e).__name__}: {e}"[:300]}
                 torch.cuda.empty_cache()
         dist.barrier()
-    wl.free()
-    torch.cuda.empty_cache()
+    wl.free()  # (kept in the caching allocator: see secondary_configs)
 
     # ---- N = 1 extras (rank 0 only): secondary configs, end-to-end, CPU baseline
     def optional(fn):  # an extra leg must never cost the headline line

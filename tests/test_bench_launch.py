@@ -58,3 +58,23 @@ def test_world_size_must_match_gpus():
     r = run_bench("--gpus", "2", "--dry-run-cpu", env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2
     assert "WORLD_SIZE" in r.stderr
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_settle_waits_for_a_steady_launch_rate():
+    """bench.py settles until the launch rate stops improving (a background VRAM wipe after a
+    large free slows every HBM-bound kernel for seconds): a window shorter than 1 s or one whose
+    newer half is faster than its older half is not steady; a flat or slowing one is."""
+    steady = _bench_module().launch_rate_steady
+    assert not steady([(0.01, 50)] * 50)  # 0.5 s: too short
+    assert steady([(0.01, 50)] * 100)
+    assert not steady([(0.0104, 50)] * 60 + [(0.0100, 50)] * 60)  # still speeding up (4 %)
+    assert steady([(0.01002, 50)] * 60 + [(0.0100, 50)] * 60)  # within 0.3 %
+    assert steady([(0.0100, 50)] * 60 + [(0.0104, 50)] * 60)  # slowing down: nothing to wait for

@@ -398,6 +398,41 @@ def test_fused_slot_kernel_wider_slots(gpu_ctx, oracle, slot_size, cs):
     assert np.array_equal(dev.cpu().numpy(), host)
 
 
+@pytest.mark.parametrize("cs,ms,off", [(4, 0, 0), (4, 0, 64), (4, 0, 192), (20, 0, 64), (4, 16, 64), (4, 16, 0),
+                                        (5, 7, 64), (6, 64, 64)])
+def test_fused_slot_kernel_line_offsets(gpu_ctx, oracle, cs, ms, off):
+    """The fused slot kernel with the channel at a 128-B line offset `off`: the even or the
+    odd slots' payloads (or both) start 64 B into a line; publish is byte-identical to the
+    oracle, nothing outside the channel is written, and verify statuses equal the oracle's
+    after corruptions, for prefix sizes 64 and 128 (with metadata)."""
+    count = 4097
+    sizes = np.full(count, 4096, dtype=np.uint64)
+    host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=off + 31 * cs + ms)
+    full = torch.zeros(len(host) + 256, dtype=torch.uint8, device=DEV)
+    assert full.data_ptr() % 256 == 0
+    full[off:off + len(host)] = torch.from_numpy(host).to(DEV)
+    status = torch.full((count,), 7, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_slots_strided(full, stride, count, message_size=4096, checksum_size=cs, metadata_size=ms,
+                                mode=gpu.SLOT_CALCULATE, status=status, base_offset=off)
+    torch.cuda.synchronize()
+    po, yo = offsets(count, stride, ps)
+    oracle.publish_slots(host, po, yo, sizes, cs, ms)
+    assert (status.cpu().numpy() == 0).all()
+    got = full.cpu().numpy()
+    assert not got[:off].any() and not got[off + len(host):].any()  # nothing outside the channel
+    bad = np.nonzero(got[off:off + len(host)] != host)[0]
+    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]} (stride {stride}, offset {off})"
+    _corrupt(host, po, ps, cs, sizes, seed=off * 5 + cs + ms)
+    want = oracle.verify_slots(host, po, yo, sizes, cs, ms)
+    full[off:off + len(host)] = torch.from_numpy(host).to(DEV)
+    err = torch.full((1,), 12345, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_slots_strided(full, stride, count, message_size=4096, checksum_size=cs, metadata_size=ms,
+                                mode=gpu.SLOT_VERIFY, status=status, error_count=err, base_offset=off)
+    torch.cuda.synchronize()
+    assert np.array_equal(status.cpu().numpy().view(np.uint32), want)
+    assert int(err.item()) == int((want == 1).sum())
+
+
 def test_fused_and_two_kernel_slot_paths_agree(gpu_ctx):
     """fused_slots off (payload kernel + crc32_slot_finish_kernel) and on give the same
     channel bytes and statuses."""

@@ -4,7 +4,10 @@ calls over 4 rotated channel buffers after ~60 ms of warm-up calls), with the ho
 enqueue time per call next to the event span, so a rocprofv3 --kernel-trace of this script
 gives every launch's duration and its gap to the next (tools/s_launches.py --analyze <csv>).
 
-  python tools/s_launches.py [calls]            one JSON line per mode
+  python tools/s_launches.py [calls] [--prealloc=GiB [--hold=s]] [--keep=GiB] [--sleep=s] [--after=GiB]
+      one JSON line per mode; optionally after allocating GiB (held s seconds) and freeing it
+      before the channel buffers, or allocating GiB and keeping it, then sleeping s seconds;
+      or allocating and freeing GiB after the channel buffers
   python tools/s_launches.py --analyze run_kernel_trace.csv
 """
 import csv
@@ -20,11 +23,31 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 N, SIZE, NBUF = 65536, 4096, 4
 
 
-def run(calls: int) -> None:
+def big_alloc_free(gib: float, hold_s: float = 0.0, keep: bool = False):
+    """As bench.py's configs C/D before S: a large allocation, touched, held hold_s seconds,
+    then freed back to the driver (or kept, and returned)."""
+    import torch
+    big = torch.empty(int(gib * 2**30), dtype=torch.uint8, device="cuda")
+    big[::1 << 20].fill_(1)
+    torch.cuda.synchronize()
+    time.sleep(hold_s)
+    if keep:
+        return big
+    del big
+    torch.cuda.empty_cache()
+    return None
+
+
+def run(calls: int, prealloc_gib: float = 0.0, sleep_s: float = 0.0, after_gib: float = 0.0, hold_s: float = 0.0,
+        keep_gib: float = 0.0) -> None:
     import torch
     from subspace_amd import gpu, slots
     dev = torch.device("cuda", 0)
     ctx = gpu.CrcContext(0)
+    if prealloc_gib:
+        big_alloc_free(prealloc_gib, hold_s)
+    kept = big_alloc_free(keep_gib, keep=True) if keep_gib else None  # allocated, never freed
+    time.sleep(sleep_s)
     cs, ms_ = 4, 0
     ps, stride = slots.compute_prefix_size(cs, ms_), slots.slot_stride(SIZE, cs, ms_)
     rng = np.random.default_rng(0x5EED0005)
@@ -36,7 +59,11 @@ def run(calls: int) -> None:
     errs = torch.zeros(1, dtype=torch.int32, device=dev)
     out = torch.empty(N, dtype=torch.int32, device=dev)
     nbytes = N * (SIZE + 44)
-    print(json.dumps({"buffers": [hex(b.data_ptr()) for b in bufs]}), flush=True)
+    if after_gib:  # the same, after the channel buffers exist (placement vs. what follows a free)
+        big_alloc_free(after_gib)
+    print(json.dumps({"buffers": [hex(b.data_ptr()) for b in bufs], "prealloc_gib": prealloc_gib, "sleep_s": sleep_s,
+                      "after_gib": after_gib, "hold_s": hold_s, "keep_gib": keep_gib, "kept": kept is not None}),
+          flush=True)
     st = torch.cuda.current_stream()
     modes = [("uniform_4160", None), ("S_publish", gpu.SLOT_CALCULATE), ("S_verify", gpu.SLOT_VERIFY),
              ("S_publish", gpu.SLOT_CALCULATE)]
@@ -102,4 +129,7 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--analyze":
         analyze(sys.argv[2])
     else:
-        run(int(sys.argv[1]) if len(sys.argv) > 1 else 400)
+        opts = {a.split("=")[0][2:]: float(a.split("=")[1]) for a in sys.argv[1:] if a.startswith("--")}
+        args = [a for a in sys.argv[1:] if not a.startswith("--")]
+        run(int(args[0]) if args else 400, opts.get("prealloc", 0.0), opts.get("sleep", 0.0), opts.get("after", 0.0),
+            opts.get("hold", 0.0), opts.get("keep", 0.0))
