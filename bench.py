@@ -72,9 +72,11 @@ def parse():
     # run in all and at least SETTLE_S seconds have passed: a fresh box's first GPU process ran
     # config B at 5,368 GiB/s after 380 settle launches (r02c25) and 5,374 after 1 s of them
     # (r02c27), 5,583 after 0.9 s on another box (r02c26) and 5,550 after 5 s (r02c28), later
-    # processes 5,520-5,583; reported as "settle_launches" (--settle 0 disables both).
+    # processes 5,520-5,583; reported as "settle_launches" (--settle 0 disables both). 8 s: a
+    # large VRAM free by an earlier process (a test run's 118 GB) is wiped in the background
+    # for 4-8 s, slowing every HBM-bound kernel 2-4 % (profiles/r03/wipe).
     ap.add_argument("--settle", type=int, default=400)
-    ap.add_argument("--settle-s", type=float, default=5.0)
+    ap.add_argument("--settle-s", type=float, default=8.0)
     # --streams 2: consecutive steps alternate between two HIP streams (independent batches)
     # and overlap (45.2 vs 46.7 us per launch in profiles/r01/ceiling.md). Off by default:
     # overlapping dispatches make rocprofv3's per-dispatch duration (~2x, both kernels
