@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """What a large VRAM free does to the next seconds: allocate, touch and free GIB of device
-memory, then every ~0.25 s print the device's free memory (hipMemGetInfo) and the time of
-100 back-to-back config-B launches (uniform 4 KiB kernel, 256 MiB each), for SECONDS.
+memory while config-B launches (uniform 4 KiB kernel, 256 MiB each) run back to back without
+pause (an idle spell would restart the power-management ramp), and every ~0.25 s print the
+device's free memory (hipMemGetInfo) and the mean time per launch of that interval, for
+SECONDS; the same for SECONDS before the free, as the reference.
 
   python tools/wipe_watch.py [GIB] [SECONDS]
 """
@@ -37,25 +39,25 @@ def main():
         torch.cuda.synchronize()
         return a.elapsed_time(b) / n * 1e3
 
-    for _ in range(40):  # power-management settle
+    def watch(phase, seconds):
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            t1, us = time.perf_counter(), []
+            while time.perf_counter() - t1 < 0.25:
+                us.append(launches_us())
+            print(json.dumps({"phase": phase, "t_s": round(time.perf_counter() - t0, 2),
+                              "free_gib": round(torch.cuda.mem_get_info()[0] / 2**30, 2),
+                              "us_per_launch": round(sum(us) / len(us), 2)}), flush=True)
+
+    for _ in range(100):  # power-management settle
         launches_us()
-    free0, total = torch.cuda.mem_get_info()
-    print(json.dumps({"phase": "before", "free_gib": round(free0 / 2**30, 2), "total_gib": round(total / 2**30, 2),
-                      "us_per_launch": round(launches_us(), 2)}), flush=True)
     big = torch.empty(int(gib * 2**30), dtype=torch.uint8, device=dev)
     big[::1 << 20].fill_(1)
     torch.cuda.synchronize()
-    print(json.dumps({"phase": "allocated", "free_gib": round(torch.cuda.mem_get_info()[0] / 2**30, 2),
-                      "us_per_launch": round(launches_us(), 2)}), flush=True)
+    watch("allocated", secs / 2)
     del big
     torch.cuda.empty_cache()
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < secs:
-        f = torch.cuda.mem_get_info()[0]
-        us = launches_us()
-        print(json.dumps({"t_s": round(time.perf_counter() - t0, 2), "free_gib": round(f / 2**30, 2),
-                          "us_per_launch": round(us, 2)}), flush=True)
-        time.sleep(0.2)
+    watch("freed", secs)
 
 
 if __name__ == "__main__":
