@@ -523,6 +523,29 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, re
     return elapsed, avg_ms, sampled, n_settle + warmup, own
 
 
+def read_ceiling(wl, launches=400):
+    """The measured streaming-read ceiling of config B's access shape at its launch size
+    (SURVEY.md 8d): gpu.stream_read (testutil.hip: the CRC kernel's loads -- lane <-> 128-B
+    line, the same sweep front, one tile in flight per wave -- with an XOR fold instead of the
+    CRC) over the same rotated batches, back to back after ~60 ms of them."""
+    import torch
+    from subspace_amd import gpu
+    sink = torch.empty(256 * 512, dtype=torch.int32, device=wl.bufs[0].device)
+    for i in range(1400):
+        gpu.stream_read(wl.bufs[i % wl.nbuf], sink)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for i in range(launches):
+        gpu.stream_read(wl.bufs[i % wl.nbuf], sink)
+    b.record()
+    torch.cuda.synchronize()
+    us = a.elapsed_time(b) / launches * 1e3
+    return {"GBps": round(wl.step_bytes / (us * 1e-6) / 1e9, 1), "us_per_launch": round(us, 2), "launches": launches,
+            "kernel": "stream_read_kernel (testutil.hip): the CRC kernel's load shape and sweep, one tile in "
+                      "flight, no CRC"}
+
+
 # ------------------------------------------------------------------------------ secondary configs
 def time_calls(fn, iters, warm_ms=60.0):
     """ms per call: one HIP event pair around `iters` back-to-back calls (after ~warm_ms of
@@ -866,6 +889,12 @@ def main():
     settle = max(0, settle - args.warmup)
     bitexact, gather = wl.check(pg)
     gather_ms = gather["gather_ms"] if gather else None
+    ceiling = None
+    if args.workload == "B" and world == 1:
+        try:
+            ceiling = read_ceiling(wl)
+        except Exception as e:  # an extra leg must never cost the headline line
+            ceiling = {"error": f"{type(e).__name__}: {e}"[:300]}
     # every rank's identity and timing, so the line shows that N distinct GPUs ran
     props = torch.cuda.get_device_properties(gpu_index)
     me = {"rank": rank, "local_rank": local, "device": torch.cuda.current_device(),
@@ -998,6 +1027,10 @@ def main():
                                              "consecutive launches overlap when 2)",
                          "sampled_launch_ms": round(sampled_ms, 4) if sampled_ms else None},
         }
+        if ceiling is not None:
+            line["roofline"]["read_ceiling"] = ceiling
+            if "GBps" in ceiling:
+                line["roofline"]["frac_of_read_ceiling"] = round(achieved / ceiling["GBps"], 4)
         steps_ms = [r["step_ms"] for r in everyone]
         line["ranks"] = everyone
         line["rank_step_ms"] = {"min": min(steps_ms), "max": max(steps_ms)}

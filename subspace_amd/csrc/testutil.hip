@@ -43,9 +43,11 @@ __global__ void synth_fill_kernel(uint8_t* __restrict__ base, const uint64_t* __
 }
 
 // Streaming-read ceiling probe: the CRC kernels' load shape (lane <-> 128-B line, 8 x
-// 16-B loads per lane, 64 consecutive lines per wave instruction, XCD-spread sweep front,
-// one tile prefetched) with the CRC replaced by an XOR fold -- what HBM gives this access
-// pattern.
+// 16-B loads per lane, 64 consecutive lines per wave instruction, the same order-0 sweep
+// front) with the CRC replaced by an XOR fold and one tile in flight per wave (each tile's
+// loads issued after the previous tile landed) -- what HBM gives this access pattern at
+// this launch size (profiles/r01/ceiling.md "8 loads then wait": 41.0 us per 256 MiB).
+// bench.py reports it next to the CRC kernel as the measured read ceiling.
 using subspace_amd::u32x4;
 __global__ __launch_bounds__(512) void stream_read_kernel(const u32x4* __restrict__ p, uint64_t ntiles,
                                                           unsigned* __restrict__ out) {
@@ -53,22 +55,12 @@ __global__ __launch_bounds__(512) void stream_read_kernel(const u32x4* __restric
   const uint64_t w = subspace_amd::front_slot(blockIdx.x, gridDim.x, subspace_amd::rfl(threadIdx.x >> 6));
   const uint64_t nw = (uint64_t)gridDim.x * 8;
   unsigned acc = 0;
-  uint64_t t = w;
-  u32x4 a[8], b[8];
-  const uint64_t last = ntiles - 1;
+  for (uint64_t t = w; t < ntiles; t += nw) {
+    u32x4 a[8];
 #pragma unroll
-  for (int i = 0; i < 8; i++) a[i] = p[(t < ntiles ? t : last) * 512 + lane * 8 + i];
-  for (; t < ntiles; t += 2 * nw) {
-    const uint64_t t1 = t + nw < ntiles ? t + nw : last;
-#pragma unroll
-    for (int i = 0; i < 8; i++) b[i] = p[t1 * 512 + lane * 8 + i];
+    for (int i = 0; i < 8; i++) a[i] = p[t * 512 + lane * 8 + i];
 #pragma unroll
     for (int i = 0; i < 8; i++) acc ^= a[i].x ^ a[i].y ^ a[i].z ^ a[i].w;
-    const uint64_t t2 = t + 2 * nw < ntiles ? t + 2 * nw : last;
-#pragma unroll
-    for (int i = 0; i < 8; i++) a[i] = p[t2 * 512 + lane * 8 + i];
-#pragma unroll
-    for (int i = 0; i < 8; i++) acc ^= b[i].x ^ b[i].y ^ b[i].z ^ b[i].w;
   }
   out[blockIdx.x * 512 + threadIdx.x] = acc;
 }
