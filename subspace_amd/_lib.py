@@ -104,6 +104,8 @@ def load() -> ctypes.CDLL:
     lib.subspace_crc_testutil_set.argtypes = [vp, ctypes.c_char_p, i32]
     lib.subspace_crc_testutil_stream_read.restype = i32
     lib.subspace_crc_testutil_stream_read.argtypes = [vp, u64, vp, vp]
+    lib.subspace_crc_testutil_stream_read_lds.restype = i32
+    lib.subspace_crc_testutil_stream_read_lds.argtypes = [vp, u64, vp, ctypes.c_uint32, vp]
     _lib = lib
     return lib
 

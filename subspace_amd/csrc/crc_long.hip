@@ -108,12 +108,16 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
   // stalls it for the write's round trip -- 3.6 % of the kernel at config D, r01au).
   u32 k = 0;
   for (; k + 1 < nk; k += 2) {
+    issue_prio_hi();  // (crc_device.h)
     drain_before_issue();
     load_next(B, mB, jB);
+    issue_prio_lo();
     if (k && (k & 63u) == 0) flush(k - 64, 64u);
     process(A, jA, k);
+    issue_prio_hi();
     drain_before_issue();
     load_next(A, mA, jA);
+    issue_prio_lo();
     process(B, jB, k + 1);
   }
   if (k < nk) {

@@ -297,18 +297,22 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   // (crc_long.hip) -- and once more at the end.
   u64 k = 0;
   for (; k + 1 < nk; k += 2) {
+    issue_prio_hi();                  // (crc_device.h)
     drain_before_issue();             // at most one tile of loads in flight (crc_uniform.hip)
     const TileDesc d1 = unpack(dB);   // tile k+1
     const u32 m1 = mB;
     fetch_desc(k + 2, dA, mA);        // tile k+2 (clamped)
     load_line(d1, B, true);
+    issue_prio_lo();
     if (k && (k & 63) == 0) flush(k - 64, 64u);
     process(A, dcur, mcur, k);
+    issue_prio_hi();
     drain_before_issue();
     const TileDesc d2 = unpack(dA);   // tile k+2 (clamped)
     const u32 m2 = mA;
     fetch_desc(k + 3, dB, mB);        // tile k+3 (clamped)
     load_line(d2, A, k + 2 < nk);
+    issue_prio_lo();
     process(B, d1, m1, k + 1);
     dcur = d2;
     mcur = m2;

@@ -329,16 +329,20 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // values, 64-tile windows and a flush only after the loop each measured slower).
   u32 k = 0;
   for (; k + 1 < nk; k += 2) {
+    issue_prio_hi();       // (crc_device.h)
     drain_before_issue();  // tile k's lines and tile k+1's record
     const u64 s1 = sB, L1 = LB;
     fetch(k + 2, sA, LA);
     load_lines(B, s1, ext(k + 1, s1, L1));
+    issue_prio_lo();
     if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
     process(A, sc, Lc, k);
+    issue_prio_hi();
     drain_before_issue();
     const u64 s2 = sA, L2 = LA;
     fetch(k + 3, sB, LB);
     load_lines(A, s2, ext(k + 2, s2, L2));
+    issue_prio_lo();
     process(B, s1, L1, k + 1);
     sc = s2;
     Lc = L2;

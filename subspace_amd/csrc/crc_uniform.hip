@@ -220,16 +220,20 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   u32 k = 0, kf = 0;
   u64 pt_finish = 0;  // PROBE, SLOT: when a finishing wave began
   for (; k + 1 < nk; k += 2) {
+    issue_prio_hi();
     drain_before_issue();
     load_tile(B, k + 1);
+    issue_prio_lo();
     if (!SLOT && k - kf == kWin) {
       wave_lds_sync();
       flush(kf, kRing / 2);
       kf = k;
     }
     tile_result(line_crc(A), k, kf);
+    issue_prio_hi();
     drain_before_issue();
     load_tile(A, k + 2);
+    issue_prio_lo();
     tile_result(line_crc(B), k + 1, kf);
   }
   if constexpr (PROBE) pt[2] = __builtin_amdgcn_s_memrealtime();

@@ -65,6 +65,26 @@ __global__ __launch_bounds__(512) void stream_read_kernel(const u32x4* __restric
   out[blockIdx.x * 512 + threadIdx.x] = acc;
 }
 
+// The same with a dynamic LDS allocation it does not use (the cost of the CRC kernels' ~152 KiB
+// LDS per workgroup alone, without the table fill)
+__global__ __launch_bounds__(512) void stream_read_lds_kernel(const u32x4* __restrict__ p, uint64_t ntiles,
+                                                              unsigned* __restrict__ out) {
+  extern __shared__ unsigned lds_unused[];
+  const int lane = threadIdx.x & 63;
+  const uint64_t w = subspace_amd::front_slot(blockIdx.x, gridDim.x, subspace_amd::rfl(threadIdx.x >> 6));
+  const uint64_t nw = (uint64_t)gridDim.x * 8;
+  unsigned acc = 0;
+  for (uint64_t t = w; t < ntiles; t += nw) {
+    u32x4 a[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) a[i] = p[t * 512 + lane * 8 + i];
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc ^= a[i].x ^ a[i].y ^ a[i].z ^ a[i].w;
+  }
+  if (acc == 0x12345678u) lds_unused[threadIdx.x] = acc;  // (keeps the allocation)
+  out[blockIdx.x * 512 + threadIdx.x] = acc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -74,6 +94,18 @@ int subspace_crc_testutil_stream_read(const void* dev_base, uint64_t bytes, unsi
   if (!dev_base || !dev_out || bytes < 8192 || (bytes % 8192)) return -1;
   stream_read_kernel<<<256, 512, 0, (hipStream_t)stream>>>(static_cast<const u32x4*>(dev_base), bytes / 8192,
                                                            dev_out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// The same read with lds_bytes (<= 160 KiB) of dynamic LDS allocated per workgroup, unused.
+int subspace_crc_testutil_stream_read_lds(const void* dev_base, uint64_t bytes, unsigned* dev_out, uint32_t lds_bytes,
+                                          void* stream) {
+  if (!dev_base || !dev_out || bytes < 8192 || (bytes % 8192) || lds_bytes > 160u * 1024u) return -1;
+  if (hipFuncSetAttribute((const void*)stream_read_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds_bytes) != hipSuccess)
+    return -2;
+  stream_read_lds_kernel<<<256, 512, lds_bytes, (hipStream_t)stream>>>(static_cast<const u32x4*>(dev_base),
+                                                                       bytes / 8192, dev_out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
