@@ -362,6 +362,14 @@ __device__ __forceinline__ void drain_before_issue() { asm volatile("s_waitcnt v
 #ifndef SUBSPACE_ISSUE_PRIO
 #define SUBSPACE_ISSUE_PRIO 1
 #endif
+// The next tile's address computed before the wait for the current one and pinned there
+// (uniform and long kernels), so only the load instructions follow the landing: config B
+// 45.2-45.7 vs 45.8-45.9 us, slot publish / verify -0.3 / -0.4 us (interleaved, r03s18). The
+// ragged and small kernels' next addresses come from records loaded one tile ahead, which
+// land with the tile, so theirs cannot move. 0: left to hipcc (A/B builds).
+#ifndef SUBSPACE_ADDR_EARLY
+#define SUBSPACE_ADDR_EARLY 1
+#endif
 __device__ __forceinline__ void issue_prio_hi() {
   if constexpr (SUBSPACE_ISSUE_PRIO > 0) __builtin_amdgcn_s_setprio(SUBSPACE_ISSUE_PRIO);
 }

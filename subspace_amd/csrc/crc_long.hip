@@ -42,15 +42,21 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
   const u32 dm = nw / pieces, dj = nw % pieces;
   u32 fm = nk ? w / pieces : count - 1, fj = nk ? w % pieces : pieces - 1;  // next tile to load
   u32 fk = 0;                                                             // its k
-  auto line_ptr = [&](u32 m, u32 j) {
-    return reinterpret_cast<const u32x4*>(base + (u64)m * stride + (u64)j * 8192u + (u64)lane * 128u);
-  };
   // Loads of the wave's next tile; past its last tile the last one is re-read (an L2 hit),
   // so every lane issues every load.
-  auto load_next = [&](u32x4 (&d)[8], u32& m, u32& j) {
+  // the wave's next tile's byte offset (wave-uniform), computed ahead of the wait for the
+  // current tile and pinned there (crc_uniform.hip addr_before_wait)
+  auto next_off = [&]() {
+    u64 off = (u64)fm * stride + (u64)fj * 8192u;
+#if SUBSPACE_ADDR_EARLY
+    asm volatile("" : "+s"(off));
+#endif
+    return off;
+  };
+  auto load_next_at = [&](u32x4 (&d)[8], u32& m, u32& j, u64 off) {
     m = fm;
     j = fj;
-    const u32x4* q = line_ptr(m, j);
+    const u32x4* q = reinterpret_cast<const u32x4*>(base + off + (u64)lane * 128u);
 #pragma unroll
     for (int i = 0; i < 8; i++) d[i] = q[i];
     __builtin_amdgcn_sched_barrier(0);
@@ -64,6 +70,7 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
       }
     }
   };
+  auto load_next = [&](u32x4 (&d)[8], u32& m, u32& j) { load_next_at(d, m, j, next_off()); };
 
   u32 H0 = 0, H1 = 0, AF = 0;  // parked half values and pieces-after | first-piece flag
   auto process = [&](const u32x4 (&d)[8], u32 j, u32 k) {
@@ -108,15 +115,17 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
   // stalls it for the write's round trip -- 3.6 % of the kernel at config D, r01au).
   u32 k = 0;
   for (; k + 1 < nk; k += 2) {
+    const u64 oB = next_off();
     issue_prio_hi();  // (crc_device.h)
     drain_before_issue();
-    load_next(B, mB, jB);
+    load_next_at(B, mB, jB, oB);
     issue_prio_lo();
     if (k && (k & 63u) == 0) flush(k - 64, 64u);
     process(A, jA, k);
+    const u64 oA = next_off();
     issue_prio_hi();
     drain_before_issue();
-    load_next(A, mA, jA);
+    load_next_at(A, mA, jA, oA);
     issue_prio_lo();
     process(B, jB, k + 1);
   }

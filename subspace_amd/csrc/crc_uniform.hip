@@ -139,15 +139,28 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   // lane issues every load, no divergent branch around loads (which forces vmcnt(0)).
   // Waves without tiles read message 0. (Buffer loads against a per-tile scalar resource,
   // which make all this address math scalar, measured 7-10 % slower: DESIGN.md 4.1.)
-  auto load_tile = [&](u32x4 (&d)[8], u32 k) {
+  auto tile_off = [&](u32 k) {  // byte offset of this lane's line of tile k from base
     const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
     u64 msg = nk ? 2 * (t0 + (u64)kk * tstep) + (u64)h : 0;
     msg = msg < count ? msg : msg - 1;
-    const u32x4* q = reinterpret_cast<const u32x4*>(base + msg * stride + (u64)l * 128);
+    return msg * stride + (u64)l * 128;
+  };
+  auto load_at = [&](u32x4 (&d)[8], u64 off) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(base + off);
 #pragma unroll
     for (int i = 0; i < 8; i++) d[i] = q[i];
     // keep the loads at this point, in order (hipcc otherwise sinks them into the compute)
     __builtin_amdgcn_sched_barrier(0);
+  };
+  auto load_tile = [&](u32x4 (&d)[8], u32 k) { load_at(d, tile_off(k)); };
+  // The next tile's offset, computed before the wait for the current one (pinned there), so
+  // only the load instructions remain between the landing and the issue
+  auto addr_before_wait = [&](u32 k) {
+    u64 off = tile_off(k);
+#if SUBSPACE_ADDR_EARLY
+    asm volatile("" : "+v"(off));
+#endif
+    return off;
   };
 
   // CRC of this lane's line of a tile (from the batch init for line 0, else from 0).
@@ -220,9 +233,10 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   u32 k = 0, kf = 0;
   u64 pt_finish = 0;  // PROBE, SLOT: when a finishing wave began
   for (; k + 1 < nk; k += 2) {
+    const u64 qB = addr_before_wait(k + 1);
     issue_prio_hi();
     drain_before_issue();
-    load_tile(B, k + 1);
+    load_at(B, qB);
     issue_prio_lo();
     if (!SLOT && k - kf == kWin) {
       wave_lds_sync();
@@ -230,9 +244,10 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
       kf = k;
     }
     tile_result(line_crc(A), k, kf);
+    const u64 qA = addr_before_wait(k + 2);
     issue_prio_hi();
     drain_before_issue();
-    load_tile(A, k + 2);
+    load_at(A, qA);
     issue_prio_lo();
     tile_result(line_crc(B), k + 1, kf);
   }
