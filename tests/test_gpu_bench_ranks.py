@@ -67,3 +67,20 @@ def test_rccl_path_one_rank():
     assert d["backend"] == "nccl" and d["rccl_world"] == 1 and d["n_gpus"] == 1
     assert d["bitexact_vs_golden"] is True
     assert d["config"]["gather"]["gather_ms"] > 0 and d["ranks"][0]["rank"] == 0
+
+
+def test_single_gpu_line_reports_read_ceiling():
+    """The N = 1 config-B line carries the measured read ceiling of the same access shape
+    (SURVEY.md 8d): the stream-read probe over the same rotated batches, and the CRC kernel's
+    fraction of it (< 1: the CRC kernel reads the same bytes plus its compute)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "50", "--warmup", "2", "--settle", "0",
+                        "--configs", "none", "--no-cpu-baseline", "--no-e2e"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    d = json.loads(lines[-1])
+    assert d["bitexact_vs_golden"] is True
+    ceil = d["roofline"]["read_ceiling"]
+    assert ceil["us_per_launch"] > 0 and ceil["GBps"] > 1000
+    assert 0.5 < d["roofline"]["frac_of_read_ceiling"] < 1.05
