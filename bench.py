@@ -383,7 +383,8 @@ class Workload:
         """(bit-exact vs the fixture on rank 0, gather timing). Collective when world > 1: the
         4-byte CRCs of every rank are all_gathered (RCCL over xGMI) and put in global order on
         the device; HIP events on the current stream time exactly that (`gather_ms`, the device
-        gather: the collective plus the on-device interleave; at world 1 one device copy). The
+        gather: the collective plus the on-device interleave, mean of 5 after an untimed first
+        call; at world 1 one device copy). The
         D2H copy and the host hash check are timed apart (`d2h_check_ms`). B: each rank's
         batch 0 is a distinct id set, so at world 1 it is exactly config B."""
         import torch
@@ -392,18 +393,25 @@ class Workload:
             if self.world > 1:
                 return None, None
             return digest(self.outs[0].cpu().numpy().view(np.uint32)) == GOLD["B"]["sha256_le_u32"], None
+        def gather():
+            if self.name == "C":
+                return shard.gather_ragged_crcs_device(self.outs[0][:self.nmsg], self.bounds, self.world, dist)
+            return shard.gather_crcs_device(self.outs[0], E_COUNT, self.world, dist)
+
+        # one untimed gather first: its buffers' allocations and the collective's first-call
+        # setup are host work the device would wait on inside the events (~20 ms at world 1)
+        gather()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
+        reps = 5
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-        if self.name == "C":
-            full = shard.gather_ragged_crcs_device(self.outs[0][:self.nmsg], self.bounds, self.world, dist)
-        else:
-            full = shard.gather_crcs_device(self.outs[0], E_COUNT, self.world, dist)
+        for _ in range(reps):
+            full = gather()
         ev[1].record()
         torch.cuda.synchronize()
-        gather_ms = ev[0].elapsed_time(ev[1])
+        gather_ms = ev[0].elapsed_time(ev[1]) / reps
         tc = time.perf_counter()
         ok = digest(full.cpu().numpy().view(np.uint32)) == GOLD[self.name]["sha256_le_u32"] if self.rank == 0 else None
         return ok, {"gather_ms": round(gather_ms, 4), "d2h_check_ms": round((time.perf_counter() - tc) * 1e3, 3),
