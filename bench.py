@@ -107,6 +107,8 @@ def parse():
                     help="N > 1 on a one-GPU machine: every rank on cuda:0, gloo instead of RCCL -- the GPU "
                          "workload, timing, gather and single-GPU legs of a multi-GPU run, for tests (the ranks "
                          "share one GPU, so the rates are not scaling numbers)")
+    ap.add_argument("--print-rank-env", action="store_true",
+                    help="each rank prints the launch environment it got (one JSON line) and exits, for tests")
     ap.add_argument("--dry-run-cpu", action="store_true",
                     help="CPU + gloo rehearsal of the spawn/shard/gather path (host SubspaceCRC32), for tests")
     return ap.parse_args()
@@ -124,17 +126,31 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+# Environment every rank runs with, whichever way it was started (the driver's own
+# `torch.distributed.run ... bench.py`, or this script spawning its ranks): applied by
+# apply_rank_env() at the top of main(), before torch is imported or any HIP call is made --
+# ROCm reads HSA_ENABLE_IPC_MODE_LEGACY when HIP initialises (the host driver supports dmabuf
+# IPC only, which RCCL's cross-process buffers need), so setting it later has no effect
+# (it used to be set after torch.cuda.device_count() in the driver's form).
+RANK_ENV_DEFAULTS = {"HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+RANK_ENV_REPORTED = ("HSA_ENABLE_IPC_MODE_LEGACY", "OMP_NUM_THREADS", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
+                     "MASTER_ADDR")
+
+
+def apply_rank_env() -> None:
+    for k, v in RANK_ENV_DEFAULTS.items():
+        os.environ.setdefault(k, v)
+
+
 def spawn_ranks(args) -> int:
     """--gpus N > 1 without a launcher: start N rank processes (one per GPU) through
     torch.distributed.run as a child and return its exit status. This process never
-    initialises a GPU (no exec from a GPU-initialised process)."""
+    initialises a GPU (no exec from a GPU-initialised process). The ranks get the same
+    environment as under the driver's own launch (apply_rank_env; tests/test_bench_launch.py)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve()),
            *sys.argv[1:]]
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    env.setdefault("OMP_NUM_THREADS", "1")
-    return subprocess.run(cmd, env=env).returncode
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
 def digest(crcs) -> str:
@@ -844,6 +860,7 @@ def dry_run_cpu(args, world, rank) -> int:
 
 # ------------------------------------------------------------------------------ main
 def main():
+    apply_rank_env()  # before torch and before any HIP call, in every launch form
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
@@ -853,6 +870,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         die(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch with --nproc-per-node equal to --gpus")
+    if args.print_rank_env:  # tests: what a rank runs with, before anything else happens
+        print(json.dumps({"rank": rank, "env": {k: os.environ.get(k) for k in RANK_ENV_REPORTED}}), flush=True)
+        sys.exit(0)
     if args.workload is None:
         args.workload = "B" if world == 1 else "E"
     if args.dry_run_cpu:
@@ -870,7 +890,6 @@ def main():
     dist_on = world > 1 or world_env is not None
     if dist_on:
         torch.cuda.set_device(gpu_index)
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if args.rehearse_one_gpu:
             dist.init_process_group("gloo")
         else:

@@ -106,6 +106,8 @@ def load() -> ctypes.CDLL:
     lib.subspace_crc_testutil_stream_read.argtypes = [vp, u64, vp, vp]
     lib.subspace_crc_testutil_stream_read_lds.restype = i32
     lib.subspace_crc_testutil_stream_read_lds.argtypes = [vp, u64, vp, ctypes.c_uint32, vp]
+    lib.subspace_crc_testutil_uniform_alias.restype = i32
+    lib.subspace_crc_testutil_uniform_alias.argtypes = [vp, vp, u64, vp, vp]
     _lib = lib
     return lib
 

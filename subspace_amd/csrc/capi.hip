@@ -22,17 +22,17 @@ __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, con
 
 struct TileDesc;
 __global__ void crc32_ragged_count_scan_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
-                                               u64*, u32*, u32*, u64, u32*);
+                                               u64*, u32*, u32*, u64, FaultRef);
 __global__ void tile_segment_scan_kernel(const u32*, u32, u32, u32, const u64*, u64, u32*, u32*);
-__global__ void segment_prefix_kernel(u32*, u64, u32, u32, const u64*, u64, u64*, u32*, u32*);
+__global__ void segment_prefix_kernel(u32*, u64, u32, u32, const u64*, u64, u64*, u32*, FaultRef);
 __global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, u64, u64, const u32*,
-                                         TileDesc*, u32*, u64*, u64, u32*, const u32*);
+                                         TileDesc*, u32*, u64*, u64, u32*, FaultRef);
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
                                     const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds, u32*, u32*, u64,
-                                    const u32*);
+                                    FaultRef);
 __global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, const u64*, u32, u64, const u32*, const u32*,
-                                          u32, u32, const u32*, const u32*, u32, u32*, u64*, u64, u32*, const u32*);
+                                          u32, u32, const u32*, const u32*, u32, u32*, u64*, u64, u32*, FaultRef);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, int, int, u32, const u32*,
                                          const u32*, const u32*, u32*, u32*, u32*);
 __global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*);
@@ -171,7 +171,9 @@ struct subspace_crc_ctx {
   bool fused_slots = true;        // contiguous 4 KiB slot batches take the fused uniform kernel
   bool small_path = true;         // batches of messages <= 4 KiB take the small-message kernel (crc_small.hip)
   u64* probe = nullptr;           // experiment hook: per-wave timestamps (subspace_crc_testutil_probe)
-  u32* d_fault = nullptr;         // fault word (crc_device.h kFault*): read and cleared by subspace_crc_ctx_check
+  u32* d_fault = nullptr;         // fault words (crc_device.h FaultRef): [0] kFault* bits, read and cleared by
+                                  // subspace_crc_ctx_check; [1] the generation of the last call whose scan faulted
+  u32 call_gen = 0;               // generation of the latest ragged / long call (never 0 once used)
   // One call at a time per context (a recursive mutex: the host-slot paths call the device
   // paths), and device workspace use ordered across streams: a call that uses the context's
   // device workspaces (ragged / long / two-kernel slot paths, the host-slot staging) on another
@@ -233,6 +235,7 @@ const char* fault_text(u32 f) {
   if (f & kFaultTicket) return "a look-back scan ticket was beyond its grid (stale scan state)";
   if (f & kFaultLookbackSpin) return "a look-back scan predecessor never published (stale scan state)";
   if (f & kFaultSlotRing) return "a fused slot kernel finishing wave never received a payload CRC";
+  if (f & kFaultGrid) return "a small-message kernel was launched with more tiles per wave than its ring holds";
   return "unknown fault";
 }
 
@@ -243,7 +246,7 @@ int fault_status(subspace_crc_ctx* c, hipStream_t st) {
   HIP_TRY(hipMemcpyAsync(&f, c->d_fault, sizeof(u32), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (f == 0) return SUBSPACE_CRC_OK;
-  HIP_TRY(hipMemsetAsync(c->d_fault, 0, sizeof(u32), st));
+  HIP_TRY(hipMemsetAsync(c->d_fault, 0, 2 * sizeof(u32), st));
   HIP_TRY(hipMemsetAsync(c->d_slot_counter, 0, kSlotCounters * sizeof(u64), st));
   HIP_TRY(hipStreamSynchronize(st));
   c->scan_dirty = true;
@@ -331,7 +334,14 @@ u64 clamp_capacity(const subspace_crc_ctx* c, u64 cap, u64 count) {
 // The tile-value combine after a ragged or long kernel: segment scans of the wave-major
 // values, then the look-back over the segment XORs. total_ptr: the device's tile count
 // (ragged) or null (long: `tiles` exact).
-int combine_tiles(subspace_crc_ctx* c, const TileGeom& g, const u64* total_ptr, u64 tiles, hipStream_t st) {
+// A new call generation for the look-back scans' fault marks (crc_device.h FaultRef).
+FaultRef new_call_fault(subspace_crc_ctx* c) {
+  if (++c->call_gen == 0) c->call_gen = 1;
+  return FaultRef{c->d_fault, c->call_gen};
+}
+
+int combine_tiles(subspace_crc_ctx* c, const TileGeom& g, const u64* total_ptr, u64 tiles, FaultRef fr,
+                  hipStream_t st) {
   const dim3 grid((unsigned)ceil_div(g.nkmax, 64), (unsigned)g.nwb);
   tile_segment_scan_kernel<<<grid, 256, 0, st>>>(c->d_tilecrc, (u32)g.nw, (u32)g.nkmax, (u32)g.nwb, total_ptr, tiles,
                                                   c->d_local, c->d_segx);
@@ -339,7 +349,7 @@ int combine_tiles(subspace_crc_ctx* c, const TileGeom& g, const u64* total_ptr, 
   u32* tickets = reinterpret_cast<u32*>(c->d_scan_state);
   segment_prefix_kernel<<<(unsigned)ceil_div(g.nseg, kScanTile), 256, 0, st>>>(
       c->d_segx, g.nseg, (u32)g.nw, (u32)g.nwb, total_ptr, tiles, c->d_scan_state + 1 + c->scan_a_words, tickets + 1,
-      c->d_fault);
+      fr);
   HIP_TRY(hipGetLastError());
   return SUBSPACE_CRC_OK;
 }
@@ -367,16 +377,17 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   rc = scan_state_clean(c, st);
   if (rc) return rc;
   c->scan_dirty = true;  // until the final kernel is launched
+  const FaultRef fr = new_call_fault(c);
   u32* tickets = reinterpret_cast<u32*>(c->d_scan_state);
   crc32_ragged_count_scan_kernel<<<(unsigned)ceil_div(n1, kCountTile), 256, 0, st>>>(
       offsets, ostride, lengths, lstride, count, init, final_xor, c->d_tbase, out, c->zero_word, c->d_scan_state + 1,
-      reinterpret_cast<u32*>(c->d_scan_state), c->d_chunk, ceil_div(cap, kDescTilesPerWave), c->d_fault);
+      reinterpret_cast<u32*>(c->d_scan_state), c->d_chunk, ceil_div(cap, kDescTilesPerWave), fr);
   c->zero_word = nullptr;
   HIP_TRY(hipGetLastError());
   // one wave per kDescTilesPerWave tiles, four waves per block
   crc32_ragged_desc_kernel<<<(unsigned)ceil_div(cap, 4 * kDescTilesPerWave), 256, 0, st>>>(
       offsets, ostride, lengths, lstride, c->d_tbase, count, cap, c->d_chunk, reinterpret_cast<TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_scan_state + 1, ceil_div(n1, kCountTile), tickets, c->d_fault);
+      c->d_overflow, c->d_scan_state + 1, ceil_div(n1, kCountTile), tickets, fr);
   HIP_TRY(hipGetLastError());
   const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU
   HeadSeeds seeds;  // Z_r^{-1}(init), r = 0..15: the seed of a message's first line, mis = r
@@ -384,17 +395,17 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   for (int r = 1; r < 16; r++) seeds.v[r] = apply(c->zinv1, seeds.v[r - 1]);
   crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, ragged_lds_bytes(), st>>>(
       base, offsets, ostride, lengths, lstride, c->d_tbase, count, reinterpret_cast<const TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_tab, c->d_rops, seeds, out, c->d_tilecrc, g.nkmax, c->d_fault);
+      c->d_overflow, c->d_tab, c->d_rops, seeds, out, c->d_tilecrc, g.nkmax, fr);
   HIP_TRY(hipGetLastError());
   // padded message CRC = XOR of its tiles' values = difference of two entries of their
   // XOR prefix (only the batch's real tiles are combined); the final kernel undoes the last
   // tile's zero padding and applies the final XOR
-  rc = combine_tiles(c, g, c->d_tbase + count, cap, st);
+  rc = combine_tiles(c, g, c->d_tbase + count, cap, fr, st);
   if (rc) return rc;
   crc32_ragged_final_kernel<<<(unsigned)ceil_div(count, 256), 256, 0, st>>>(
       c->d_tbase, offsets, ostride, lengths, lstride, count, c->d_local, c->d_segx, (u32)g.nw, (u32)g.nwb,
       c->d_overflow, c->d_rops, final_xor, out, c->d_scan_state + 1 + c->scan_a_words, ceil_div(g.nseg, kScanTile),
-      tickets + 1, c->d_fault);
+      tickets + 1, fr);
   HIP_TRY(hipGetLastError());
   c->scan_dirty = false;
   return SUBSPACE_CRC_OK;
@@ -431,7 +442,12 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
   a.out = out;
   a.rops = c->d_rops;
   a.pow2 = c->d_pow2;
-  const unsigned blocks = (unsigned)grid_for(c, (count + 1) / 2, 8);  // persistent: one per CU at most
+  a.fault = c->d_fault;
+  // one workgroup per CU, or more, so that no wave gets more than one ring window of tiles
+  // (the kernel's loop holds no flush: crc_small.hip)
+  const u64 tiles = (count + 1) / 2;
+  const unsigned blocks =
+      (unsigned)std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSmallRingTiles));
   const size_t lds = small_lds_bytes() + 16;
   if (slot) {
     a.prefixes = slot->prefixes;
@@ -775,7 +791,7 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
         static_cast<const uint8_t*>(dev_base), stride, (u32)pieces, (u32)count, c->d_tab, c->d_rops, init, final_xor,
         c->d_tilecrc, (u32)g.nkmax);
     HIP_TRY(hipGetLastError());
-    rc = combine_tiles(c, g, nullptr, tiles, st);
+    rc = combine_tiles(c, g, nullptr, tiles, new_call_fault(c), st);
     if (rc) return rc;
     crc32_long_final_kernel<<<(unsigned)ceil_div(count, 256), 256, 0, st>>>(
         c->d_local, c->d_segx, (u32)g.nw, (u32)g.nwb, (u32)pieces, (u32)count, dev_out,
@@ -1244,6 +1260,24 @@ uint64_t subspace_crc_testutil_probe_waves(subspace_crc_ctx* c, uint64_t count) 
   // when a wave would get more than kSlotRingRounds tiles)
   const u64 tiles = (count + 1) / 2;
   return std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSlotRingRounds)) * 8u;
+}
+
+// Experiment hook (not part of the public header): the uniform 4 KiB kernel's product
+// instantiation over `count` messages that all alias the same 4 KiB at dev_base (stride 0), so
+// every line load hits the cache: the kernel's compute-only time at the headline's grid and
+// tile count (the ledger's "compute" row, tools/pmc_ledger.sh). out[i] = the CRC of that one
+// message for every i.
+int subspace_crc_testutil_uniform_alias(subspace_crc_ctx* c, const void* dev_base, uint64_t count, uint32_t* dev_out,
+                                        void* stream) {
+  if (!c || !dev_base || !dev_out || count == 0 || ((uintptr_t)dev_base % 16)) return SUBSPACE_CRC_EINVAL;
+  CallScope scope(c);
+  HIP_TRY(hipSetDevice(c->device));
+  const u64 tiles = (count + 1) / 2;
+  crc32_uniform4k_kernel<512, false, false><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), (hipStream_t)stream>>>(
+      static_cast<const uint8_t*>(dev_base), 0, count, c->d_tab, c->d_laneops, 0u, 0u, dev_out, 0, nullptr,
+      SlotArgs{});
+  HIP_TRY(hipGetLastError());
+  return SUBSPACE_CRC_OK;
 }
 
 // Tuning hook for experiments (not part of the public header): uniform-kernel workgroup

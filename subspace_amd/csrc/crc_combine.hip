@@ -92,13 +92,13 @@ __device__ __forceinline__ typename Op::T shfl_xor_t(typename Op::T v, int m) {
 // beyond the grid means the counter was not zero at launch (stale state, or a call racing
 // another on the context's workspace): kFaultTicket is raised and the caller leaves at once
 // (its status word would lie past the scan's words), workgroup-uniformly.
-__device__ __forceinline__ u64 scan_ticket(u32* ticket, u32* fault, bool* stale) {
+__device__ __forceinline__ u64 scan_ticket(u32* ticket, FaultRef fault, bool* stale) {
   __shared__ u32 s_tile;
   if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
   __syncthreads();
   const u64 t = s_tile;
   *stale = t >= gridDim.x;
-  if (*stale && threadIdx.x == 0) raise_fault(fault, kFaultTicket);
+  if (*stale && threadIdx.x == 0) raise_scan_fault(fault, kFaultTicket);
   return t;
 }
 
@@ -109,7 +109,7 @@ __device__ __forceinline__ u64 scan_ticket(u32* ticket, u32* fault, bool* stale)
 // kFaultLookbackSpin in the context's fault word, so the call reports an error
 // (subspace_crc_ctx_check) instead of returning wrong CRCs as OK, and the GPU never hangs.
 template <class Op, int ITEMS>
-__device__ __forceinline__ void scan_tile_lookback(typename Op::T (&x)[ITEMS], u64 tile, u64* status, u32* fault) {
+__device__ __forceinline__ void scan_tile_lookback(typename Op::T (&x)[ITEMS], u64 tile, u64* status, FaultRef fault) {
   using T = typename Op::T;
   __shared__ T s_wave[kScanThreads / 64];
   __shared__ T s_prefix;
@@ -153,7 +153,7 @@ __device__ __forceinline__ void scan_tile_lookback(typename Op::T (&x)[ITEMS], u
             s = __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           } while (Op::flag(s) == 0 && ++spins < kSpinBound);
           if (Op::flag(s) == 0) {
-            raise_fault(fault, kFaultLookbackSpin);
+            raise_scan_fault(fault, kFaultLookbackSpin);
             s = Op::pack(kFlagInclusive, Op::identity());
           }
         }
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kScanThreads) void crc32_ragged_count_scan_kernel(
     const u64* __restrict__ offsets, u32 ostride, const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
     u32 final_xor, u64* __restrict__ tile_base, u32* __restrict__ out, u32* __restrict__ zero_word,
     u64* __restrict__ status, u32* __restrict__ ticket, u32* __restrict__ chunk_msg, u64 nchunks,
-    u32* __restrict__ fault) {
+    FaultRef fault) {
   __shared__ u64 sx[kCountTile];  // striped (coalesced) global order <-> per-thread runs
   bool stale;
   const u64 tile = scan_ticket(ticket, fault, &stale);
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256) void tile_segment_scan_kernel(const u32* __res
 __global__ __launch_bounds__(kScanThreads) void segment_prefix_kernel(u32* __restrict__ segx, u64 nseg, u32 nw,
                                                                       u32 nwb, const u64* __restrict__ total_ptr,
                                                                       u64 n_cap, u64* __restrict__ status,
-                                                                      u32* __restrict__ ticket, u32* __restrict__ fault) {
+                                                                      u32* __restrict__ ticket, FaultRef fault) {
   bool stale;
   const u64 tile = scan_ticket(ticket, fault, &stale);
   if (stale) return;

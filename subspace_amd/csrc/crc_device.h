@@ -80,8 +80,29 @@ constexpr u32 kSlotFusedMaxMeta = 64;  // metadata bytes the fused slot kernel f
 constexpr u32 kFaultLookbackSpin = 1u;  // a look-back scan predecessor never published
 constexpr u32 kFaultTicket = 2u;        // a look-back scan ticket beyond the grid (stale ticket)
 constexpr u32 kFaultSlotRing = 4u;      // a slot finishing wave waited too long for a payload CRC
+constexpr u32 kFaultGrid = 8u;          // a kernel got more tiles per wave than its ring window
 __device__ __forceinline__ void raise_fault(u32* fault, u32 bit) {
   if (fault) __hip_atomic_fetch_or(fault, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The look-back scans' faults (kFaultTicket, kFaultLookbackSpin) also mark the call they
+// happened in: word[1] of the fault words takes the call's generation (a per-context counter,
+// never 0), so the kernels of that call that would index with its untrusted tile_base do
+// nothing, while a later call on the context -- whose kernels reset the scan state as usual --
+// runs normally even when nobody has called subspace_crc_ctx_check in between (ADVICE r03:
+// the accumulated word[0] alone made every later call skip and return the previous CRCs).
+struct FaultRef {
+  u32* word;  // the context's fault words: [0] kFault* bits (ctx_check), [1] generation
+  u32 gen;    // this call's generation
+};
+__device__ __forceinline__ void raise_scan_fault(FaultRef f, u32 bit) {
+  if (f.word) {
+    __hip_atomic_fetch_or(f.word, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(f.word + 1, f.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// A look-back scan of this call gave up: its tile_base is not to be trusted.
+__device__ __forceinline__ bool scan_faulted(FaultRef f) {
+  return f.word && __hip_atomic_load(f.word + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == f.gen;
 }
 // spin bounds: ~2^20 polls of s_sleep(8) (~0.2 s), far beyond any real wait
 constexpr u32 kSpinBound = 1u << 20;
@@ -119,7 +140,7 @@ constexpr int kSmallInvOps = 12;
 constexpr int kSmallOpSlots = kSmallOpInv + kSmallInvOps;
 constexpr u32 kSmallMaxExt = 4096;  // extended bytes (length + offset & 15) of one half-tile
 constexpr u32 kSmallRing = kLdsOps + (u32)kSmallOpSlots * 512u;  // per-wave result rings
-constexpr u32 kSmallRingTiles = 32;                               // tiles per ring window
+constexpr u32 kSmallRingTiles = 32;                               // tiles per wave (one ring window)
 constexpr u32 kSmallRingBytesPerWave = kSmallRingTiles * 2u * 8u;  // (value | code << 32) per message
 constexpr size_t small_lds_bytes() { return kSmallRing + 8u * kSmallRingBytesPerWave; }
 static_assert(small_lds_bytes() <= 160u * 1024u, "small-message kernel LDS exceeds 160 KiB");
@@ -145,6 +166,7 @@ struct SmallArgs {
   u32* zero_word;    // !SLOT, optional: zeroed at the end (the next kernel's mismatch count)
   const u32* rops;   // the ragged operator array (Z_8192; Z_4096^{-1}, the 13th padding inverse)
   const u32* pow2;   // SLOT: Z_{2^k}, k < 64 (a long message's Z_L)
+  u32* fault;        // context fault word (kFaultGrid: a grid too small for the batch)
 };
 
 // Ragged path: tiles per wave of the descriptor kernel, = the chunk of the tile-count scan's
@@ -187,6 +209,9 @@ __device__ __forceinline__ u32 lds_ld_volatile(u32 addr) {
 __device__ __forceinline__ u32x4 lds_ld4(u32 addr) { return *reinterpret_cast<const lds_u32x4_t*>((uintptr_t)addr); }
 __device__ __forceinline__ void lds_st4(u32 addr, u32x4 v) { *reinterpret_cast<lds_u32x4_t*>((uintptr_t)addr) = v; }
 
+#ifndef SUBSPACE_FILL_ROTATE
+#define SUBSPACE_FILL_ROTATE 1  // conflict-free table fill (0: the round-3 store order, for A/B builds)
+#endif
 // Fill of the replicated step tables and the first NOPS operator slots, split into a
 // load phase and a store phase so a kernel can issue its first tile's global loads in
 // between: vmcnt retires in issue order, so the table loads (older) can be waited for
@@ -223,8 +248,16 @@ struct LdsFill {
         const int k = t & 3, e = t >> 2;
         const u32x4 vv = {tv[i], tv[i], tv[i], tv[i]};
         const u32 dst = sbase + (((u32)(k >> 1) << 16) | ((u32)e << 8) | ((u32)(k & 1) << 7));
+        // A lane writes its entry's 32 copies as 8 x 16 B, starting at chunk (lane & 7): every
+        // entry row is 128-B aligned, so without the rotation all lanes of a ds_write_b128 lane
+        // group (8 consecutive lanes) hit the same 4 banks, an 8-way conflict (64 instead of 8
+        // LDS cycles per store: ~7,200 cycles per CU per launch, 78 % of the uniform kernel's
+        // SQ_LDS_BANK_CONFLICT, profiles/r04/ledger).
 #pragma unroll
-        for (int j = 0; j < 8; j++) lds_st4(dst + 16 * j, vv);
+        for (int j = 0; j < 8; j++) {
+          const u32 jj = SUBSPACE_FILL_ROTATE ? ((u32)(j + tid) & 7u) : (u32)j;
+          lds_st4(dst + 16u * jj, vv);
+        }
       }
     }
 #pragma unroll

@@ -86,12 +86,6 @@ __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, u32 ostrid
   return d;
 }
 
-// A look-back scan of this call gave up (kFaultTicket / kFaultLookbackSpin): tile_base is not
-// to be trusted, so the kernels that index with it do nothing (the call reports the fault).
-__device__ __forceinline__ bool scan_faulted(const u32* fault) {
-  return fault && (__hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
-                   (kFaultTicket | kFaultLookbackSpin)) != 0u;
-}
 
 // Per tile (up to `capacity`): its descriptor. Sets *overflow if the batch has more tiles.
 // Wave g covers tiles [g*kDescTilesPerWave, +kDescTilesPerWave). The message of its first
@@ -109,7 +103,7 @@ __global__ __launch_bounds__(256) void crc32_ragged_desc_kernel(const u64* __res
                                                                 const u64* __restrict__ tile_base, u64 count,
                                                                 u64 capacity, const u32* __restrict__ chunk_msg,
                                                                 TileDesc* __restrict__ desc, u32* __restrict__ overflow, u64* scan_status,
-                                                                u64 scan_words, u32* scan_ticket, const u32* fault) {
+                                                                u64 scan_words, u32* scan_ticket, FaultRef fault) {
   reset_scan_state(scan_status, scan_words, scan_ticket);  // the tile-count scan is done
   if (scan_faulted(fault)) return;
   const u64 total = tile_base[count];
@@ -334,7 +328,7 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
                                                           const u32* __restrict__ overflow,
                                                           const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                           HeadSeeds seeds, u32* __restrict__ out,
-                                                          u32* __restrict__ tilecrc, u64 nkmax, const u32* fault) {
+                                                          u32* __restrict__ tilecrc, u64 nkmax, FaultRef fault) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
   if (scan_faulted(fault)) return;  // workgroup-uniform, before any barrier
@@ -350,7 +344,7 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
 
 template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
                                                   const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds,
-                                                  u32*, u32*, u64, const u32*);
+                                                  u32*, u32*, u64, FaultRef);
 
 // Per message with tiles: its padded CRC = XOR of its tiles' values = P(t1 - 1) ^ P(t0 - 1)
 // (P = inclusive XOR prefix of the tile values in tile order, crc_combine.hip), or the XOR
@@ -362,7 +356,7 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
                                           const u32* __restrict__ local, const u32* __restrict__ segx, u32 nw, u32 nwb,
                                           const u32* __restrict__ overflow, const u32* __restrict__ gops,
                                           u32 final_xor, u32* __restrict__ out, u64* scan_status, u64 scan_words,
-                                          u32* scan_ticket, const u32* fault) {
+                                          u32* scan_ticket, FaultRef fault) {
   reset_scan_state(scan_status, scan_words, scan_ticket);  // the segment scan is done
   if (scan_faulted(fault)) return;
   // the 13 inverse operators (6.5 KiB) staged in LDS: up to 104 dependent table lookups

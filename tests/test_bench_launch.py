@@ -78,3 +78,37 @@ def test_settle_waits_for_a_steady_launch_rate():
     assert not steady([(0.0104, 50)] * 60 + [(0.0100, 50)] * 60)  # still speeding up (4 %)
     assert steady([(0.01002, 50)] * 60 + [(0.0100, 50)] * 60)  # within 0.3 %
     assert steady([(0.0100, 50)] * 60 + [(0.0104, 50)] * 60)  # slowing down: nothing to wait for
+
+
+def _rank_envs(stdout: str) -> dict:
+    recs = [json.loads(ln) for ln in stdout.splitlines() if ln.startswith('{"rank"')]
+    return {r["rank"]: r["env"] for r in recs}
+
+
+def test_both_launch_forms_give_ranks_the_same_environment():
+    """the driver starts `python -m torch.distributed.run --nproc-per-node N
+    ... bench.py --gpus N`, a plain `python bench.py --gpus N` spawns the same itself. In both,
+    every rank must see HSA_ENABLE_IPC_MODE_LEGACY=0 before torch or HIP initialise (bench.py
+    apply_rank_env, first thing in main), even when the parent environment lacks it."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "HSA_ENABLE_IPC_MODE_LEGACY")}
+    spawn = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--print-rank-env"],
+                           capture_output=True, text=True, timeout=120, env=env, cwd=str(ROOT))
+    assert spawn.returncode == 0, spawn.stderr[-3000:]
+    port = _bench_module().free_port()
+    driver = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                             "--master-addr=127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"),
+                             "--gpus", "2", "--print-rank-env"],
+                            capture_output=True, text=True, timeout=120, env=env, cwd=str(ROOT))
+    assert driver.returncode == 0, driver.stderr[-3000:]
+    a, b = _rank_envs(spawn.stdout), _rank_envs(driver.stdout)
+    assert sorted(a) == sorted(b) == [0, 1]
+    assert a == b
+    for r in (0, 1):
+        assert a[r]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+        assert a[r]["WORLD_SIZE"] == "2" and a[r]["MASTER_ADDR"] == "127.0.0.1"
+    # a value the caller sets is kept, not overridden
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    again = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--print-rank-env"],
+                           capture_output=True, text=True, timeout=120, env=env, cwd=str(ROOT))
+    assert _rank_envs(again.stdout) == a

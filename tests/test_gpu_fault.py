@@ -3,9 +3,10 @@
 The look-back scans of the ragged path (crc_combine.hip) keep a ticket and status words in
 the context that every call expects at zero. A stale ticket used to be absorbed by a bounded
 spin that substituted the identity prefix: wrong CRCs and SUBSPACE_CRC_OK. Now the kernels
-raise a bit in the context's fault word, the downstream kernels skip work that would index
-with an untrusted tile_base, and subspace_crc_ctx_check returns SUBSPACE_CRC_EFAULT (then
-clears the fault and resets the scan state, so the next call is correct again).
+raise a bit in the context's fault word, the downstream kernels of that call (its generation
+in the fault words) skip work that would index with an untrusted tile_base, and
+subspace_crc_ctx_check returns SUBSPACE_CRC_EFAULT (then clears the fault and resets the scan
+state). A later call is correct with or without a check in between.
 """
 import numpy as np
 import pytest
@@ -72,3 +73,26 @@ def test_calls_on_two_streams_are_ordered(gpu_ctx, oracle):
     gpu_ctx.check()
     assert np.array_equal(out1.cpu().numpy().view(np.uint32), oracle.synth_crc_batch(0x5151, len1))
     assert np.array_equal(out2.cpu().numpy().view(np.uint32), oracle.synth_crc_batch(0x5252, len2))
+
+
+def test_fault_marks_only_its_own_call(gpu_ctx, oracle):
+    """a scan fault marks the call it happened in (the fault words' generation),
+    not every later one. A caller that never calls check still gets correct CRCs from the next
+    call (whose kernels start from the state the faulted call's later kernels reset), and the
+    fault is still reported by the next check."""
+    lib = _lib.load()
+    n = 3 * 4096
+    buf, d_off, d_len, lengths = _ragged_batch(n, seed=0xFA18)
+    want = oracle.synth_crc_batch(0xFA18, lengths)
+    out = torch.zeros(n, dtype=torch.int32, device=DEV)
+    gpu_ctx.check()
+    assert lib.subspace_crc_testutil_set(gpu_ctx._h, b"stale_ticket", 1 << 30) == 0
+    gpu_ctx.crc32_ragged(buf, d_off, d_len, out)  # faults: its kernels skip
+    out2 = torch.zeros(n, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_ragged(buf, d_off, d_len, out2)  # no check in between
+    torch.cuda.synchronize()
+    assert np.array_equal(out2.cpu().numpy().view(np.uint32), want)
+    with pytest.raises(gpu.CrcError) as ei:
+        gpu_ctx.check()
+    assert ei.value.code == gpu.EFAULT
+    gpu_ctx.check()  # cleared
