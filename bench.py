@@ -74,7 +74,7 @@ def parse():
     # (r02c27), 5,583 after 0.9 s on another box (r02c26) and 5,550 after 5 s (r02c28), later
     # processes 5,520-5,583; reported as "settle_launches" (--settle 0 disables both). 8 s: a
     # large VRAM free by an earlier process (a test run's 118 GB) is wiped in the background
-    # for 4-8 s, slowing every HBM-bound kernel 2-4 % (profiles/r03/wipe).
+    # for 4-8 s, slowing every HBM-bound kernel 2-4 % (profiles/DESIGN_r01-r03.md 6, profiles/r03/wipe).
     ap.add_argument("--settle", type=int, default=400)
     ap.add_argument("--settle-s", type=float, default=8.0)
     # --streams 2: consecutive steps alternate between two HIP streams (independent batches)
@@ -244,6 +244,24 @@ def cpu_baseline(samples: dict, runs: int) -> dict:
                      "value_all_cores": round(nbytes / float(np.median(tn)) / 2**30, 3)}
         del touched
     arena_b, offs_b, lens_b, _ = samples["B"]
+    # informational: config B's sample on every CPU of the affinity set (nproc may count a whole
+    # machine shared with other jobs; BASELINE.md's plan says "all cores", `value` keeps the
+    # job's share)
+    all_aff = None
+    aff = share["affinity_cpus"]
+    if aff > threads:
+        touched = orc.first_touch_copy(arena_b, offs_b, lens_b, aff)
+        ta, pinned_a = [], 0
+        for _ in range(runs):
+            t = time.perf_counter()
+            got_a, pinned_a = orc.crc32_batch_pinned(touched, offs_b, lens_b, threads=aff)
+            ta.append(time.perf_counter() - t)
+        del touched
+        all_aff = {"value": round(BATCH_BYTES / float(np.median(ta)) / 2**30, 3), "threads": aff,
+                   "workers_pinned": pinned_a, "bitexact": bool(np.array_equal(got_a, orc.crc32_batch(
+                       arena_b, offs_b, lens_b, threads=threads))),
+                   "note": "config B's sample, one pinned worker per CPU of the affinity set; informational "
+                           "(the CPUs beyond the job's share belong to other jobs' GPUs on the gpurun boxes)"}
     sse = None
     if orc.has_sse42():  # informational: the reference's -msse4.2 path computes CRC-32C
         ts = []
@@ -277,6 +295,7 @@ def cpu_baseline(samples: dict, runs: int) -> dict:
             "cores_note": "cores = the job's CPU share: the affinity set, limited by OMP_NUM_THREADS where set "
                           "(16 per GPU on the gpurun boxes, where nproc counts the whole machine)",
             "configs": per,
+            "all_affinity_cpus": all_aff,
             "sse42_crc32c_value": sse,
             "sse42_crc32c_note": "client/checksum.cc:56-76 (-msse4.2 builds) restated on config B's sample and "
                                  "the same threads: CRC-32C, NOT bit-exact with the IEEE parity path; informational",
@@ -496,7 +515,7 @@ def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, re
     # ... and, up to SETTLE_CAP_S, until the launch rate is steady: the mean time per launch of
     # the last 0.5 s within 0.3 % of the 0.5 s before. VRAM freed to the driver (by this or an
     # earlier process, e.g. a test run's 118 GB config-C buffer) is wiped in the background for
-    # several seconds, and every HBM-bound kernel runs 2-4 % slower meanwhile (DESIGN.md 6,
+    # several seconds, and every HBM-bound kernel runs 2-4 % slower meanwhile (profiles/DESIGN_r01-r03.md 6,
     # tools/s_launches.py, r03s4-r03s6)
     blocks = []  # (seconds, launches) per block of back-to-back launches
     while (n_settle < max(0, settle - warmup) or time.perf_counter() - t_settle < settle_s or
@@ -574,7 +593,7 @@ def read_ceiling(wl, launches=400):
 def time_calls(fn, iters, warm_ms=60.0):
     """ms per call: one HIP event pair around `iters` back-to-back calls (after ~warm_ms of
     back-to-back warm-up calls: a stop-and-go warm-up leaves short calls in the GPU's
-    power-management ramp), / iters -- the headline's timing rule."""
+    power-management ramp, profiles/DESIGN_r01-r03.md 4.0), / iters -- the headline's timing rule."""
     import torch
     fn()
     torch.cuda.synchronize()
@@ -720,7 +739,8 @@ def slot_configs(ctx, dev, iters) -> dict:
                                             mode=gpu.SLOT_VERIFY, status=status, error_count=errs), 50)
     torch.cuda.synchronize()
     ok = int(errs.item()) == 0 and bool((status == 0).all().item())
-    res["S_list_verify"] = config_line(nbytes, ms, ok, "subspace_crc32_slots (ragged kernel + slot finish)", {
+    res["S_list_verify"] = config_line(nbytes, ms, ok, "subspace_crc32_slots: subspace_amd::crc32_small_kernel<512, "
+                                      "true> (one launch, slots finished in it; crc_small.hip)", {
         "workload": "S_list: config S's 65,536 slots as a device slot list (subspace_crc_slot records) in "
                     "shuffled order, verify",
         "check": "every slot passes"})
@@ -985,13 +1005,17 @@ def main():
             return cpu_baseline(samples, args.cpu_runs)
         cpu = optional(cpu_leg)
 
-    traffic = None
-    # PMC-measured HBM bytes per config-B launch (tools/summarize_profile.py); other
+    traffic, traffic_source = None, None
+    # PMC-measured HBM bytes per config-B launch (tools/summarize_profile.py), read from the
+    # committed profile: PMC passes are separate rocprofv3 runs, not part of this process; other
     # workloads' launches are a different size, so no figure for them
     tfile = ROOT / "profiles" / "traffic_uniform4k.json"
     if tfile.exists() and args.workload == "B":
         try:
-            traffic = json.loads(tfile.read_text()).get("hbm_bytes_per_launch")
+            tj = json.loads(tfile.read_text())
+            traffic = tj.get("hbm_bytes_per_launch")
+            traffic_source = (f"profiles/traffic_uniform4k.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, "
+                              f"{tj.get('source', '?')}; not measured in this run)")
         except (OSError, ValueError):
             traffic = None
 
@@ -1048,7 +1072,8 @@ def main():
             "per_gpu_value": round(value / world, 2),
             "bitexact_vs_golden": bitexact,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_source,
+                         "kernel": kernel,
                          "avg_launch_ms": round(avg_kern_ms, 4),
                          "launch_ms_source": f"HIP event span of rank 0's timed region / K ({args.streams} stream(s), "
                                              "consecutive launches overlap when 2)",

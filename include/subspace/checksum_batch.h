@@ -70,6 +70,7 @@ enum class SlotCheck : uint32_t {
   kUnchecked = SUBSPACE_CRC_SLOT_UNCHECKED,  // the publisher stored no checksum
   kSkipped = 3u,                             // the subscriber has checksums off: valid, not read
 };
+static_assert(SUBSPACE_CRC_SLOT_OVERSIZE != 3u, "kSkipped is not a library status");
 
 inline constexpr const char* kChecksumVerificationFailed = "Checksum verification failed";
 
@@ -206,6 +207,7 @@ class BatchChecksum {
   // has kMessageHasChecksum (client/client.cc:1346-1356); slots without it are kUnchecked.
   int Verify(const std::vector<ChecksumSlot>& slots, uint64_t max_message_size, const ChecksumOptions& opts,
              std::vector<SlotCheck>* results, uint32_t* mismatches = nullptr) {
+    if (const int rc = check_options(opts)) return rc;
     if (!opts.checksum) {  // ValidateChecksum: options_.Checksum() false -> true, nothing read
       if (results) results->assign(slots.size(), SlotCheck::kSkipped);
       if (mismatches) *mismatches = 0;
@@ -236,6 +238,7 @@ class BatchChecksum {
   // Publisher batch of one channel (client/publisher.cc:664-675): nothing with checksums off;
   // else SetHasChecksum() and the callback's or the CRC32 checksum into the checksum area.
   int Calculate(const std::vector<ChecksumSlot>& slots, uint64_t max_message_size, const ChecksumOptions& opts) {
+    if (const int rc = check_options(opts)) return rc;
     if (!opts.checksum) return SUBSPACE_CRC_OK;
     if (!opts.callback) return Calculate(slots, max_message_size, opts.checksum_size, opts.metadata_size);
     for (const ChecksumSlot& s : slots) {
@@ -264,6 +267,8 @@ class BatchChecksum {
         error_ = "channel index out of range";
         return SUBSPACE_CRC_EINVAL;
       }
+    for (const ChecksumOptions& o : channels)
+      if (const int rc = check_options(o)) return rc;
     std::vector<SlotCheck> out(slots.size(), SlotCheck::kSkipped);
     uint32_t bad = 0;
     // group the slots: by channel for callbacks (each has its own callback), by span shape
@@ -329,6 +334,21 @@ class BatchChecksum {
   static const subspace_crc_slot* recs(const std::vector<ChecksumSlot>& s) {
     return reinterpret_cast<const subspace_crc_slot*>(s.data());
   }
+  // The device path's argument rules (capi.hip check_slot_args) for every gated form, so a
+  // callback channel with a bad size fails the same way instead of throwing (a negative size
+  // as a vector length) or passing silently.
+  int check_options(const ChecksumOptions& o) {
+    if (o.checksum_size < 4) {
+      error_ = "checksum_size < 4";
+      return SUBSPACE_CRC_EINVAL;
+    }
+    if (o.metadata_size < 0) {
+      error_ = "metadata_size < 0";
+      return SUBSPACE_CRC_EINVAL;
+    }
+    return SUBSPACE_CRC_OK;
+  }
+
   int fail(int rc) {
     error_ = subspace_crc_last_error();
     return rc;

@@ -129,6 +129,9 @@ int subspace_crc32_batch(subspace_crc_ctx* ctx, const void* dev_base, uint64_t a
 #define SUBSPACE_CRC_SLOT_OK 0u        /* checksum stored (CALCULATE) or matched (VERIFY) */
 #define SUBSPACE_CRC_SLOT_MISMATCH 1u  /* VERIFY: "Checksum verification failed" (client/client.cc:1447) */
 #define SUBSPACE_CRC_SLOT_UNCHECKED 2u /* VERIFY: prefix has no kMessageHasChecksum flag */
+#define SUBSPACE_CRC_SLOT_OVERSIZE 4u  /* strided layouts: the slot's size exceeds its payload area
+                                          (slot_stride - prefix size); neither checksummed nor
+                                          modified, not counted as a mismatch */
 
 /* One slot: device addresses of its MessagePrefix and payload, and the payload size
  * (slot->message_size at publish, the delivered size at read). 24 B, device array. */
@@ -154,7 +157,9 @@ int subspace_crc32_slots(subspace_crc_ctx* ctx, const subspace_crc_slot* dev_slo
  * payload at prefix + ComputePrefixSize(checksum_size, metadata_size)
  * (= Aligned<64>(48 + checksum_size + metadata_size), common/channel.h:914-919).
  * Payload sizes: dev_message_sizes[i] (uint64) when not NULL, else `message_size` for
- * every slot. */
+ * every slot. A per-slot size larger than the slot's payload area (slot_stride - prefix size:
+ * the reference never publishes more than the slot holds) gets SUBSPACE_CRC_SLOT_OVERSIZE: its
+ * bytes would run into the next slot, whose prefix a publish rewrites in the same call. */
 int subspace_crc32_slots_strided(subspace_crc_ctx* ctx, void* dev_buffer, uint64_t slot_stride, uint64_t count,
                                  uint64_t message_size, const uint64_t* dev_message_sizes, int32_t checksum_size,
                                  int32_t metadata_size, uint32_t mode, uint32_t* dev_status,

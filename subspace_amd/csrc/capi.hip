@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -16,7 +17,7 @@
 
 namespace subspace_amd {
 
-template <int WG, bool SLOT, bool PROBE>
+template <int WG, bool SLOT, bool PROBE, bool SHIFT2>
 __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int, u32*,
                                        SlotArgs);
 
@@ -33,8 +34,8 @@ __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*,
                                     FaultRef);
 __global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, const u64*, u32, u64, const u32*, const u32*,
                                           u32, u32, const u32*, const u32*, u32, u32*, u64*, u64, u32*, FaultRef);
-__global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, int, int, u32, const u32*,
-                                         const u32*, const u32*, u32*, u32*, u32*);
+__global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, u64, int, int, u32,
+                                         const u32*, const u32*, const u32*, u32*, u32*, u32*);
 __global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*);
 __global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* offsets, u64* lengths);
 template <int WG>
@@ -111,6 +112,8 @@ struct subspace_crc_ctx {
   u32* d_rops = nullptr;  // ragged kernel: line-shift operators, Z_4096, tile shifts, padding inverses
   u32* d_pow2 = nullptr;  // Z_{2^k}, k = 0..63, nibble operators (slot checksums)
   u32* d_laneops = nullptr;  // uniform kernel: Z_{128*s}, s = 0..31, as [nibble][value][s]; Z_4096
+  u32* d_laneops2 = nullptr;  // two-shift plain kernel: Z_{128*s}, then Z_{128*s + 64}, s = 0..31
+  bool uniform_shift2 = false;  // config-B-shaped batches take the two-shift plain kernel
   Tables host_tab;
   Mat32 zinv1;  // Z_1^{-1}: the ragged kernel's head seeds Z_r^{-1}(init)
   // ragged workspace
@@ -192,6 +195,10 @@ struct subspace_crc_ctx {
 namespace {
 
 constexpr u32 kSlotCounters = 64;  // the fused slot kernel's counter ring (subspace_crc_ctx::d_slot_counter)
+#ifndef SUBSPACE_UNIFORM_SHIFT2
+#define SUBSPACE_UNIFORM_SHIFT2 0
+#endif
+constexpr bool kUniformShift2Default = SUBSPACE_UNIFORM_SHIFT2 != 0;  // the two-shift plain kernel by default
 
 bool capturing(hipStream_t st) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -246,9 +253,14 @@ int fault_status(subspace_crc_ctx* c, hipStream_t st) {
   HIP_TRY(hipMemcpyAsync(&f, c->d_fault, sizeof(u32), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (f == 0) return SUBSPACE_CRC_OK;
-  HIP_TRY(hipMemsetAsync(c->d_fault, 0, 2 * sizeof(u32), st));
-  HIP_TRY(hipMemsetAsync(c->d_slot_counter, 0, kSlotCounters * sizeof(u64), st));
-  HIP_TRY(hipStreamSynchronize(st));
+  // (rare path) a fused slot kernel of this context may still run on another stream, and it
+  // owns a counter word and may raise more bits: let every stream finish before the reset
+  // (ADVICE r03), then report everything raised
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(&f, c->d_fault, sizeof(u32), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemset(c->d_fault, 0, 2 * sizeof(u32)));
+  HIP_TRY(hipMemset(c->d_slot_counter, 0, kSlotCounters * sizeof(u64)));
+  HIP_TRY(hipDeviceSynchronize());
   c->scan_dirty = true;
   return fail(SUBSPACE_CRC_EFAULT, "device fault 0x%x: %s; the results of the calls since the last check are not valid",
               f, fault_text(f));
@@ -423,6 +435,7 @@ struct SmallSlot {
   const u64* prefixes;
   u32 pstride;
   u64 pdelta;
+  u64 max_len;  // larger sizes: SUBSPACE_CRC_SLOT_OVERSIZE (~0: no bound)
   u32 mode;
   int32_t checksum_size, metadata_size;
   u32 *status, *crc_out, *error_count;
@@ -453,6 +466,7 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
     a.prefixes = slot->prefixes;
     a.pstride = slot->pstride;
     a.pdelta = slot->pdelta;
+    a.max_len = slot->max_len;
     a.mode = slot->mode;
     a.checksum_size = (u32)slot->checksum_size;
     a.metadata_size = (u32)slot->metadata_size;
@@ -508,11 +522,12 @@ bool was_zeroed(subspace_crc_ctx* c, u32* err) {
 }
 
 int slot_finish(subspace_crc_ctx* c, const u64* slots, uint8_t* buf, u64 stride, const u64* sizes, u64 usize,
-                u64 count, int32_t cs, int32_t ms, u32 mode, u32* status, u32* err, hipStream_t st,
+                u64 count, u64 max_len, int32_t cs, int32_t ms, u32 mode, u32* status, u32* err, hipStream_t st,
                 u32* crc_out = nullptr, bool err_zeroed = false) {
   if (err && !err_zeroed) HIP_TRY(hipMemsetAsync(err, 0, sizeof(u32), st));
   crc32_slot_finish_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(
-      slots, buf, stride, sizes, usize, count, cs, ms, mode, c->d_crc0, c->d_tab, c->d_pow2, status, err, crc_out);
+      slots, buf, stride, sizes, usize, count, max_len, cs, ms, mode, c->d_crc0, c->d_tab, c->d_pow2, status, err,
+      crc_out);
   HIP_TRY(hipGetLastError());
   return SUBSPACE_CRC_OK;
 }
@@ -552,8 +567,12 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   c->poly = poly;
   c->host_tab = make_tables(poly);
   c->zinv1 = inverse(z_one(c->host_tab));
+  // experiment hook: SUBSPACE_CRC_UNIFORM_SHIFT2=0/1 overrides the default (A/B sessions)
+  c->uniform_shift2 = kUniformShift2Default;
+  if (const char* v = std::getenv("SUBSPACE_CRC_UNIFORM_SHIFT2")) c->uniform_shift2 = v[0] == '1';
 
-  std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kSmallOpSlots * 128, 0u), rops(kRagOpWords, 0u);
+  std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kSmallOpSlots * 128, 0u), rops(kRagOpWords, 0u),
+      laneops2(kShift2OpSlots * 128, 0u);
   for (int k = 0; k < 4; k++)
     for (int b = 0; b < 256; b++) tab[k * 256 + b] = c->host_tab.t[k][b];
 
@@ -568,6 +587,13 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
     for (int k = 0; k < 8; k++)
       for (int n = 0; n < 16; n++) laneops[((size_t)k * 16 + n) * 32 + sl] = nt[k * 16 + n];
   }
+  for (int sl = 0; sl < 32; sl++) {  // the two-shift kernel's second set: Z_{128*s + 64}
+    u32 nt[128];
+    nibble_tables(z_bytes(c->host_tab, 128ull * sl + 64), nt);
+    for (int k = 0; k < 8; k++)
+      for (int n = 0; n < 16; n++) laneops2[kLaneOpWords + ((size_t)k * 16 + n) * 32 + sl] = nt[k * 16 + n];
+  }
+  std::copy(laneops.begin(), laneops.begin() + kLaneOpWords, laneops2.begin());
   // ragged kernel: the line-shift operators, Z_4096, Z_{8192 * 2^k} for k = 0..20, Z_64 (x4)
   // -- the LDS part -- then Z_{8192 * 2^k} for k = 21..30 (crc_device.h ragged layout)
   std::copy(laneops.begin(), laneops.begin() + kLaneOpWords, rops.begin());
@@ -596,6 +622,8 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   hipError_t e = hipMalloc(&c->d_tab, tab.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_laneops, laneops.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(c->d_laneops, laneops.data(), laneops.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&c->d_laneops2, laneops2.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(c->d_laneops2, laneops2.data(), laneops2.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&c->d_rops, rops.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_pow2, pow2.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(c->d_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice);
@@ -603,19 +631,22 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess) e = hipMemcpy(c->d_rops, rops.data(), rops.size() * 4, hipMemcpyHostToDevice);
 #define SET_LDS(WGV)                                                                                         \
   if (e == hipSuccess)                                                                                       \
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV, false, false>,                                  \
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV, false, false, false>,                                  \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_lds_bytes(WGV / 64));
   SET_LDS(256) SET_LDS(512) SET_LDS(768) SET_LDS(1024)
 #undef SET_LDS
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)uniform_slot_lds_bytes(8));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, false, true>,
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, false, true, false>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_lds_bytes(8));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, true>,
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, true, false>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_slot_lds_bytes(8));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, false, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_shift2_lds_bytes());
   if (e == hipSuccess) e = hipMalloc(&c->d_slot_counter, kSlotCounters * sizeof(u64));
   if (e == hipSuccess) e = hipMemset(c->d_slot_counter, 0, kSlotCounters * sizeof(u64));
   if (e == hipSuccess) e = hipMalloc(&c->d_fault, 4 * sizeof(u32));
@@ -668,6 +699,7 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_rops);
   (void)hipFree(c->d_pow2);
   (void)hipFree(c->d_laneops);
+  (void)hipFree(c->d_laneops2);
   (void)hipFree(c->d_crc0);
   (void)hipFree(c->d_soff);
   (void)hipFree(c->d_tbase);
@@ -751,14 +783,21 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     if (c->probe != nullptr) {  // experiment hook: the timestamp-recording instantiation (512 threads)
       SlotArgs sa{};
       sa.probe = c->probe;
-      crc32_uniform4k_kernel<512, false, true><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), st>>>(
+      crc32_uniform4k_kernel<512, false, true, false><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), st>>>(
           b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, sa);
       c->zero_word = nullptr;
       HIP_TRY(hipGetLastError());
       return SUBSPACE_CRC_OK;
     }
+    if (c->uniform_shift2 && wg == 512) {
+      crc32_uniform4k_kernel<512, false, false, true><<<blocks, 512, uniform_shift2_lds_bytes(), st>>>(
+          b, stride, count, c->d_tab, c->d_laneops2, init, final_xor, dev_out, ord, c->zero_word, SlotArgs{});
+      c->zero_word = nullptr;
+      HIP_TRY(hipGetLastError());
+      return SUBSPACE_CRC_OK;
+    }
 #define LAUNCH(WGV)                                                                                           \
-  crc32_uniform4k_kernel<WGV, false, false><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(                             \
+  crc32_uniform4k_kernel<WGV, false, false, false><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(                             \
       b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, SlotArgs{})
     switch (wg) {
       case 256: LAUNCH(256); break;
@@ -846,7 +885,7 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
   if (small && small_slot_fused(checksum_size, metadata_size)) {
     // one kernel, the slots finished in it; no context workspace (the counter ring, as the
     // fused uniform slot kernel)
-    const SmallSlot ss{rec, 3, 0, mode, checksum_size, metadata_size, dev_status, nullptr, dev_error_count};
+    const SmallSlot ss{rec, 3, 0, ~0ull, mode, checksum_size, metadata_size, dev_status, nullptr, dev_error_count};
     return small_run(c, nullptr, rec + 1, 3, rec + 2, 3, count, 0u, 0u, nullptr, st, &ss);
   }
   rc = use_workspace(c, st);
@@ -862,7 +901,7 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
   }
   const bool zeroed = was_zeroed(c, dev_error_count);
   if (rc) return rc;
-  return slot_finish(c, rec, nullptr, 0, nullptr, 0, count, checksum_size, metadata_size, mode, dev_status,
+  return slot_finish(c, rec, nullptr, 0, nullptr, 0, count, ~0ull, checksum_size, metadata_size, mode, dev_status,
                      dev_error_count, st, nullptr, zeroed);
 }
 
@@ -892,6 +931,9 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
   if (!dev_message_sizes && slot_stride < prefix_size + message_size && count > 1)
     return fail(SUBSPACE_CRC_EINVAL, "slot_stride %llu < prefix %llu + message %llu",
                 (unsigned long long)slot_stride, (unsigned long long)prefix_size, (unsigned long long)message_size);
+  if (dev_message_sizes && slot_stride < prefix_size && count > 1)
+    return fail(SUBSPACE_CRC_EINVAL, "slot_stride %llu < prefix %llu", (unsigned long long)slot_stride,
+                (unsigned long long)prefix_size);
   HIP_TRY(hipSetDevice(c->device));
   auto* buf = static_cast<uint8_t*>(dev_buffer);
   // Fused path (crc_uniform.hip SLOT): 4 KiB payloads, 16-B aligned, no metadata span -- the
@@ -907,10 +949,10 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
                 c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters), c->probe, c->d_fault,
                 (u32)checksum_size, (u32)metadata_size};
     if (c->probe)  // experiment hook: the timestamp-recording instantiation
-      crc32_uniform4k_kernel<512, true, true><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
+      crc32_uniform4k_kernel<512, true, true, false><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
           buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, 0, nullptr, sa);
     else
-      crc32_uniform4k_kernel<512, true, false><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
+      crc32_uniform4k_kernel<512, true, false, false><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
           buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, 0, nullptr, sa);
     HIP_TRY(hipGetLastError());
     return SUBSPACE_CRC_OK;
@@ -926,12 +968,12 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
     HIP_TRY(hipGetLastError());
     const bool aligned = slot_stride % 16 == 0 && ((uintptr_t)(buf + prefix_size) % 16) == 0;
     if (count > 1 && small_fits(slot_stride - prefix_size, aligned) && c->small_path) {
-      // slots of at most 4 KiB (a larger size, past its slot, still gets its CRC: the small
-      // kernel's last workgroup); the prefix of slot i is its payload offset - prefix_size
+      // slots of at most 4 KiB (a size beyond the slot's payload area is OVERSIZE); the prefix
+      // of slot i is its payload offset - prefix_size
       if (small_slot_fused(checksum_size, metadata_size)) {
         was_zeroed(c, dev_error_count);  // the fused kernel writes the count itself
-        const SmallSlot ss{c->d_soff, 1, prefix_size, mode, checksum_size, metadata_size, dev_status, dev_crc_out,
-                           dev_error_count};
+        const SmallSlot ss{c->d_soff, 1, prefix_size, slot_stride - prefix_size, mode, checksum_size, metadata_size,
+                           dev_status, dev_crc_out, dev_error_count};
         return small_run(c, buf, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, nullptr, st, &ss);
       }
       rc = small_run(c, buf, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st);
@@ -945,7 +987,9 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
   }
   const bool zeroed = was_zeroed(c, dev_error_count);
   if (rc) return rc;
-  return slot_finish(c, nullptr, buf, slot_stride, dev_message_sizes, message_size, count, checksum_size,
+  // a per-slot size beyond the payload area: SUBSPACE_CRC_SLOT_OVERSIZE (one slot: no bound)
+  const u64 max_len = dev_message_sizes && count > 1 ? slot_stride - prefix_size : ~0ull;
+  return slot_finish(c, nullptr, buf, slot_stride, dev_message_sizes, message_size, count, max_len, checksum_size,
                      metadata_size, mode, dev_status, dev_error_count, st, dev_crc_out, zeroed);
 }
 
@@ -1236,6 +1280,10 @@ int subspace_crc_testutil_set(subspace_crc_ctx* c, const char* key, int value) {
     c->fused_slots = value != 0;
     return SUBSPACE_CRC_OK;
   }
+  if (!std::strcmp(key, "uniform_shift2")) {  // 1: 4 KiB batches take the two-shift plain kernel (A/B)
+    c->uniform_shift2 = value != 0;
+    return SUBSPACE_CRC_OK;
+  }
   if (!std::strcmp(key, "small_path")) {  // 0: messages <= 4 KiB take the ragged path (A/B, parity)
     c->small_path = value != 0;
     return SUBSPACE_CRC_OK;
@@ -1273,7 +1321,7 @@ int subspace_crc_testutil_uniform_alias(subspace_crc_ctx* c, const void* dev_bas
   CallScope scope(c);
   HIP_TRY(hipSetDevice(c->device));
   const u64 tiles = (count + 1) / 2;
-  crc32_uniform4k_kernel<512, false, false><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), (hipStream_t)stream>>>(
+  crc32_uniform4k_kernel<512, false, false, false><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), (hipStream_t)stream>>>(
       static_cast<const uint8_t*>(dev_base), 0, count, c->d_tab, c->d_laneops, 0u, 0u, dev_out, 0, nullptr,
       SlotArgs{});
   HIP_TRY(hipGetLastError());

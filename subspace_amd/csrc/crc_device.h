@@ -41,6 +41,13 @@ constexpr int kUniSlotOpZ64 = kUniSlotOpZ4096 + 1;
 constexpr int kUniOpSlots = kUniSlotOpZ64 + 4;
 constexpr int kUniOpSlotsOneChain = kUniSlotOpZ4096 + 1;
 constexpr u32 kUniRing = kLdsOps + kUniOpSlots * 512u;
+// Two-shift variant of the plain kernel (crc_uniform.hip SHIFT2): no Z_64 join; the line's two
+// 64-B chains are shifted by their own per-lane operators, Z_{128 s} (slots 0..31, as above) and
+// Z_{128 s + 64} (slots 32..63), both conflict-free, so the LDS holds the tables and 32 KiB of
+// lane operators (exactly 160 KiB) and the results are parked in a register instead of a ring.
+constexpr int kShift2OpSlots = 64;
+constexpr size_t uniform_shift2_lds_bytes() { return kLdsOps + (size_t)kShift2OpSlots * 512u; }
+static_assert(uniform_shift2_lds_bytes() <= 160u * 1024u, "two-shift kernel LDS exceeds 160 KiB");
 // results per wave ring: 256 (128 tiles), or 128 where 16 waves' rings would not fit
 constexpr int uni_ring_results(int waves) { return kUniRing + (u32)waves * 1024u <= 160u * 1024u ? 256 : 128; }
 constexpr size_t uniform_lds_bytes(int waves) { return kUniRing + (size_t)waves * 4u * uni_ring_results(waves); }
@@ -104,7 +111,10 @@ __device__ __forceinline__ void raise_scan_fault(FaultRef f, u32 bit) {
 __device__ __forceinline__ bool scan_faulted(FaultRef f) {
   return f.word && __hip_atomic_load(f.word + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == f.gen;
 }
-// spin bounds: ~2^20 polls of s_sleep(8) (~0.2 s), far beyond any real wait
+// Spin bound of every bounded wait, far beyond any real one: the look-back scans poll an
+// uncached status word up to 2^20 times without sleeping (~1 s, tests/test_gpu_fault.py); the
+// fused slot kernel's finishing waves poll their LDS ring up to 2^20 times with s_sleep(2)
+// between polls (~0.1 s).
 constexpr u32 kSpinBound = 1u << 20;
 // Per-wave probe record of the uniform kernel's PROBE instantiation: realtime clock (100 MHz)
 // at entry, after the LDS fill + barrier, after the tile loop, at exit, after the table and
@@ -167,6 +177,8 @@ struct SmallArgs {
   const u32* rops;   // the ragged operator array (Z_8192; Z_4096^{-1}, the 13th padding inverse)
   const u32* pow2;   // SLOT: Z_{2^k}, k < 64 (a long message's Z_L)
   u32* fault;        // context fault word (kFaultGrid: a grid too small for the batch)
+  u64 max_len;       // SLOT: a larger message size is SUBSPACE_CRC_SLOT_OVERSIZE (strided layouts:
+                     // the slot's payload area); ~0 for slot lists
 };
 
 // Ragged path: tiles per wave of the descriptor kernel, = the chunk of the tile-count scan's
@@ -391,7 +403,7 @@ __device__ __forceinline__ void drain_before_issue() { asm volatile("s_waitcnt v
 // and issues the next one's loads, then drops back to 0 for the lookups. The two waves of a
 // SIMD otherwise issue oldest first, so a younger wave whose tile has landed waits behind its
 // partner's lookups before its next loads go out. Config B 44.6-45.3 vs 44.9-45.5 us, the
-// stride-4,160 plain kernel 45.7 vs 46.4 (interleaved, r03s15/r03s16).
+// stride-4,160 plain kernel 45.7 vs 46.4 (interleaved, r03s15/r03s16; profiles/DESIGN_r01-r03.md 4.1).
 #ifndef SUBSPACE_ISSUE_PRIO
 #define SUBSPACE_ISSUE_PRIO 1
 #endif

@@ -51,10 +51,11 @@ __device__ u32 shift_zeros(const u32* __restrict__ gpow2, u32 v, u64 n) {
 
 // Slot i: prefix = slots ? slots[3i] : buf + i*stride; payload size = slots ? slots[3i+2]
 // : (sizes ? sizes[i] : usize). CALCULATE also writes the stored value to crc_out[i] when
-// crc_out is not null.
+// crc_out is not null. A size above max_len (strided layouts: the slot's payload area) is
+// SUBSPACE_CRC_SLOT_OVERSIZE: nothing stored or compared.
 __global__ __launch_bounds__(kSlotWG) void crc32_slot_finish_kernel(
     const u64* __restrict__ slots, uint8_t* __restrict__ buf, u64 stride, const u64* __restrict__ sizes, u64 usize,
-    u64 count, int checksum_size, int metadata_size, u32 mode, const u32* __restrict__ crc0,
+    u64 count, u64 max_len, int checksum_size, int metadata_size, u32 mode, const u32* __restrict__ crc0,
     const u32* __restrict__ gtab, const u32* __restrict__ gpow2, u32* __restrict__ status,
     u32* __restrict__ error_count, u32* __restrict__ crc_out) {
   __shared__ u32 t[1024];
@@ -65,6 +66,10 @@ __global__ __launch_bounds__(kSlotWG) void crc32_slot_finish_kernel(
   uint8_t* prefix = slots ? reinterpret_cast<uint8_t*>(slots[3 * i]) : buf + i * stride;
   const u64 len = slots ? slots[3 * i + 2] : (sizes ? sizes[i] : usize);
   u32* pw = reinterpret_cast<u32*>(prefix);  // 8-B aligned (int64 fields)
+  if (len > max_len) {
+    if (status) status[i] = 4u;  // SUBSPACE_CRC_SLOT_OVERSIZE
+    return;
+  }
 
   // span 0: prefix[4, 48) = dwords 1..11; flags (int64 at offset 32) is dword 8
   u32 w[12];

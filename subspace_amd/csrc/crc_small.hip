@@ -6,7 +6,7 @@
 // ~118 us for 65,536 slots of 4 KiB) with one kernel, because a message of at most one
 // half-tile needs neither a tile index nor a cross-tile combine.
 //
-// Decomposition (DESIGN.md 4.3):
+// Decomposition (DESIGN.md 4.4):
 //  * Message m = bytes [s, s + L) of base (s = offsets[m*ostride], L = lengths[m*lstride]),
 //    mis = s & 15, extended length E = L + mis. With E <= 4096 it fills one half of a tile:
 //    lane l of half h owns the 128-B line [s0 + 128 l, +128) of message 2 tau + h, s0 = s -
@@ -105,7 +105,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // message, an empty one, or one longer than a half-tile, computed apart: long_crc).
   auto ext = [&](u32 k, u64 s, u64 L) __attribute__((always_inline)) -> u32 {
     const u64 E = L + (s & 15u);
-    return (k < nk && msg_of(k) < count && L != 0 && E <= kSmallMaxExt) ? (u32)E : 0u;
+    return (k < nk && msg_of(k) < count && L != 0 && E <= kSmallMaxExt && (!SLOT || L <= a.max_len)) ? (u32)E
+                                                                                                    : 0u;
   };
   auto load_lines = [&](u32x4 (&D)[8], u64 s, u32 E) __attribute__((always_inline)) {
     const uint8_t* p0 = E ? base + (s & ~(u64)15) : safe;
@@ -132,8 +133,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // Each message's value and code are parked in the wave's LDS ring, entry 2 k + h.
   // Code: p = 4096 - E (bits 0-11) | mis << 12 for a half-tile message (value: Z_p(crc_raw(
   // init, D))); kCodeLong for a longer one (computed after the loop: long_crc); kCodeEmpty for
-  // length 0 (CRC init ^ final_xor; a checksum over the spans only); kCodeSkip for no message.
-  constexpr u32 kCodeLong = 0x20000000u, kCodeEmpty = 0x40000000u, kCodeSkip = 0x80000000u;
+  // length 0 (CRC init ^ final_xor; a checksum over the spans only); kCodeSkip for no message;
+  // SLOT: kCodeOversize for a size beyond the slot's payload area (nothing read, computed or
+  // stored: SUBSPACE_CRC_SLOT_OVERSIZE).
+  constexpr u32 kCodeOversize = 0x10000000u, kCodeLong = 0x20000000u, kCodeEmpty = 0x40000000u,
+                kCodeSkip = 0x80000000u;
   auto process = [&](const u32x4 (&cur)[8], u64 s, u64 L, u32 k) __attribute__((always_inline)) {
     const u32 mis = (u32)s & 15u;
     const u32 E = ext(k, s, L);
@@ -161,8 +165,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u64 m = msg_of(k);
     const bool present = k < nk && m < count;
     const bool over = present && L + mis > kSmallMaxExt;
-    const u32 code = !present ? kCodeSkip
-                   : over     ? kCodeLong
+    const u32 code = !present                  ? kCodeSkip
+                   : SLOT && L > a.max_len     ? kCodeOversize
+                   : over                      ? kCodeLong
                    : L == 0   ? kCodeEmpty
                               : (kSmallMaxExt - E) | (mis << 12);
     // lane 31 of each half: its message's value and code, one 8-B LDS store
@@ -324,9 +329,10 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32 r = long_crc(s, L, P);
     v = lane == (int)src ? r : v;
   }
-  const bool half = code < kCodeLong;  // a half-tile message: Z_p undone here
+  const bool half = code < kCodeOversize;  // a half-tile message: Z_p undone here
   if constexpr (SLOT) {
-    const bool live = code != kCodeSkip;
+    const bool oversize = code == kCodeOversize;
+    const bool live = code != kCodeSkip && !oversize;
     if constexpr (!SUBSPACE_SMALL_EARLY_PFX) fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
     const uint8_t* pfx = live ? base + fpre - a.pdelta : safe;  // (a read-only block)
     u32 F, S;
@@ -338,6 +344,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32 R = half ? inv_bits(X, code & 0xFFFu, kSmallInvOps) : (code == kCodeLong ? v : H);
     const u32 res = ~R;  // *reinterpret_cast<uint32_t*>(checksum.data()) = ~crc (client/checksum.h:36)
     u32 mism = 0;
+    if (oversize && a.status) a.status[fm] = 4u;  // SUBSPACE_CRC_SLOT_OVERSIZE
     if (calc) {
       if (live) {
         u32* pw = reinterpret_cast<u32*>(const_cast<uint8_t*>(pfx));

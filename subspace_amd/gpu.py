@@ -19,7 +19,7 @@ POLY_CASTAGNOLI = 0x82F63B78  # CRC-32C: -msse4.2 reference builds (SubspaceCRC3
 # message-slot checksums (include/subspace_crc.h)
 SLOT_CALCULATE = 0  # publisher: set kMessageHasChecksum, store the 3-span checksum in the prefix
 SLOT_VERIFY = 1     # subscriber: check the stored checksum of slots that carry the flag
-SLOT_OK, SLOT_MISMATCH, SLOT_UNCHECKED = 0, 1, 2
+SLOT_OK, SLOT_MISMATCH, SLOT_UNCHECKED, SLOT_OVERSIZE = 0, 1, 2, 4  # 3: the C++ helper's kSkipped
 EFAULT = -5  # SUBSPACE_CRC_EFAULT: a kernel of an earlier call gave up a bounded wait
 
 

@@ -177,9 +177,28 @@ int main(int argc, char** argv) {
     no_device_rc = batch.VerifyDrain(one, c0, opts, kSlotSize, &got);
     failures += no_device_rc == SUBSPACE_CRC_OK;
   }
+  // bad span sizes on the callback forms fail like the device path's (EINVAL), never throw
+  // (a negative checksum_size once became a huge scratch vector: ADVICE r03)
+  int bad_args = 0;
+  {
+    subspace::ChecksumOptions neg = ch[1].opts, small = ch[1].opts, negmeta = ch[1].opts;
+    neg.checksum_size = -1;
+    small.checksum_size = 3;
+    negmeta.metadata_size = -5;
+    std::vector<subspace::ChecksumSlot> one = {drain[0]};
+    std::vector<uint32_t> c0 = {0};
+    for (const subspace::ChecksumOptions& o : {neg, small, negmeta}) {
+      bad_args += batch.Verify(one, kSlotSize, o, &got) == SUBSPACE_CRC_EINVAL;
+      bad_args += batch.Calculate(one, kSlotSize, o) == SUBSPACE_CRC_EINVAL;
+      std::vector<subspace::ChecksumOptions> o1 = {o};
+      bad_args += batch.VerifyDrain(one, c0, o1, kSlotSize, &got) == SUBSPACE_CRC_EINVAL;
+    }
+    failures += bad_args != 9;
+  }
   std::printf("{\"mode\": \"%s\", \"drained\": %zu, \"mismatches\": %u, \"expected_mismatches\": %u, "
-              "\"callback_mismatches\": %u, \"skipped\": %u, \"no_device_rc\": %d, \"failures\": %d}\n",
-              full ? "full" : "host", drain.size(), mism, want_mism, cb_mism, skipped, no_device_rc, failures);
+              "\"callback_mismatches\": %u, \"skipped\": %u, \"no_device_rc\": %d, \"bad_args_einval\": %d, "
+              "\"failures\": %d}\n",
+              full ? "full" : "host", drain.size(), mism, want_mism, cb_mism, skipped, no_device_rc, bad_args, failures);
   if (full) batch.UnregisterBuffer(mem);
   munmap(mem, total);
   close(fd);

@@ -522,3 +522,38 @@ def test_verify_metadata_channels(gpu_ctx, oracle, cs, ms):
     torch.cuda.synchronize()
     assert np.array_equal(st.cpu().numpy().view(np.uint32), want)
     assert int(err.item()) == int((want == 1).sum()) > 0
+
+
+@pytest.mark.parametrize("slot_size,cs,ms", [(1000, 4, 0), (4000, 8, 5), (1000, 4, 100), (5000, 20, 32)])
+def test_strided_oversize_sizes_are_flagged(gpu_ctx, oracle, slot_size, cs, ms):
+    """a per-slot size beyond the slot's payload area would run into the next slot,
+    whose prefix a publish rewrites in the same (fused) launch. Such slots get
+    SUBSPACE_CRC_SLOT_OVERSIZE and are left untouched, on every path: the fused small-slot
+    kernel (1000 / 4000-B slots), small + finish kernels (metadata > 64 B), ragged + finish
+    (5000-B slots); every other slot is published and verified as the oracle's."""
+    count = 900
+    rng = np.random.default_rng(slot_size + ms)
+    area = (slot_size + 63) & ~63
+    sizes = rng.integers(0, area + 1, count).astype(np.uint64)
+    big = rng.random(count) < 0.1
+    sizes[big] = rng.integers(area + 1, area + 3000, int(big.sum()))
+    host, ps, stride = build_channel(count, slot_size, cs, ms, sizes, seed=slot_size + cs + ms)
+    assert stride - ps == area
+    orig = host.copy()
+    dev, status = publish_strided(gpu_ctx, host, stride, count, cs, ms, sizes=sizes)
+    assert np.array_equal(status == gpu.SLOT_OVERSIZE, big)
+    assert (status[~big] == 0).all()
+    po, yo = offsets(count, stride, ps)
+    oracle.publish_slots(host, po[~big], yo[~big], sizes[~big], cs, ms)
+    got = dev.cpu().numpy()
+    assert np.array_equal(got, host)
+    for i in np.nonzero(big)[0]:  # oversize slots: prefix untouched
+        assert np.array_equal(got[i * stride:i * stride + ps], orig[i * stride:i * stride + ps])
+    st = torch.full((count,), 7, dtype=torch.int32, device=DEV)
+    err = torch.full((1,), 123, dtype=torch.int32, device=DEV)
+    d_sizes = torch.from_numpy(sizes.view(np.int64)).to(DEV)
+    gpu_ctx.crc32_slots_strided(dev, stride, count, sizes=d_sizes, checksum_size=cs, metadata_size=ms,
+                                mode=gpu.SLOT_VERIFY, status=st, error_count=err)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert np.array_equal(st == gpu.SLOT_OVERSIZE, big) and (st[~big] == 0).all() and int(err.item()) == 0

@@ -356,7 +356,7 @@ def test_r02s3i_prefix_variant_was_in_bounds():
     """The round-2 variant that faulted (r02s3i: three dwordx4 prefix loads per window at
     prefix + 4, + 20, + 36) read inside each slot: its addresses were in bounds, so the fault
     was not an out-of-range address -- the property it alone had is the 4-B-aligned b128 load
-    (DESIGN.md 4.4). Every product b128 load is 16-B aligned (test above)."""
+    (DESIGN.md 4.8). Every product b128 load is 16-B aligned (test above)."""
     stride, prefix = 4160, 64
     for msg in (0, 1, 65535):
         addrs = [msg * stride + off for off in (4, 20, 36)]
@@ -427,3 +427,111 @@ def test_small_kernel_loads_stay_in_messages(seed, count, G):
             if L and L + (s & 15) <= 4096:
                 assert covered.get(m) == set(range(s, s + L)), m
 
+
+
+# ------------------------------------------------------------------ zero-copy host slot lists
+def small_grid(count, num_cus=256):
+    """capi.hip small_run: one workgroup per CU, or more so no wave gets more than 32 tiles."""
+    tiles = (count + 1) // 2
+    return max(min(num_cus, max(1, -(-tiles // 8))), -(-tiles // (8 * 32)))
+
+
+def small_slot_accesses(recs, cs, ms, num_cus=256):
+    """Replays every global access of crc32_small_kernel<512, true> (crc_small.hip) for slot
+    records (prefix, payload, size): the line loads of half-tile messages, the whole-wave chunk
+    loads of messages longer than a half-tile (long_crc), the finish's prefix loads (7 x 8 B,
+    then the metadata words), and a publish's two 4-B stores. Yields (slot, kind, address,
+    width); record and table reads (device memory) are left out."""
+    count = len(recs)
+    G = small_grid(count, num_cus)
+    ntiles, nw = (count + 1) // 2, 8 * G
+    for b in range(G):
+        for wid in range(8):
+            t0 = front_slot(b, G, wid)
+            nk = (ntiles - t0 + nw - 1) // nw if t0 < ntiles else 0
+            assert nk <= 32
+            for k in range(nk):
+                for h in (0, 1):
+                    m = 2 * (t0 + k * nw) + h
+                    if m >= count:
+                        continue
+                    pre, s, L = recs[m]
+                    E = L + (s & 15)
+                    s0 = s & ~15
+                    if L and E <= 4096:  # load_lines
+                        lastb = (E - 1) & ~15
+                        for lane in range(32):
+                            for blk in range(8):
+                                yield m, "line", s0 + min(128 * lane + 16 * blk, lastb), 16
+                    elif E > 4096:  # long_crc: 8 KiB chunks, all 64 lanes
+                        for j in range((E + 8191) >> 13):
+                            ln = min(8192, E - (j << 13))
+                            lastb = (ln - 1) & ~15
+                            for lane in range(64):
+                                for blk in range(8):
+                                    yield m, "chunk", s0 + (j << 13) + min(128 * lane + 16 * blk, lastb), 16
+                    for i in range(7):  # span_crc: prefix words 0..13
+                        yield m, "prefix", pre + 8 * i, 8
+                    if ms:
+                        o1 = 48 + cs
+                        sh = o1 & 3
+                        for j in range((sh + ms + 3) >> 2):
+                            yield m, "meta", pre + (o1 & ~3) + 4 * j, 4
+                    yield m, "store", pre + 32, 4  # flags word (SetHasChecksum)
+                    yield m, "store", pre + 48, 4  # checksum
+
+
+@pytest.mark.parametrize("seed,count,cs,ms", [(0, 1, 4, 0), (1, 37, 4, 0), (2, 999, 4, 16), (3, 2001, 20, 33),
+                                              (4, 5000, 64, 64)])
+def test_host_slot_list_accesses_stay_in_registered_regions(seed, count, cs, ms):
+    """VERDICT r03 item 6 (the r02s3i question): the zero-copy drain (subspace_crc32_host_slot_list
+    -> subspace_crc32_slots -> crc32_small_kernel) reads and writes host memory through the
+    device aliases of regions registered with subspace_crc_host_register. capi.hip admits a
+    record only if [prefix, prefix + prefix_size) and [payload, payload + size) each lie inside
+    one registered region; then every access the kernel makes is width-aligned (16-B line and
+    chunk loads on 16-B boundaries, 8-B prefix loads, 4-B metadata words and stores -- no b128
+    load at a 4-B-aligned address, the one property only the faulting r02s3i variant had) and
+    stays inside the 16-B blocks that hold the record's own bytes, hence inside the pinned
+    pages of its region, for payloads at every offset & 15 (a region's first byte included)
+    and for sizes beyond max_message_size (whole-wave chunks)."""
+    rng = np.random.default_rng(seed)
+    ps = ((48 + cs + ms) + 63) & ~63
+    page = 4096
+    # payload regions at arbitrary byte offsets (a payload may start at a region's first byte),
+    # prefixes in one 8-B aligned region, as the ABI requires
+    regions, recs, owner = [], [], []
+    pre_base = 7 * page + 8 * int(rng.integers(0, 32))
+    regions.append((pre_base, count * ps))
+    cursor = 1 << 30
+    for i in range(count):
+        L = int(rng.choice([rng.integers(0, 4097), 4096, rng.integers(4097, 20000)], p=[0.8, 0.15, 0.05]))
+        mis = int(rng.integers(0, 16))
+        start = cursor + mis
+        if rng.random() < 0.3:  # the payload is its region's first byte
+            regions.append((start, max(L, 1)))
+            owner.append(len(regions) - 1)
+        else:
+            owner.append(None)
+        recs.append((pre_base + i * ps, start, L))
+        cursor = ((start + L + 4095) // 4096 + 1) * 4096 + int(rng.integers(0, 64))
+    big = (1 << 30, cursor - (1 << 30))  # one region holding every other payload
+    regions.append(big)
+    order = rng.permutation(count)
+    recs = [recs[i] for i in order]
+    owner = [owner[i] for i in order]
+
+    def pages(reg):
+        a, n = reg
+        return a - a % page, -(-(a + n) // page) * page
+
+    for m, kind, addr, w in small_slot_accesses(recs, cs, ms):
+        assert addr % w == 0, (kind, addr, w)
+        pre, s, L = recs[m]
+        if kind in ("line", "chunk"):
+            assert addr + w > s and addr < s + L, (kind, m, addr)  # a block holding payload bytes
+            reg = regions[owner[m]] if owner[m] is not None else big
+        else:
+            assert pre <= addr and addr + w <= pre + ps, (kind, m, addr)
+            reg = regions[0]
+        lo, hi = pages(reg)
+        assert lo <= addr and addr + w <= hi, (kind, m, addr, reg)

@@ -1,10 +1,11 @@
 #!/bin/bash
 # Interleaved A/B of library builds on one GPU box, one process per run, after one discarded
-# warm-up process (a fresh box's first GPU process runs slower: DESIGN.md 4.0).
+# warm-up process (a fresh box's first GPU process runs slower: profiles/DESIGN_r01-r03.md 4.0).
 #   bash tools/ab_session.sh <tag> <mode> <lib>...
 #   lib:  0 = the product library; N = tools/ubench/probes/libslotN.so
-#         (tools/ubench/build_variants.sh); anything else = a path (e.g. abtmp/lib_x.so from
-#         tools/ab_lib.sh). Repeat libs for an A B A B order.
+#         (tools/ubench/build_variants.sh); env:VAR=VALUE = the product library with VAR set
+#         (a context knob, e.g. env:SUBSPACE_CRC_UNIFORM_SHIFT2=1); anything else = a path
+#         (e.g. abtmp/lib_x.so from tools/ab_lib.sh). Repeat libs for an A B A B order.
 #   mode: slotgap -- tools/slot_gap.py: config S publish / verify vs the plain kernel over the
 #                    same buffers (timing only: variants may compute nothing valid)
 #         uniform -- tools/sweep_uniform.py: config B through the uniform kernel
@@ -15,7 +16,10 @@ set -u
 TAG=$1; MODE=$2; shift 2
 OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/$TAG
 mkdir -p $OUT
-run() {  # $1 = output stem, $2 = library path or ""
+run() {  # $1 = output stem, $2 = library path or "" (or env:VAR=VALUE)
+  local envset=""
+  case $2 in env:*) envset=${2#env:}; set -- "$1" "" ;; esac
+  if [ -n "$envset" ]; then export "${envset?}"; fi
   if [ "$MODE" = slotgap ]; then
     SUBSPACE_CRC_PROBE_LIB=$2 SLOT_GAP_NOCHECK=1 timeout -k 10 200 python tools/slot_gap.py 3 > $OUT/$1.jsonl 2> $OUT/$1.err
   elif [ "$MODE" = slotlist ]; then
@@ -23,6 +27,9 @@ run() {  # $1 = output stem, $2 = library path or ""
   else
     SUBSPACE_CRC_PROBE_LIB=$2 timeout -k 10 200 python tools/sweep_uniform.py 65536 512 7 0 > $OUT/$1.jsonl 2> $OUT/$1.err
   fi
+  local rc=$?
+  if [ -n "$envset" ]; then unset "${envset%%=*}"; fi
+  return $rc
 }
 run warm "" || exit $?
 i=0
@@ -31,11 +38,13 @@ for v in "$@"; do
   lib=""
   if [ "$v" != 0 ]; then
     case $v in
+      env:*) lib=$v ;;
       *[!0-9]*) lib=$v ;;
       *) lib=$PWD/tools/ubench/probes/libslot$v.so ;;
     esac
   fi
-  run "run${i}_$(basename ${v%.so})" "$lib"
+  stem=$(basename "${v%.so}"); stem=${stem//[:=]/_}
+  run "run${i}_$stem" "$lib"
   rc=$?
   echo "run$i $v rc=$rc" >> $OUT/status.txt
   if [ $rc -ne 0 ]; then exit $rc; fi

@@ -19,7 +19,8 @@ for f in sorted(d.glob("run*_*.jsonl")):
             res[lib][r["variant"]].append(r["median_us"])
         else:
             for k, v in r.items():
-                if isinstance(v, (int, float)) and ("us" in k or "ms" in k or "GiB" in k):
+                if isinstance(v, (int, float)) and not isinstance(v, bool) and k not in ("round", "count", "wg",
+                                                                                         "order", "launches"):
                     res[lib][k].append(v)
 for lib, r in sorted(res.items()):
     print(lib, json.dumps({k: sorted(x) for k, x in r.items()}))

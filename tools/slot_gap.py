@@ -42,7 +42,7 @@ def main():
         "slot_verify": lambda b: ctx.crc32_slots_strided(b, stride, N, message_size=SIZE, mode=gpu.SLOT_VERIFY,
                                                          status=status, error_count=errs),
     }
-    for i in range(600):  # power-management settle
+    for i in range(600):  # power-management settle (profiles/DESIGN_r01-r03.md 4.0)
         variants["uniform_4096"](bufs[i % NBUF])
     torch.cuda.synchronize()
     res = {}
