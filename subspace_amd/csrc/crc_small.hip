@@ -57,6 +57,12 @@
 #ifndef SUBSPACE_SMALL_FENCE
 #define SUBSPACE_SMALL_FENCE 0
 #endif
+#ifndef SUBSPACE_SMALL_SPAN_EARLY
+#define SUBSPACE_SMALL_SPAN_EARLY 1  // the slot's span terms hashed in the prologue (0: in the finish)
+#endif
+#ifndef SUBSPACE_SMALL_LOOP_PAD
+#define SUBSPACE_SMALL_LOOP_PAD 0  // s_nop instructions (4 B each) before the tile loop (A/B builds)
+#endif
 
 namespace subspace_amd {
 
@@ -174,6 +180,59 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     if (l == 31u) lds_st64(sring + 8u * (2u * k + h), (u64)v | ((u64)code << 32));
   };
 
+  // SLOT: the prefix terms of a slot: H = crc_raw(~0, span 0 || span 1) with the flag word as
+  // stored (kMessageHasChecksum set first for a publish), the flag word F, the stored checksum
+  // S (prefix + 48) and whether the flag was set. Prefixes are 8-B aligned (the C ABI's rule):
+  // 8-B loads. span_load issues the loads, span_hash computes from the words (so the loads can
+  // be issued ahead of other loads and waited for later).
+  constexpr u32 kW = kSlotFusedMaxMeta / 4 + 2;
+  auto span_load = [&](const uint8_t* pfx, u32 (&w)[14], u32 (&W1)[kW]) __attribute__((always_inline)) {
+    const u64* q = reinterpret_cast<const u64*>(pfx);
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+      const u64 x = q[i];
+      w[2 * i] = (u32)x;
+      w[2 * i + 1] = (u32)(x >> 32);
+    }
+#pragma unroll
+    for (u32 j = 0; j < kW; j++) W1[j] = 0u;
+    if (a.metadata_size) {  // wave-uniform: span 1 after the checksum area (crc_uniform.hip)
+      const u32 o1 = 48u + a.checksum_size, sh = o1 & 3u, ms = a.metadata_size;
+      const u32 nwords = (sh + ms + 3u) >> 2;
+      const u32* p1 = reinterpret_cast<const u32*>(pfx + (o1 & ~3u));
+#pragma unroll
+      for (u32 j = 0; j < kW; j++)
+        if (j < nwords) W1[j] = p1[j];
+    }
+  };
+  auto span_hash = [&](u32 (&w)[14], const u32 (&W1)[kW], u32& F, u32& S, bool& has) __attribute__((always_inline))
+      -> u32 {
+    has = (w[8] & 4u) != 0u;  // kMessageHasChecksum (common/channel.h:62-70)
+    F = calc ? (w[8] | 4u) : w[8];
+    w[8] = F;
+    S = w[12];
+    u32 hh = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 1; i < 12; i++) hh = step4(hh ^ w[i], lc0, lc1);
+    if (a.metadata_size) {  // realigned with a uniform byte shift; full words by step4, the tail by bytes
+      const u32 o1 = 48u + a.checksum_size, sh = o1 & 3u, ms = a.metadata_size;
+      u32 tail = 0;
+#pragma unroll
+      for (u32 j = 0; j + 1 < kW; j++) {
+        const u32 x = __builtin_amdgcn_alignbyte(W1[j + 1], W1[j], sh);
+        if (j < (ms >> 2)) hh = step4(hh ^ x, lc0, lc1);
+        if (j == (ms >> 2)) tail = x;
+      }
+      for (u32 b = 0; b < (ms & 3u); b++) hh = step1(hh, (tail >> (8u * b)) & 0xFFu, lc1);
+    }
+    return hh;
+  };
+  auto span_crc = [&](const uint8_t* pfx, u32& F, u32& S, bool& has) __attribute__((always_inline)) -> u32 {
+    u32 w[14], W1[kW];
+    span_load(pfx, w, W1);
+    return span_hash(w, W1, F, S, has);
+  };
+
   // Prologue: table loads, tile 0's and 1's records, (SLOT) this lane's finishing record,
   // tile 0's lines, then the LDS stores and the barrier (tile 0's latency hides behind the
   // fill). Lane i finishes message i of the ring: tile i / 2, half i & 1.
@@ -185,16 +244,29 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   fetch(1, sB, LB);
   u64 fpre = 0;  // SLOT: the prefix offset of this lane's finishing message (a real record)
   if constexpr (SLOT && SUBSPACE_SMALL_EARLY_PFX) fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
+  // SLOT, SUBSPACE_SMALL_SPAN_EARLY: the slot's prefix words are loaded here, ahead of tile 0's
+  // lines, and hashed right after the barrier while tile 0 is in flight, so the finish after the
+  // loop only combines (no prefix round trip in the kernel's tail)
+  u32 pwords[14], pmeta[kW];
+  if constexpr (SLOT && SUBSPACE_SMALL_EARLY_PFX && SUBSPACE_SMALL_SPAN_EARLY) {
+    span_load(flive ? base + fpre - a.pdelta : safe, pwords, pmeta);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   u32x4 A[8], B[8];
   u64 sc = sA, Lc = LA;
   load_lines(A, sc, ext(0, sc, Lc));
   fill.store(sbase);
   if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
   __syncthreads();
+  u32 eF = 0, eS = 0, eH = 0;
+  bool ehas = false;
+  if constexpr (SLOT && SUBSPACE_SMALL_EARLY_PFX && SUBSPACE_SMALL_SPAN_EARLY) eH = span_hash(pwords, pmeta, eF, eS, ehas);
 
   // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines: the
   // uniform kernel's stream plus two record loads per tile, nothing else in the loop.
   u32 k = 0;
+#pragma unroll
+  for (int i = 0; i < SUBSPACE_SMALL_LOOP_PAD; i++) asm volatile("s_nop 0");
   for (; k + 1 < nk; k += 2) {
     issue_prio_hi();       // (crc_device.h)
     drain_before_issue();  // tile k's lines and tile k+1's record
@@ -225,48 +297,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   const u64 e = lds_ld64(sring + 8u * (u32)lane);
   u32 v = (u32)e;
   const u32 code = flive ? (u32)(e >> 32) : kCodeSkip;
-  // SLOT: the prefix terms of a slot: H = crc_raw(~0, span 0 || span 1) with the flag word as
-  // stored (kMessageHasChecksum set first for a publish), the flag word F, the stored checksum
-  // S (prefix + 48) and whether the flag was set. Prefixes are 8-B aligned (the C ABI's rule):
-  // 8-B loads.
-  auto span_crc = [&](const uint8_t* pfx, u32& F, u32& S, bool& has) __attribute__((always_inline)) -> u32 {
-    const u64* q = reinterpret_cast<const u64*>(pfx);
-    u32 w[14];
-#pragma unroll
-    for (int i = 0; i < 7; i++) {
-      const u64 x = q[i];
-      w[2 * i] = (u32)x;
-      w[2 * i + 1] = (u32)(x >> 32);
-    }
-    has = (w[8] & 4u) != 0u;  // kMessageHasChecksum (common/channel.h:62-70)
-    F = calc ? (w[8] | 4u) : w[8];
-    w[8] = F;
-    S = w[12];
-    u32 hh = 0xFFFFFFFFu;
-#pragma unroll
-    for (int i = 1; i < 12; i++) hh = step4(hh ^ w[i], lc0, lc1);
-    if (a.metadata_size) {  // wave-uniform: span 1 after the checksum area (crc_uniform.hip)
-      const u32 o1 = 48u + a.checksum_size, sh = o1 & 3u, ms = a.metadata_size;
-      const u32 nwords = (sh + ms + 3u) >> 2;
-      const u32* p1 = reinterpret_cast<const u32*>(pfx + (o1 & ~3u));
-      constexpr u32 kW = kSlotFusedMaxMeta / 4 + 2;
-      u32 W1[kW];
-#pragma unroll
-      for (u32 j = 0; j < kW; j++) {
-        W1[j] = 0u;
-        if (j < nwords) W1[j] = p1[j];
-      }
-      u32 tail = 0;
-#pragma unroll
-      for (u32 j = 0; j + 1 < kW; j++) {
-        const u32 x = __builtin_amdgcn_alignbyte(W1[j + 1], W1[j], sh);
-        if (j < (ms >> 2)) hh = step4(hh ^ x, lc0, lc1);
-        if (j == (ms >> 2)) tail = x;
-      }
-      for (u32 b = 0; b < (ms & 3u); b++) hh = step1(hh, (tail >> (8u * b)) & 0xFFu, lc1);
-    }
-    return hh;
-  };
   // A message longer than a half-tile, by the whole wave (s, L, P wave-uniform): 8 KiB chunks
   // as the ragged kernel's tiles (lines, line shifts, halves joined by Z_4096), acc =
   // Z_8192(acc) ^ chunk, the last chunk's padding p = 8192 nt - E < 8192 undone (b < 12 from
@@ -335,9 +365,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const bool live = code != kCodeSkip && !oversize;
     if constexpr (!SUBSPACE_SMALL_EARLY_PFX) fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
     const uint8_t* pfx = live ? base + fpre - a.pdelta : safe;  // (a read-only block)
-    u32 F, S;
-    bool has;
-    const u32 H = span_crc(pfx, F, S, has);
+    u32 F = eF, S = eS, H = eH;
+    bool has = ehas;
+    if constexpr (!(SUBSPACE_SMALL_EARLY_PFX && SUBSPACE_SMALL_SPAN_EARLY)) H = span_crc(pfx, F, S, has);
     // Z_p(crc_raw(H, payload)) = Z_4096(Z_mis^{-1}(H)) ^ V, then Z_p undone
     const u32 Hm = inv_bits(H, half ? (code >> 12) & 15u : 0u, 4);
     const u32 X = opmul(sbase, kUniSlotOpZ4096, Hm) ^ v;

@@ -49,6 +49,9 @@
 #ifndef SUBSPACE_SLOT_VARIANT
 #define SUBSPACE_SLOT_VARIANT 0
 #endif
+#ifndef SUBSPACE_UNI_LOOP_PAD
+#define SUBSPACE_UNI_LOOP_PAD 0  // s_nop instructions (4 B each) before the tile loop (A/B builds)
+#endif
 
 namespace subspace_amd {
 
@@ -256,6 +259,8 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   constexpr u32 kWin = SLOT ? ~0u : (u32)(kRing / 2);
   u32 k = 0, kf = 0;
   u64 pt_finish = 0;  // PROBE, SLOT: when a finishing wave began
+#pragma unroll
+  for (int i = 0; i < SUBSPACE_UNI_LOOP_PAD; i++) asm volatile("s_nop 0");
   for (; k + 1 < nk; k += 2) {
     const u64 qB = addr_before_wait(k + 1);
     issue_prio_hi();
