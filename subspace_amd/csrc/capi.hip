@@ -6,7 +6,6 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -17,7 +16,7 @@
 
 namespace subspace_amd {
 
-template <int WG, bool SLOT, bool PROBE, bool SHIFT2>
+template <int WG, bool SLOT, bool PROBE>
 __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, const u32*, u32, u32, u32*, int, u32*,
                                        SlotArgs);
 
@@ -112,8 +111,6 @@ struct subspace_crc_ctx {
   u32* d_rops = nullptr;  // ragged kernel: line-shift operators, Z_4096, tile shifts, padding inverses
   u32* d_pow2 = nullptr;  // Z_{2^k}, k = 0..63, nibble operators (slot checksums)
   u32* d_laneops = nullptr;  // uniform kernel: Z_{128*s}, s = 0..31, as [nibble][value][s]; Z_4096
-  u32* d_laneops2 = nullptr;  // two-shift plain kernel: Z_{128*s}, then Z_{128*s + 64}, s = 0..31
-  bool uniform_shift2 = false;  // config-B-shaped batches take the two-shift plain kernel
   Tables host_tab;
   Mat32 zinv1;  // Z_1^{-1}: the ragged kernel's head seeds Z_r^{-1}(init)
   // ragged workspace
@@ -195,10 +192,6 @@ struct subspace_crc_ctx {
 namespace {
 
 constexpr u32 kSlotCounters = 64;  // the fused slot kernel's counter ring (subspace_crc_ctx::d_slot_counter)
-#ifndef SUBSPACE_UNIFORM_SHIFT2
-#define SUBSPACE_UNIFORM_SHIFT2 0
-#endif
-constexpr bool kUniformShift2Default = SUBSPACE_UNIFORM_SHIFT2 != 0;  // the two-shift plain kernel by default
 
 bool capturing(hipStream_t st) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -242,7 +235,6 @@ const char* fault_text(u32 f) {
   if (f & kFaultTicket) return "a look-back scan ticket was beyond its grid (stale scan state)";
   if (f & kFaultLookbackSpin) return "a look-back scan predecessor never published (stale scan state)";
   if (f & kFaultSlotRing) return "a fused slot kernel finishing wave never received a payload CRC";
-  if (f & kFaultGrid) return "a small-message kernel was launched with more tiles per wave than its ring holds";
   return "unknown fault";
 }
 
@@ -455,9 +447,8 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
   a.out = out;
   a.rops = c->d_rops;
   a.pow2 = c->d_pow2;
-  a.fault = c->d_fault;
   // one workgroup per CU, or more, so that no wave gets more than one ring window of tiles
-  // (the kernel's loop holds no flush: crc_small.hip)
+  // (the kernel's in-loop flush then never runs: crc_small.hip)
   const u64 tiles = (count + 1) / 2;
   const unsigned blocks =
       (unsigned)std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSmallRingTiles));
@@ -567,12 +558,8 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   c->poly = poly;
   c->host_tab = make_tables(poly);
   c->zinv1 = inverse(z_one(c->host_tab));
-  // experiment hook: SUBSPACE_CRC_UNIFORM_SHIFT2=0/1 overrides the default (A/B sessions)
-  c->uniform_shift2 = kUniformShift2Default;
-  if (const char* v = std::getenv("SUBSPACE_CRC_UNIFORM_SHIFT2")) c->uniform_shift2 = v[0] == '1';
 
-  std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kSmallOpSlots * 128, 0u), rops(kRagOpWords, 0u),
-      laneops2(kShift2OpSlots * 128, 0u);
+  std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kSmallOpSlots * 128, 0u), rops(kRagOpWords, 0u);
   for (int k = 0; k < 4; k++)
     for (int b = 0; b < 256; b++) tab[k * 256 + b] = c->host_tab.t[k][b];
 
@@ -587,13 +574,6 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
     for (int k = 0; k < 8; k++)
       for (int n = 0; n < 16; n++) laneops[((size_t)k * 16 + n) * 32 + sl] = nt[k * 16 + n];
   }
-  for (int sl = 0; sl < 32; sl++) {  // the two-shift kernel's second set: Z_{128*s + 64}
-    u32 nt[128];
-    nibble_tables(z_bytes(c->host_tab, 128ull * sl + 64), nt);
-    for (int k = 0; k < 8; k++)
-      for (int n = 0; n < 16; n++) laneops2[kLaneOpWords + ((size_t)k * 16 + n) * 32 + sl] = nt[k * 16 + n];
-  }
-  std::copy(laneops.begin(), laneops.begin() + kLaneOpWords, laneops2.begin());
   // ragged kernel: the line-shift operators, Z_4096, Z_{8192 * 2^k} for k = 0..20, Z_64 (x4)
   // -- the LDS part -- then Z_{8192 * 2^k} for k = 21..30 (crc_device.h ragged layout)
   std::copy(laneops.begin(), laneops.begin() + kLaneOpWords, rops.begin());
@@ -622,8 +602,6 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   hipError_t e = hipMalloc(&c->d_tab, tab.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_laneops, laneops.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(c->d_laneops, laneops.data(), laneops.size() * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc(&c->d_laneops2, laneops2.size() * 4);
-  if (e == hipSuccess) e = hipMemcpy(c->d_laneops2, laneops2.data(), laneops2.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&c->d_rops, rops.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_pow2, pow2.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(c->d_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice);
@@ -631,22 +609,19 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess) e = hipMemcpy(c->d_rops, rops.data(), rops.size() * 4, hipMemcpyHostToDevice);
 #define SET_LDS(WGV)                                                                                         \
   if (e == hipSuccess)                                                                                       \
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV, false, false, false>,                                  \
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV, false, false>,                                  \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_lds_bytes(WGV / 64));
   SET_LDS(256) SET_LDS(512) SET_LDS(768) SET_LDS(1024)
 #undef SET_LDS
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)uniform_slot_lds_bytes(8));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, false, true, false>,
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, false, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_lds_bytes(8));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, true, false>,
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_slot_lds_bytes(8));
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, false, false, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_shift2_lds_bytes());
   if (e == hipSuccess) e = hipMalloc(&c->d_slot_counter, kSlotCounters * sizeof(u64));
   if (e == hipSuccess) e = hipMemset(c->d_slot_counter, 0, kSlotCounters * sizeof(u64));
   if (e == hipSuccess) e = hipMalloc(&c->d_fault, 4 * sizeof(u32));
@@ -699,7 +674,6 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_rops);
   (void)hipFree(c->d_pow2);
   (void)hipFree(c->d_laneops);
-  (void)hipFree(c->d_laneops2);
   (void)hipFree(c->d_crc0);
   (void)hipFree(c->d_soff);
   (void)hipFree(c->d_tbase);
@@ -783,21 +757,14 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     if (c->probe != nullptr) {  // experiment hook: the timestamp-recording instantiation (512 threads)
       SlotArgs sa{};
       sa.probe = c->probe;
-      crc32_uniform4k_kernel<512, false, true, false><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), st>>>(
+      crc32_uniform4k_kernel<512, false, true><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), st>>>(
           b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, sa);
       c->zero_word = nullptr;
       HIP_TRY(hipGetLastError());
       return SUBSPACE_CRC_OK;
     }
-    if (c->uniform_shift2 && wg == 512) {
-      crc32_uniform4k_kernel<512, false, false, true><<<blocks, 512, uniform_shift2_lds_bytes(), st>>>(
-          b, stride, count, c->d_tab, c->d_laneops2, init, final_xor, dev_out, ord, c->zero_word, SlotArgs{});
-      c->zero_word = nullptr;
-      HIP_TRY(hipGetLastError());
-      return SUBSPACE_CRC_OK;
-    }
 #define LAUNCH(WGV)                                                                                           \
-  crc32_uniform4k_kernel<WGV, false, false, false><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(                             \
+  crc32_uniform4k_kernel<WGV, false, false><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(                             \
       b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, SlotArgs{})
     switch (wg) {
       case 256: LAUNCH(256); break;
@@ -949,10 +916,10 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
                 c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters), c->probe, c->d_fault,
                 (u32)checksum_size, (u32)metadata_size};
     if (c->probe)  // experiment hook: the timestamp-recording instantiation
-      crc32_uniform4k_kernel<512, true, true, false><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
+      crc32_uniform4k_kernel<512, true, true><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
           buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, 0, nullptr, sa);
     else
-      crc32_uniform4k_kernel<512, true, false, false><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
+      crc32_uniform4k_kernel<512, true, false><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
           buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, 0, nullptr, sa);
     HIP_TRY(hipGetLastError());
     return SUBSPACE_CRC_OK;
@@ -1280,10 +1247,6 @@ int subspace_crc_testutil_set(subspace_crc_ctx* c, const char* key, int value) {
     c->fused_slots = value != 0;
     return SUBSPACE_CRC_OK;
   }
-  if (!std::strcmp(key, "uniform_shift2")) {  // 1: 4 KiB batches take the two-shift plain kernel (A/B)
-    c->uniform_shift2 = value != 0;
-    return SUBSPACE_CRC_OK;
-  }
   if (!std::strcmp(key, "small_path")) {  // 0: messages <= 4 KiB take the ragged path (A/B, parity)
     c->small_path = value != 0;
     return SUBSPACE_CRC_OK;
@@ -1321,7 +1284,7 @@ int subspace_crc_testutil_uniform_alias(subspace_crc_ctx* c, const void* dev_bas
   CallScope scope(c);
   HIP_TRY(hipSetDevice(c->device));
   const u64 tiles = (count + 1) / 2;
-  crc32_uniform4k_kernel<512, false, false, false><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), (hipStream_t)stream>>>(
+  crc32_uniform4k_kernel<512, false, false><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), (hipStream_t)stream>>>(
       static_cast<const uint8_t*>(dev_base), 0, count, c->d_tab, c->d_laneops, 0u, 0u, dev_out, 0, nullptr,
       SlotArgs{});
   HIP_TRY(hipGetLastError());

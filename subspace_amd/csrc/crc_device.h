@@ -41,13 +41,6 @@ constexpr int kUniSlotOpZ64 = kUniSlotOpZ4096 + 1;
 constexpr int kUniOpSlots = kUniSlotOpZ64 + 4;
 constexpr int kUniOpSlotsOneChain = kUniSlotOpZ4096 + 1;
 constexpr u32 kUniRing = kLdsOps + kUniOpSlots * 512u;
-// Two-shift variant of the plain kernel (crc_uniform.hip SHIFT2): no Z_64 join; the line's two
-// 64-B chains are shifted by their own per-lane operators, Z_{128 s} (slots 0..31, as above) and
-// Z_{128 s + 64} (slots 32..63), both conflict-free, so the LDS holds the tables and 32 KiB of
-// lane operators (exactly 160 KiB) and the results are parked in a register instead of a ring.
-constexpr int kShift2OpSlots = 64;
-constexpr size_t uniform_shift2_lds_bytes() { return kLdsOps + (size_t)kShift2OpSlots * 512u; }
-static_assert(uniform_shift2_lds_bytes() <= 160u * 1024u, "two-shift kernel LDS exceeds 160 KiB");
 // results per wave ring: 256 (128 tiles), or 128 where 16 waves' rings would not fit
 constexpr int uni_ring_results(int waves) { return kUniRing + (u32)waves * 1024u <= 160u * 1024u ? 256 : 128; }
 constexpr size_t uniform_lds_bytes(int waves) { return kUniRing + (size_t)waves * 4u * uni_ring_results(waves); }
@@ -87,7 +80,6 @@ constexpr u32 kSlotFusedMaxMeta = 64;  // metadata bytes the fused slot kernel f
 constexpr u32 kFaultLookbackSpin = 1u;  // a look-back scan predecessor never published
 constexpr u32 kFaultTicket = 2u;        // a look-back scan ticket beyond the grid (stale ticket)
 constexpr u32 kFaultSlotRing = 4u;      // a slot finishing wave waited too long for a payload CRC
-constexpr u32 kFaultGrid = 8u;          // a kernel got more tiles per wave than its ring window
 __device__ __forceinline__ void raise_fault(u32* fault, u32 bit) {
   if (fault) __hip_atomic_fetch_or(fault, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -150,7 +142,7 @@ constexpr int kSmallInvOps = 12;
 constexpr int kSmallOpSlots = kSmallOpInv + kSmallInvOps;
 constexpr u32 kSmallMaxExt = 4096;  // extended bytes (length + offset & 15) of one half-tile
 constexpr u32 kSmallRing = kLdsOps + (u32)kSmallOpSlots * 512u;  // per-wave result rings
-constexpr u32 kSmallRingTiles = 32;                               // tiles per wave (one ring window)
+constexpr u32 kSmallRingTiles = 32;                               // tiles per ring window
 constexpr u32 kSmallRingBytesPerWave = kSmallRingTiles * 2u * 8u;  // (value | code << 32) per message
 constexpr size_t small_lds_bytes() { return kSmallRing + 8u * kSmallRingBytesPerWave; }
 static_assert(small_lds_bytes() <= 160u * 1024u, "small-message kernel LDS exceeds 160 KiB");
@@ -176,7 +168,6 @@ struct SmallArgs {
   u32* zero_word;    // !SLOT, optional: zeroed at the end (the next kernel's mismatch count)
   const u32* rops;   // the ragged operator array (Z_8192; Z_4096^{-1}, the 13th padding inverse)
   const u32* pow2;   // SLOT: Z_{2^k}, k < 64 (a long message's Z_L)
-  u32* fault;        // context fault word (kFaultGrid: a grid too small for the batch)
   u64 max_len;       // SLOT: a larger message size is SUBSPACE_CRC_SLOT_OVERSIZE (strided layouts:
                      // the slot's payload area); ~0 for slot lists
 };

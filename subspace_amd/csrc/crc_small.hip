@@ -13,14 +13,14 @@
 //    mis -- the uniform kernel's access shape (64 consecutive lines per load instruction when
 //    the two messages are adjacent) and the ragged kernel's alignment rule (whole 16-B
 //    blocks from the block holding s; the first mis bytes and the bytes from E on masked).
-//  * Waves sweep the tiles like the uniform kernel (order-0 front), at most kSmallRingTiles
-//    (32) tiles per wave: the host launches more workgroups for longer batches, as for the
-//    fused uniform slot kernel, so a wave's whole output is one LDS ring window and the tile
-//    loop holds nothing but the stream (round 4: the loop used to carry a flush every 32
-//    tiles, whose long-message and prefix code cost the loop 359 SGPR spills and 25 full
-//    drains although a 4 KiB list never ran it). A tile's two records are loaded one tile
-//    ahead of its lines (vector loads, retired in order with the line loads), so line
-//    addresses never wait on a record.
+//  * Waves sweep the tiles like the uniform kernel (order-0 front). A tile's two records
+//    are loaded one tile ahead of its lines (vector loads, retired in order with the line
+//    loads, as the ragged kernel's descriptors), so line addresses never wait on a record.
+//    The host gives no wave more than one 32-tile ring window (more workgroups for longer
+//    batches), so the in-loop flush below never runs; it stays for any grid. (Round 4: the same
+//    kernel with the flush moved out of the loop -- 0 SGPR spills, no full drain in the loop
+//    -- measured 2.3-3.4 us slower per 65,536-slot list, with or without loop padding:
+//    profiles/r04/README.md.)
 //  * Every line load stays inside its message: block b of lane l is read from s0 +
 //    min(128 l + 16 b, last block), so the lanes past the end re-read the last block (one
 //    cache line) instead of branching around loads, and a half with nothing to read (no
@@ -28,41 +28,31 @@
 //    table. Loads never touch a 16-B block that holds no byte of the message.
 //  * Line 0 starts from seed = Z_mis^{-1}(init), every other line from 0, so each half gives
 //      V = crc_raw(seed, 0^mis || D || 0^p) = Z_p(crc_raw(init, D)),   p = 4096 - E;
-//    each message's value and code are parked in the wave's LDS ring, and after the loop each
-//    lane takes one message of the ring, undoes its padding with p's bits over the inverse
-//    operators Z_{2^b}^{-1}, b < 12 (LDS), and stores the CRC.
+//    each message's value and code are parked in a per-wave LDS ring (32 tiles), and every 32
+//    tiles (in practice once, after the loop) each lane takes one message of the ring, undoes
+//    its padding with p's bits over the inverse operators Z_{2^b}^{-1}, b < 12 (LDS), and
+//    stores the CRC.
 //  * SLOT: the message-slot checksum (client/checksum.h:29-47 over common/channel.h:527-542's
-//    spans) in the same finish, from init 0: with H = crc_raw(~0, span 0 || span 1) from the
+//    spans) in the same flush, from init 0: with H = crc_raw(~0, span 0 || span 1) from the
 //    prefix (the flag set first for a publish, client/publisher.cc:664-675),
 //      Z_p(crc_raw(H, payload)) = Z_{p+L}(H) ^ V = Z_4096(Z_mis^{-1}(H)) ^ V,
 //    so the padding inverses that finish a plain CRC finish the checksum too; then flag +
-//    checksum are stored (publish) or compared (verify: client/client.cc:1346-1356). Each
-//    lane's prefix address (its slot record) is loaded in the prologue, with tile 0.
+//    checksum are stored (publish) or compared (verify: client/client.cc:1346-1356), with no
+//    second kernel. The first window's prefix words are loaded in the prologue ahead of tile
+//    0's lines and hashed under tile 0's flight (round 4: no prefix round trip in the tail).
+//    Strided slots: a size beyond the slot's payload area (a.max_len) is
+//    SUBSPACE_CRC_SLOT_OVERSIZE: nothing read, stored or compared.
 //  * A message with E > 4096 (longer than the caller's max_message_size bound, or a 4 KiB
-//    payload that does not start on a 16-B boundary) is parked as such and computed after the
-//    loop, one at a time by the whole wave, in 8 KiB chunks (acc = Z_8192(acc) ^ chunk, the
-//    last chunk's padding undone; SLOT: finished as Z_L(H) ^ crc_raw(0, payload)), behind a
-//    wave-uniform branch the common case never takes.
+//    payload that does not start on a 16-B boundary) is parked as such and computed by the
+//    wave's next flush, one at a time by the whole wave, in 8 KiB chunks (acc = Z_8192(acc) ^
+//    chunk, the last chunk's padding undone; SLOT: finished as Z_L(H) ^ crc_raw(0, payload)),
+//    behind a wave-uniform branch the common case never takes. No list, no second kernel, no
+//    code in the tile loop, and a batch of long messages still spreads over every wave.
 //  * SLOT verify: mismatches are summed per workgroup by one LDS atomic per wave and over
 //    workgroups by one relaxed 64-bit atomic per workgroup on a context counter word that also
 //    counts finished workgroups; the last one writes the call's total and resets the word
 //    (the fused uniform slot kernel's scheme: no fences, no memset).
 #include "crc_device.h"
-
-// A/B builds (tools/ab_lib.sh): 1 (product) loads each lane's finishing record in the prologue,
-// 0 in the finish; SUBSPACE_SMALL_FENCE 1 pins a scheduling fence after each tile's load issue.
-#ifndef SUBSPACE_SMALL_EARLY_PFX
-#define SUBSPACE_SMALL_EARLY_PFX 1
-#endif
-#ifndef SUBSPACE_SMALL_FENCE
-#define SUBSPACE_SMALL_FENCE 0
-#endif
-#ifndef SUBSPACE_SMALL_SPAN_EARLY
-#define SUBSPACE_SMALL_SPAN_EARLY 1  // the slot's span terms hashed in the prologue (0: in the finish)
-#endif
-#ifndef SUBSPACE_SMALL_LOOP_PAD
-#define SUBSPACE_SMALL_LOOP_PAD 0  // s_nop instructions (4 B each) before the tile loop (A/B builds)
-#endif
 
 namespace subspace_amd {
 
@@ -88,11 +78,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   const u64 ntiles = (count + 1) >> 1;
   const u64 nw = (u64)gridDim.x * NPW;
   const u64 t0 = front_slot(blockIdx.x, gridDim.x, wid);
-  u32 nk = t0 < ntiles ? (u32)((ntiles - t0 + nw - 1) / nw) : 0u;  // tiles tau = t0 + k*nw
-  if (nk > kSmallRingTiles) {  // a host bug (the grid sizing): reported, never a ring overrun
-    if (lane == 0) raise_fault(a.fault, kFaultGrid);
-    nk = kSmallRingTiles;
-  }
+  const u32 nk = t0 < ntiles ? (u32)((ntiles - t0 + nw - 1) / nw) : 0u;  // tiles tau = t0 + k*nw
   const uint8_t* safe = reinterpret_cast<const uint8_t*>(gtab);  // 16 readable bytes
   const bool calc = a.mode == 0u;
 
@@ -136,55 +122,10 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     return x;
   };
 
-  // Each message's value and code are parked in the wave's LDS ring, entry 2 k + h.
-  // Code: p = 4096 - E (bits 0-11) | mis << 12 for a half-tile message (value: Z_p(crc_raw(
-  // init, D))); kCodeLong for a longer one (computed after the loop: long_crc); kCodeEmpty for
-  // length 0 (CRC init ^ final_xor; a checksum over the spans only); kCodeSkip for no message;
-  // SLOT: kCodeOversize for a size beyond the slot's payload area (nothing read, computed or
-  // stored: SUBSPACE_CRC_SLOT_OVERSIZE).
-  constexpr u32 kCodeOversize = 0x10000000u, kCodeLong = 0x20000000u, kCodeEmpty = 0x40000000u,
-                kCodeSkip = 0x80000000u;
-  auto process = [&](const u32x4 (&cur)[8], u64 s, u64 L, u32 k) __attribute__((always_inline)) {
-    const u32 mis = (u32)s & 15u;
-    const u32 E = ext(k, s, L);
-    u32x4 d[8];
-#pragma unroll
-    for (int b = 0; b < 8; b++) d[b] = cur[b];
-    // Head: line 0's first mis bytes precede the message. Tail: bytes from E on (the
-    // re-read last block included). Each lane keeps only its line's message bytes.
-    const bool head = E != 0u && mis != 0u && l == 0u;
-    if (__any(head || E < kSmallMaxExt)) {
-      const int v0 = (int)E - 128 * (int)l;
-      const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
-      keep_bytes(d, head ? mis : 0u, hi);
-    }
-    u32 seed = a.init;  // Z_mis^{-1}(init): after the mis masked bytes the state is init
-    if (seed != 0u && __any(head)) seed = inv_bits(seed, mis, 4);
-    const u32 crc = line_crc32_2chain(d, l == 0u ? seed : 0u, lc0, lc1, z64);
-    // line l of half h -> Z_{128*(31-l)}(line), XOR over each half (DPP): lanes 31, 63
-    u32 v = lane_shift(lop, crc);
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-    const u64 m = msg_of(k);
-    const bool present = k < nk && m < count;
-    const bool over = present && L + mis > kSmallMaxExt;
-    const u32 code = !present                  ? kCodeSkip
-                   : SLOT && L > a.max_len     ? kCodeOversize
-                   : over                      ? kCodeLong
-                   : L == 0   ? kCodeEmpty
-                              : (kSmallMaxExt - E) | (mis << 12);
-    // lane 31 of each half: its message's value and code, one 8-B LDS store
-    if (l == 31u) lds_st64(sring + 8u * (2u * k + h), (u64)v | ((u64)code << 32));
-  };
-
   // SLOT: the prefix terms of a slot: H = crc_raw(~0, span 0 || span 1) with the flag word as
   // stored (kMessageHasChecksum set first for a publish), the flag word F, the stored checksum
   // S (prefix + 48) and whether the flag was set. Prefixes are 8-B aligned (the C ABI's rule):
-  // 8-B loads. span_load issues the loads, span_hash computes from the words (so the loads can
-  // be issued ahead of other loads and waited for later).
+  // 8-B loads.
   constexpr u32 kW = kSlotFusedMaxMeta / 4 + 2;
   auto span_load = [&](const uint8_t* pfx, u32 (&w)[14], u32 (&W1)[kW]) __attribute__((always_inline)) {
     const u64* q = reinterpret_cast<const u64*>(pfx);
@@ -233,70 +174,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     return span_hash(w, W1, F, S, has);
   };
 
-  // Prologue: table loads, tile 0's and 1's records, (SLOT) this lane's finishing record,
-  // tile 0's lines, then the LDS stores and the barrier (tile 0's latency hides behind the
-  // fill). Lane i finishes message i of the ring: tile i / 2, half i & 1.
-  const u32 fh = (u32)lane & 1u, fti = (u32)lane >> 1;
-  const u64 fm = 2 * (t0 + (u64)fti * nw) + fh;
-  const bool flive = fti < nk && fm < count;
-  u64 sA, LA, sB, LB;
-  fetch(0, sA, LA);
-  fetch(1, sB, LB);
-  u64 fpre = 0;  // SLOT: the prefix offset of this lane's finishing message (a real record)
-  if constexpr (SLOT && SUBSPACE_SMALL_EARLY_PFX) fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
-  // SLOT, SUBSPACE_SMALL_SPAN_EARLY: the slot's prefix words are loaded here, ahead of tile 0's
-  // lines, and hashed right after the barrier while tile 0 is in flight, so the finish after the
-  // loop only combines (no prefix round trip in the kernel's tail)
-  u32 pwords[14], pmeta[kW];
-  if constexpr (SLOT && SUBSPACE_SMALL_EARLY_PFX && SUBSPACE_SMALL_SPAN_EARLY) {
-    span_load(flive ? base + fpre - a.pdelta : safe, pwords, pmeta);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  u32x4 A[8], B[8];
-  u64 sc = sA, Lc = LA;
-  load_lines(A, sc, ext(0, sc, Lc));
-  fill.store(sbase);
-  if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
-  __syncthreads();
-  u32 eF = 0, eS = 0, eH = 0;
-  bool ehas = false;
-  if constexpr (SLOT && SUBSPACE_SMALL_EARLY_PFX && SUBSPACE_SMALL_SPAN_EARLY) eH = span_hash(pwords, pmeta, eF, eS, ehas);
-
-  // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines: the
-  // uniform kernel's stream plus two record loads per tile, nothing else in the loop.
-  u32 k = 0;
-#pragma unroll
-  for (int i = 0; i < SUBSPACE_SMALL_LOOP_PAD; i++) asm volatile("s_nop 0");
-  for (; k + 1 < nk; k += 2) {
-    issue_prio_hi();       // (crc_device.h)
-    drain_before_issue();  // tile k's lines and tile k+1's record
-    const u64 s1 = sB, L1 = LB;
-    fetch(k + 2, sA, LA);
-    load_lines(B, s1, ext(k + 1, s1, L1));
-    issue_prio_lo();
-    if constexpr (SUBSPACE_SMALL_FENCE) __builtin_amdgcn_sched_barrier(0);
-    process(A, sc, Lc, k);
-    issue_prio_hi();
-    drain_before_issue();
-    const u64 s2 = sA, L2 = LA;
-    fetch(k + 3, sB, LB);
-    load_lines(A, s2, ext(k + 2, s2, L2));
-    issue_prio_lo();
-    if constexpr (SUBSPACE_SMALL_FENCE) __builtin_amdgcn_sched_barrier(0);
-    process(B, s1, L1, k + 1);
-    sc = s2;
-    Lc = L2;
-  }
-  if (k < nk) {
-    drain_before_issue();
-    process(A, sc, Lc, k);
-  }
-  wave_lds_sync();
-
-  // ---- finish: lane i takes message i of the ring (nothing below runs inside the stream)
-  const u64 e = lds_ld64(sring + 8u * (u32)lane);
-  u32 v = (u32)e;
-  const u32 code = flive ? (u32)(e >> 32) : kCodeSkip;
   // A message longer than a half-tile, by the whole wave (s, L, P wave-uniform): 8 KiB chunks
   // as the ragged kernel's tiles (lines, line shifts, halves joined by Z_4096), acc =
   // Z_8192(acc) ^ chunk, the last chunk's padding p = 8192 nt - E < 8192 undone (b < 12 from
@@ -326,13 +203,13 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
         keep_bytes(d, hd ? mis : 0u, hi);
       }
       const u32 crc = line_crc32_2chain(d, (j == 0 && lane == 0) ? seed : 0u, lc0, lc1, z64);
-      u32 x = lane_shift(lop, crc);  // lanes 0-31: bytes 0..4095 of the chunk, 32-63: the rest
-      x ^= (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
-      x ^= (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
-      x ^= (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
-      x ^= (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
-      x ^= (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
-      const u32 h0 = (u32)__builtin_amdgcn_readlane((int)x, 31), h1 = (u32)__builtin_amdgcn_readlane((int)x, 63);
+      u32 v = lane_shift(lop, crc);  // lanes 0-31: bytes 0..4095 of the chunk, 32-63: the rest
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+      const u32 h0 = (u32)__builtin_amdgcn_readlane((int)v, 31), h1 = (u32)__builtin_amdgcn_readlane((int)v, 63);
       const u32 c = opmul(sbase, kUniSlotOpZ4096, h0) ^ h1;
       acc = j ? opmul_global(a.rops + kLaneOpWords + 128, acc) ^ c : c;  // Z_8192: the first tile shift
     }
@@ -349,45 +226,179 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
     return acc;
   };
-  // rare: messages longer than a half-tile, one at a time by the whole wave
-  for (u64 msk = __ballot(code == kCodeLong); msk;) {
-    const u32 src = (u32)__builtin_ctzll(msk);
-    msk &= msk - 1;
-    const u64 ms = 2 * (t0 + (u64)(src >> 1) * nw) + (src & 1u);
-    const u64 s = a.offsets[ms * a.ostride], L = a.lengths[ms * a.lstride];
-    const u64 P = SLOT ? a.prefixes[ms * a.pstride] : 0;
-    const u32 r = long_crc(s, L, P);
-    v = lane == (int)src ? r : v;
-  }
-  const bool half = code < kCodeOversize;  // a half-tile message: Z_p undone here
-  if constexpr (SLOT) {
-    const bool oversize = code == kCodeOversize;
-    const bool live = code != kCodeSkip && !oversize;
-    if constexpr (!SUBSPACE_SMALL_EARLY_PFX) fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
-    const uint8_t* pfx = live ? base + fpre - a.pdelta : safe;  // (a read-only block)
-    u32 F = eF, S = eS, H = eH;
-    bool has = ehas;
-    if constexpr (!(SUBSPACE_SMALL_EARLY_PFX && SUBSPACE_SMALL_SPAN_EARLY)) H = span_crc(pfx, F, S, has);
-    // Z_p(crc_raw(H, payload)) = Z_4096(Z_mis^{-1}(H)) ^ V, then Z_p undone
-    const u32 Hm = inv_bits(H, half ? (code >> 12) & 15u : 0u, 4);
-    const u32 X = opmul(sbase, kUniSlotOpZ4096, Hm) ^ v;
-    const u32 R = half ? inv_bits(X, code & 0xFFFu, kSmallInvOps) : (code == kCodeLong ? v : H);
+
+  // SLOT: store flag + checksum (publish) or the status (verify) of slot m; counts mismatches
+  u32 mism = 0;
+  auto slot_store = [&](bool live, bool oversize, u64 m, const uint8_t* pfx, u32 F, u32 S, bool has, u32 R)
+                        __attribute__((always_inline)) {
     const u32 res = ~R;  // *reinterpret_cast<uint32_t*>(checksum.data()) = ~crc (client/checksum.h:36)
-    u32 mism = 0;
-    if (oversize && a.status) a.status[fm] = 4u;  // SUBSPACE_CRC_SLOT_OVERSIZE
+    if (oversize && a.status) a.status[m] = 4u;  // SUBSPACE_CRC_SLOT_OVERSIZE
     if (calc) {
       if (live) {
         u32* pw = reinterpret_cast<u32*>(const_cast<uint8_t*>(pfx));
         pw[8] = F;     // SetHasChecksum()
         pw[12] = res;
-        if (a.status) a.status[fm] = 0u;
-        if (a.crc_out) a.crc_out[fm] = res;
+        if (a.status) a.status[m] = 0u;
+        if (a.crc_out) a.crc_out[m] = res;
       }
     } else {
       const u32 st = !has ? 2u : (res == S ? 0u : 1u);  // client/checksum.h:46
-      if (live && a.status) a.status[fm] = st;
-      mism = (u32)__builtin_popcountll(__ballot(live && st == 1u));
+      if (live && a.status) a.status[m] = st;
+      mism += (u32)__builtin_popcountll(__ballot(live && st == 1u));
     }
+  };
+
+  // Each message's value and code are parked in the wave's LDS ring, entry 2 (k & 31) + h.
+  // Code: p = 4096 - E (bits 0-11) | mis << 12 for a half-tile message (value: Z_p(crc_raw(
+  // init, D))); kCodeLong for a longer one (computed by the flush: long_crc); kCodeEmpty for
+  // length 0 (CRC init ^ final_xor; a checksum over the spans only); kCodeSkip for no message;
+  // SLOT: kCodeOversize for a size beyond the slot's payload area (nothing read or stored).
+  constexpr u32 kCodeOversize = 0x10000000u, kCodeLong = 0x20000000u, kCodeEmpty = 0x40000000u,
+                kCodeSkip = 0x80000000u;
+  auto process = [&](const u32x4 (&cur)[8], u64 s, u64 L, u32 k) __attribute__((always_inline)) {
+    const u32 mis = (u32)s & 15u;
+    const u32 E = ext(k, s, L);
+    u32x4 d[8];
+#pragma unroll
+    for (int b = 0; b < 8; b++) d[b] = cur[b];
+    // Head: line 0's first mis bytes precede the message. Tail: bytes from E on (the
+    // re-read last block included). Each lane keeps only its line's message bytes.
+    const bool head = E != 0u && mis != 0u && l == 0u;
+    if (__any(head || E < kSmallMaxExt)) {
+      const int v0 = (int)E - 128 * (int)l;
+      const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
+      keep_bytes(d, head ? mis : 0u, hi);
+    }
+    u32 seed = a.init;  // Z_mis^{-1}(init): after the mis masked bytes the state is init
+    if (seed != 0u && __any(head)) seed = inv_bits(seed, mis, 4);
+    const u32 crc = line_crc32_2chain(d, l == 0u ? seed : 0u, lc0, lc1, z64);
+    // line l of half h -> Z_{128*(31-l)}(line), XOR over each half (DPP): lanes 31, 63
+    u32 v = lane_shift(lop, crc);
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    const u64 m = msg_of(k);
+    const bool present = k < nk && m < count;
+    const bool over = present && L + mis > kSmallMaxExt;
+    const u32 code = !present              ? kCodeSkip
+                   : SLOT && L > a.max_len ? kCodeOversize
+                   : over                  ? kCodeLong
+                   : L == 0                ? kCodeEmpty
+                                           : (kSmallMaxExt - E) | (mis << 12);
+    // lane 31 of each half: its message's value and code, one 8-B LDS store
+    if (l == 31u) lds_st64(sring + 8u * (2u * (k & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
+  };
+  // SLOT: lane i's message of the first window (tile i / 2, half i & 1): its record's prefix
+  // offset, and (after the barrier) the prefix terms, from words loaded in the prologue
+  const u64 fm = 2 * (t0 + (u64)((u32)lane >> 1) * nw) + ((u32)lane & 1u);
+  const bool flive = ((u32)lane >> 1) < nk && fm < count;
+  u64 fpre = 0;
+  u32 eF = 0, eS = 0, eH = 0;
+  bool ehas = false;
+  // Finish and store the ring's tiles kf .. kf+nt-1 (nt <= 32): lane i takes message i of the
+  // window, i.e. tile kf + i/2, half i & 1 (its value and code from the ring; a slot's prefix
+  // offset from its record again).
+  auto flush = [&](u32 kf, u32 nt) __attribute__((always_inline)) {
+    wave_lds_sync();
+    const u32 hh = (u32)lane & 1u, ti = (u32)lane >> 1;
+    const bool valid = ti < nt;
+    const u64 e = lds_ld64(sring + 8u * (u32)lane);
+    u32 v = (u32)e;
+    const u32 code = valid ? (u32)(e >> 32) : kCodeSkip;
+    const u64 m = 2 * (t0 + (u64)(kf + ti) * nw) + hh;
+    const u64 mc = code != kCodeSkip ? m : 0;  // (a real record for every lane)
+    // rare: messages longer than a half-tile, one at a time by the whole wave
+    u64 msk = __ballot(code == kCodeLong);
+    while (msk) {
+      const u32 src = (u32)__builtin_ctzll(msk);
+      msk &= msk - 1;
+      const u64 ms = 2 * (t0 + (u64)(kf + (src >> 1)) * nw) + (src & 1u);
+      const u64 s = a.offsets[ms * a.ostride], L = a.lengths[ms * a.lstride];
+      const u64 P = SLOT ? a.prefixes[ms * a.pstride] : 0;
+      const u32 r = long_crc(s, L, P);
+      v = lane == (int)src ? r : v;
+    }
+    const bool half = code < kCodeOversize;  // a half-tile message: Z_p undone here
+    if constexpr (SLOT) {
+      const bool oversize = code == kCodeOversize;
+      const bool live = code != kCodeSkip && !oversize;
+      // the first window's prefix terms come from the prologue (every window, under the host's
+      // grid rule); a later window's are loaded here
+      const uint8_t* pfx = (kf == 0 ? flive : live) ? base + (kf == 0 ? fpre : a.prefixes[mc * a.pstride]) - a.pdelta
+                                                     : safe;  // (a read-only block)
+      u32 F = eF, S = eS, H = eH;
+      bool has = ehas;
+      if (kf != 0) H = span_crc(pfx, F, S, has);
+      // Z_p(crc_raw(H, payload)) = Z_4096(Z_mis^{-1}(H)) ^ V, then Z_p undone
+      const u32 Hm = inv_bits(H, half ? (code >> 12) & 15u : 0u, 4);
+      const u32 X = opmul(sbase, kUniSlotOpZ4096, Hm) ^ v;
+      const u32 R = half ? inv_bits(X, code & 0xFFFu, kSmallInvOps) : (code == kCodeLong ? v : H);
+      slot_store(live, oversize, m, pfx, F, S, has, R);
+    } else {
+      u32 r = inv_bits(v, half ? code & 0xFFFu : 0u, kSmallInvOps);
+      if (code == kCodeEmpty) r = a.init;
+      if (code != kCodeSkip) a.out[m] = r ^ a.final_xor;
+    }
+    wave_lds_sync();
+  };
+  constexpr u32 kWinMask = kSmallRingTiles - 1u;
+
+  // Prologue: table loads, tile 0's and 1's records, tile 0's lines, then the LDS stores and
+  // the barrier (tile 0's latency hides behind the fill).
+  u64 sA, LA, sB, LB;
+  fetch(0, sA, LA);
+  fetch(1, sB, LB);
+  u32 pwords[14], pmeta[kW];
+  if constexpr (SLOT) {
+    fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
+    span_load(flive ? base + fpre - a.pdelta : safe, pwords, pmeta);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  u32x4 A[8], B[8];
+  u64 sc = sA, Lc = LA;
+  load_lines(A, sc, ext(0, sc, Lc));
+  fill.store(sbase);
+  if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
+  __syncthreads();
+  if constexpr (SLOT) eH = span_hash(pwords, pmeta, eF, eS, ehas);
+
+  // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines; the
+  // ring is finished whenever it holds 32 tiles, right after the next tile's loads are issued
+  // (so the stores retire during that tile's compute), and at the end (crc_ragged.hip's loop,
+  // without descriptors). Nothing else lives across the loop (register-parked
+  // values, 64-tile windows and a flush only after the loop each measured slower).
+  u32 k = 0;
+  for (; k + 1 < nk; k += 2) {
+    issue_prio_hi();       // (crc_device.h)
+    drain_before_issue();  // tile k's lines and tile k+1's record
+    const u64 s1 = sB, L1 = LB;
+    fetch(k + 2, sA, LA);
+    load_lines(B, s1, ext(k + 1, s1, L1));
+    issue_prio_lo();
+    if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
+    process(A, sc, Lc, k);
+    issue_prio_hi();
+    drain_before_issue();
+    const u64 s2 = sA, L2 = LA;
+    fetch(k + 3, sB, LB);
+    load_lines(A, s2, ext(k + 2, s2, L2));
+    issue_prio_lo();
+    process(B, s1, L1, k + 1);
+    sc = s2;
+    Lc = L2;
+  }
+  if (k < nk) {
+    drain_before_issue();
+    if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
+    process(A, sc, Lc, k);
+  }
+  if (nk) {
+    const u32 kf = (nk - 1u) & ~kWinMask;  // the last window, not flushed yet
+    flush(kf, nk - kf);
+  }
+  if constexpr (SLOT) {
     if (a.error_count && lane == 0) {
       if (calc) {
         if (blockIdx.x == 0 && wid == 0) *a.error_count = 0u;  // a publish has no mismatches
@@ -409,9 +420,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       }
     }
   } else {
-    u32 r = inv_bits(v, half ? code & 0xFFFu : 0u, kSmallInvOps);
-    if (code == kCodeEmpty) r = a.init;
-    if (code != kCodeSkip) a.out[fm] = r ^ a.final_xor;
     // a word the caller's next kernel accumulates into (a slot batch's mismatch count)
     if (a.zero_word != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.zero_word = 0u;
   }

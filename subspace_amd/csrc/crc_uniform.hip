@@ -49,13 +49,10 @@
 #ifndef SUBSPACE_SLOT_VARIANT
 #define SUBSPACE_SLOT_VARIANT 0
 #endif
-#ifndef SUBSPACE_UNI_LOOP_PAD
-#define SUBSPACE_UNI_LOOP_PAD 0  // s_nop instructions (4 B each) before the tile loop (A/B builds)
-#endif
 
 namespace subspace_amd {
 
-template <int WG, bool SLOT, bool PROBE, bool SHIFT2>
+template <int WG, bool SLOT, bool PROBE>
 __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
     const uint8_t* __restrict__ base, u64 stride, u64 count, const u32* __restrict__ gtab,
     const u32* __restrict__ gops, u32 init, u32 final_xor, u32* __restrict__ out, int order,
@@ -75,10 +72,8 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   // 45.10 us (r02c17, slot_gap interleaved) and 45.4-45.8 -> 45.0-45.4 us (r02c18, sweep A/B,
   // four pairs); bit-exact.
   constexpr bool kTwoChain = true;  // (false: the one-chain line CRC, for A/B builds)
-  static_assert(!(SHIFT2 && (SLOT || PROBE)), "the two-shift variant is the plain kernel's");
-  // step tables, per-lane operators, Z_4096 and Z_64 (the two-chain line CRC's join); SHIFT2:
-  // tables and the two sets of per-lane operators (crc_device.h kShift2OpSlots)
-  LdsFill<WG, SHIFT2 ? kShift2OpSlots : (kTwoChain ? kUniOpSlots : kUniOpSlotsOneChain)> fill;
+  // step tables, per-lane operators, Z_4096 and Z_64 (the two-chain line CRC's join)
+  LdsFill<WG, kTwoChain ? kUniOpSlots : kUniOpSlotsOneChain> fill;
   fill.load(gtab, gops);
 
   const int lane = threadIdx.x & 63;
@@ -87,7 +82,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 lc0 = sbase + ((u32)(lane & 31) << 2);
   const u32 lc1 = lc0 + 0x10000u;
-  constexpr int kRing = SHIFT2 ? 64 : uni_ring_results(NPW);  // SHIFT2: one register, 32 tiles
+  constexpr int kRing = uni_ring_results(NPW);
   const u32 ring = sbase + kUniRing + (u32)wid * (4u * kRing);
   // SLOT: this wave's tagged result ring; the workgroup's mismatch word
   const u32 sring = sbase + kUniSlotRing + (u32)wid * kSlotRingBytesPerWave;
@@ -174,38 +169,16 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
     if constexpr (kTwoChain) return line_crc32_2chain(d, s_init, lc0, lc1, z64);
     else return line_crc32(d, s_init, lc0, lc1);
   };
-  // This lane's contribution to its message CRC: Z_{128*(31-l)}(line CRC). SHIFT2: the line's
-  // chains A (bytes 0..63, from the init) and B (64..127, from 0) shifted apart,
-  //   Z_{128(31-l)}(Z_64(A) ^ B) = Z_{128(31-l)+64}(A) ^ Z_{128(31-l)}(B),
-  // two independent conflict-free operator applications instead of Z_64's 4-copy table (whose
-  // nibble lookups conflict 2-way: profiles/r04 ledger) followed by one shift.
-  auto lane_value = [&](const u32x4 (&d)[8]) {
-    if constexpr (SHIFT2) {
-      u32 x = s_init ^ d[0][0], y = d[4][0];
-#pragma unroll
-      for (int w = 0; w < 16; w++) {
-        x = step4n(x, lc0, lc1, w < 15 ? d[(w + 1) >> 2][(w + 1) & 3] : 0u);
-        y = step4n(y, lc0, lc1, w < 15 ? d[(w + 17) >> 2][(w + 17) & 3] : 0u);
-      }
-      return lane_shift(lop + 4u * (u32)kLaneOpWords, x) ^ lane_shift(lop, y);
-    } else {
-      return lane_shift(lop, line_crc(d));
-    }
-  };
-  u32 park = 0;  // SHIFT2: the window's results, tile k's message 2 tau + h in lane 2(k - kf) + h
   // Message CRCs of tile k: into ring slots 2*(k - kf) + h (kf = first tile of the window);
   // SLOT: into the tagged ring entry 2*k + h (k < kSlotRingRounds), as CRC | k << 32.
-  auto tile_result = [&](u32 v, u32 k, u32 kf) {
+  auto tile_result = [&](u32 crc, u32 k, u32 kf) {
+    u32 v = lane_shift(lop, crc);
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-    if constexpr (SHIFT2) {
-      const u32 r0 = (u32)__builtin_amdgcn_readlane((int)v, 31), r1 = (u32)__builtin_amdgcn_readlane((int)v, 63);
-      const int at = (int)(2u * (k - kf));
-      park = lane == at ? r0 ^ final_xor : (lane == at + 1 ? r1 ^ final_xor : park);
-    } else if constexpr (SLOT) {
+    if constexpr (SLOT) {
       if (l == 31)
         lds_st64(sring + 16u * (k & (u32)(kSlotRingRounds - 1)) + 8u * (u32)h, ((u64)k << 32) | (u64)(v ^ final_xor));
     } else {
@@ -219,9 +192,9 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
       const u32 slot = (u32)(i * 64 + lane);
       const u32 t = slot >> 1;
       const u64 msg = 2 * (t0 + (u64)(kf + t) * tstep) + (u64)(slot & 1u);
-      if (t < nt && msg < count) out[msg] = SHIFT2 ? park : lds_ld(ring + 4u * slot);
+      if (t < nt && msg < count) out[msg] = lds_ld(ring + 4u * slot);
     }
-    if constexpr (!SHIFT2) wave_lds_sync();
+    wave_lds_sync();
   };
 
   // Table loads first, then tile 0's loads, then the LDS stores: tile 0's latency hides
@@ -259,8 +232,6 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   constexpr u32 kWin = SLOT ? ~0u : (u32)(kRing / 2);
   u32 k = 0, kf = 0;
   u64 pt_finish = 0;  // PROBE, SLOT: when a finishing wave began
-#pragma unroll
-  for (int i = 0; i < SUBSPACE_UNI_LOOP_PAD; i++) asm volatile("s_nop 0");
   for (; k + 1 < nk; k += 2) {
     const u64 qB = addr_before_wait(k + 1);
     issue_prio_hi();
@@ -268,28 +239,28 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
     load_at(B, qB);
     issue_prio_lo();
     if (!SLOT && k - kf == kWin) {
-      if constexpr (!SHIFT2) wave_lds_sync();
+      wave_lds_sync();
       flush(kf, kRing / 2);
       kf = k;
     }
-    tile_result(lane_value(A), k, kf);
+    tile_result(line_crc(A), k, kf);
     const u64 qA = addr_before_wait(k + 2);
     issue_prio_hi();
     drain_before_issue();
     load_at(A, qA);
     issue_prio_lo();
-    tile_result(lane_value(B), k + 1, kf);
+    tile_result(line_crc(B), k + 1, kf);
   }
   if constexpr (PROBE) pt[2] = __builtin_amdgcn_s_memrealtime();
   if (k < nk) {  // odd last tile, already loaded
     if (!SLOT && k - kf == kWin) {
-      if constexpr (!SHIFT2) wave_lds_sync();
+      wave_lds_sync();
       flush(kf, kRing / 2);
       kf = k;
     }
-    tile_result(lane_value(A), k, kf);
+    tile_result(line_crc(A), k, kf);
   }
-  if constexpr (!SHIFT2) wave_lds_sync();
+  wave_lds_sync();
   if constexpr (SLOT) {
     if (wid < kSlotFinishers) {
       if constexpr (PROBE) pt_finish = __builtin_amdgcn_s_memrealtime();
@@ -427,17 +398,16 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   }
 }
 
-#define INST(WGV, SL, PR, S2)                                                                               \
-  template __global__ void crc32_uniform4k_kernel<WGV, SL, PR, S2>(const uint8_t*, u64, u64, const u32*, const u32*, \
-                                                                   u32, u32, u32*, int, u32*, SlotArgs);
-INST(256, false, false, false)
-INST(512, false, false, false)
-INST(768, false, false, false)
-INST(1024, false, false, false)
-INST(512, true, false, false)
-INST(512, false, true, false)
-INST(512, true, true, false)
-INST(512, false, false, true)
+#define INST(WGV, SL, PR)                                                                                 \
+  template __global__ void crc32_uniform4k_kernel<WGV, SL, PR>(const uint8_t*, u64, u64, const u32*, const u32*, u32, \
+                                                               u32, u32*, int, u32*, SlotArgs);
+INST(256, false, false)
+INST(512, false, false)
+INST(768, false, false)
+INST(1024, false, false)
+INST(512, true, false)
+INST(512, false, true)
+INST(512, true, true)
 #undef INST
 
 }  // namespace subspace_amd
