@@ -22,17 +22,17 @@ __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, con
 
 struct TileDesc;
 __global__ void crc32_ragged_count_scan_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
-                                               u64*, u32*, u32*, u64, FaultRef);
+                                               u64*, u32*, u32*, FaultRef);
 __global__ void tile_segment_scan_kernel(const u32*, u32, u32, u32, const u64*, u64, u32*, u32*);
 __global__ void segment_prefix_kernel(u32*, u64, u32, u32, const u64*, u64, u64*, u32*, FaultRef);
-__global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, u64, u64, const u32*,
-                                         TileDesc*, u32*, u64*, u64, u32*, FaultRef);
+__global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const u64*, u64, u64, TileDesc*, u32*,
+                                         u64*, u64, u32*, FaultRef);
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
-                                    const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds, u32*, u32*, u64,
+                                    const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds, u32*, u32*, u32,
                                     FaultRef);
 __global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, const u64*, u32, u64, const u32*, const u32*,
-                                          u32, u32, const u32*, const u32*, u32, u32*, u64*, u64, u32*, FaultRef);
+                                          u32, u32, u32*, const u32*, u32, u32*, u64*, u64, u32*, FaultRef);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, u64, int, int, u32,
                                          const u32*, const u32*, const u32*, u32*, u32*, u32*);
 __global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*);
@@ -85,7 +85,7 @@ uintptr_t host_alias(uintptr_t p, uint64_t n) {
     if (p >= r.host && p - r.host <= r.bytes && n <= r.bytes - (p - r.host)) return r.dev + (p - r.host);
   return 0;
 }
-constexpr size_t kTileDescBytes = 16;
+constexpr size_t kTileDescBytes = 16;  // the wide form; 8 B (TileDesc8) for most batches
 constexpr u64 kScanTile = 4096;   // segments per workgroup of the segment scan (crc_combine.hip)
 constexpr u64 kCountTile = 4096;  // messages per workgroup of the tile-count scan
 constexpr u64 ceil_div(u64 a, u64 b) { return (a + b - 1) / b; }
@@ -120,7 +120,6 @@ struct subspace_crc_ctx {
   u32* d_tilecrc = nullptr;  // per-tile values, wave-major (desc_capacity + one tile per wave)
   u32* d_local = nullptr;    // per-segment inclusive XOR prefixes of the values, tile order
   u32* d_segx = nullptr;     // per-segment XORs, then their exclusive XOR prefixes
-  u32* d_chunk = nullptr;    // message of every kDescTilesPerWave-th tile (tile-count scan)
   u64 desc_capacity = 0;
   // look-back scan state: word 0 = the two workgroup tickets (u32 each), then the
   // tile-count scan's status words (scan_a_words), then the segment scan's (scan_b_words).
@@ -261,7 +260,7 @@ int fault_status(subspace_crc_ctx* c, hipStream_t st) {
 // Geometry of the wave-major tile values of the persistent ragged / long kernels: nw waves,
 // nkmax values per wave, segments of 64 tiles of one sweep row (crc_combine.hip).
 struct TileGeom {
-  u64 nw, nkmax, nwb, nseg;
+  u64 nw, nkmax, nwb, nseg, nblk;
 };
 TileGeom tile_geom(const subspace_crc_ctx* c, u64 tiles) {
   TileGeom g;
@@ -269,6 +268,7 @@ TileGeom tile_geom(const subspace_crc_ctx* c, u64 tiles) {
   g.nkmax = ceil_div(tiles ? tiles : 1, g.nw);
   g.nwb = ceil_div(g.nw, 64);
   g.nseg = g.nkmax * g.nwb;
+  g.nblk = ceil_div(g.nkmax, 64) * g.nwb;  // 64 x 64 blocks of the tile values and prefixes
   return g;
 }
 
@@ -287,17 +287,15 @@ int ensure_ragged_ws(subspace_crc_ctx* c, u64 messages, u64 tiles) {
     (void)hipFree(c->d_tilecrc);
     (void)hipFree(c->d_local);
     (void)hipFree(c->d_segx);
-    (void)hipFree(c->d_chunk);
     c->d_desc = nullptr;
-    c->d_tilecrc = c->d_local = c->d_segx = c->d_chunk = nullptr;
+    c->d_tilecrc = c->d_local = c->d_segx = nullptr;
     c->desc_capacity = 0;
     const TileGeom g = tile_geom(c, tiles);
     HIP_TRY(hipMalloc(&c->d_desc, tiles * kTileDescBytes));
-    // wave-major: nw * nkmax < tiles + nw entries
-    HIP_TRY(hipMalloc(&c->d_tilecrc, g.nw * g.nkmax * sizeof(u32)));
-    HIP_TRY(hipMalloc(&c->d_local, tiles * sizeof(u32)));
+    // blocked (crc_device.h tilecrc_index): whole 64 x 64 blocks of (w, k)
+    HIP_TRY(hipMalloc(&c->d_tilecrc, g.nblk * 4096 * sizeof(u32)));
+    HIP_TRY(hipMalloc(&c->d_local, g.nblk * 4096 * sizeof(u32)));
     HIP_TRY(hipMalloc(&c->d_segx, g.nseg * sizeof(u32)));
-    HIP_TRY(hipMalloc(&c->d_chunk, ceil_div(tiles, kDescTilesPerWave) * sizeof(u32)));
     c->desc_capacity = tiles;
     state = true;
   }
@@ -314,7 +312,11 @@ int ensure_ragged_ws(subspace_crc_ctx* c, u64 messages, u64 tiles) {
     HIP_TRY(hipDeviceSynchronize());
     c->scan_dirty = false;
   }
-  if (!c->d_overflow) HIP_TRY(hipMalloc(&c->d_overflow, 16));
+  if (!c->d_overflow) {  // [0] overflow (written by every call), [1] wide batch (zero between calls)
+    HIP_TRY(hipMalloc(&c->d_overflow, 16));
+    HIP_TRY(hipMemset(c->d_overflow, 0, 16));
+    HIP_TRY(hipDeviceSynchronize());  // the null stream does not order non-blocking streams
+  }
   return SUBSPACE_CRC_OK;
 }
 
@@ -385,12 +387,16 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   u32* tickets = reinterpret_cast<u32*>(c->d_scan_state);
   crc32_ragged_count_scan_kernel<<<(unsigned)ceil_div(n1, kCountTile), 256, 0, st>>>(
       offsets, ostride, lengths, lstride, count, init, final_xor, c->d_tbase, out, c->zero_word, c->d_scan_state + 1,
-      reinterpret_cast<u32*>(c->d_scan_state), c->d_chunk, ceil_div(cap, kDescTilesPerWave), fr);
+      reinterpret_cast<u32*>(c->d_scan_state), c->d_overflow + 1, fr);
   c->zero_word = nullptr;
   HIP_TRY(hipGetLastError());
-  // one wave per kDescTilesPerWave tiles, four waves per block
-  crc32_ragged_desc_kernel<<<(unsigned)ceil_div(cap, 4 * kDescTilesPerWave), 256, 0, st>>>(
-      offsets, ostride, lengths, lstride, c->d_tbase, count, cap, c->d_chunk, reinterpret_cast<TileDesc*>(c->d_desc),
+  // one thread per message; rows of workgroups share the later tiles of long messages when a
+  // batch has few messages for its tiles (config D: 256 x 8,192 tiles: 2,048 rows), up to ~8 Ki
+  // waves and no more rows than tiles per message
+  const u64 dx = ceil_div(count, 256), waves_x = ceil_div(count, 64);
+  const u64 dy = std::max<u64>(1, std::min<u64>({4096, ceil_div(8192, waves_x), cap / count}));
+  crc32_ragged_desc_kernel<<<dim3((unsigned)dx, (unsigned)dy), 256, 0, st>>>(
+      offsets, ostride, lengths, lstride, c->d_tbase, count, cap, reinterpret_cast<TileDesc*>(c->d_desc),
       c->d_overflow, c->d_scan_state + 1, ceil_div(n1, kCountTile), tickets, fr);
   HIP_TRY(hipGetLastError());
   const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU
@@ -399,7 +405,7 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   for (int r = 1; r < 16; r++) seeds.v[r] = apply(c->zinv1, seeds.v[r - 1]);
   crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, ragged_lds_bytes(), st>>>(
       base, offsets, ostride, lengths, lstride, c->d_tbase, count, reinterpret_cast<const TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_tab, c->d_rops, seeds, out, c->d_tilecrc, g.nkmax, fr);
+      c->d_overflow, c->d_tab, c->d_rops, seeds, out, c->d_tilecrc, (u32)g.nwb, fr);
   HIP_TRY(hipGetLastError());
   // padded message CRC = XOR of its tiles' values = difference of two entries of their
   // XOR prefix (only the batch's real tiles are combined); the final kernel undoes the last
@@ -681,7 +687,6 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_tilecrc);
   (void)hipFree(c->d_local);
   (void)hipFree(c->d_segx);
-  (void)hipFree(c->d_chunk);
   (void)hipFree(c->d_scan_state);
   (void)hipFree(c->d_overflow);
   (void)hipFree(c->d_uoff);
@@ -795,7 +800,7 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     c->scan_dirty = true;  // until the final kernel is launched
     crc32_long_kernel<kRaggedWG><<<c->num_cus, kRaggedWG, ragged_lds_bytes(), st>>>(
         static_cast<const uint8_t*>(dev_base), stride, (u32)pieces, (u32)count, c->d_tab, c->d_rops, init, final_xor,
-        c->d_tilecrc, (u32)g.nkmax);
+        c->d_tilecrc, (u32)g.nwb);
     HIP_TRY(hipGetLastError());
     rc = combine_tiles(c, g, nullptr, tiles, new_call_fault(c), st);
     if (rc) return rc;

@@ -6,22 +6,21 @@
 //    its exclusive prefix sum in ONE pass (decoupled look-back): tile_base[m] = tiles before
 //    message m, tile_base[count] = the batch's total. It also writes the (constant) result
 //    of zero-length messages, zeroes every other output word (the overflow path XORs tile
-//    values into it) and a slot batch's mismatch count, and the descriptor kernel's chunk
-//    hints: chunk_msg[c] = the message holding tile c * kDescTilesPerWave, for up to
-//    kChunkHints chunks per message (the descriptor kernel checks a hint against tile_base
-//    and searches when it does not hold -- a stale entry of an earlier call included).
-//  * Tile values. The main kernels store one value per tile wave-major, tilecrc[w*nkmax + k]
-//    for tile tau = k*nw + w (contiguous per flush: crc_ragged.hip). A message's CRC is the
+//    values into it) and a slot batch's mismatch count, and flags a batch whose tiles the
+//    8-B descriptors cannot hold (crc_ragged.hip TileDesc8).
+//  * Tile values. The main kernels store one value per tile, tile tau = k*nw + w at
+//    tilecrc[tilecrc_index(w, k)] (64 x 64 blocks of (w, k), w-major inside a block: contiguous
+//    per flush, crc_device.h). A message's CRC is the
 //    XOR of its tiles' values, i.e. P(t1 - 1) ^ P(t0 - 1) for the inclusive XOR prefix P in
 //    tile order. P is kept in two levels instead of as a full scan:
 //      segment s = 64 consecutive tiles of one sweep row k (tau = k*nw + 64*b + x, x < 64;
 //                  s = k*nwb + b, nwb = ceil(nw / 64)), ordered like tau;
-//      local[tau] = XOR of the values of tau's segment up to tau (inclusive),
+//      local[tau] = XOR of the values of tau's segment up to tau (inclusive; stored blocked),
 //      segx[s]    = XOR of all tile values before segment s (exclusive),
-//      P(tau)     = segx[s(tau)] ^ local[tau]                          (tile_prefix below).
-//    tile_segment_scan_kernel reads 64 x 64 blocks of the wave-major array through LDS (both
-//    the reads along k and the writes along w coalesced), scans each 64-tile row segment with
-//    a wave-wide XOR scan, writes local[] in tile order and each segment's XOR; the segment
+//      P(tau)     = segx[s(tau)] ^ local[tau]                          (tile_prefix, crc_device.h).
+//    tile_segment_scan_kernel reads one 16 KiB block of tilecrc through LDS, scans each 64-tile
+//    row segment with a wave-wide XOR scan, writes the block of local[] (k-major, local_index)
+//    and each segment's XOR; the segment
 //    XORs (1/64 of the tiles) get a single-pass exclusive look-back scan in place. (Storing
 //    local[] only at message-last tiles, the only ones the final kernels read, from a
 //    per-tile end mask written by the descriptor kernel, was slower: 36 -> 43 us at config
@@ -46,7 +45,6 @@ constexpr u64 kScanTile = (u64)kScanThreads * kScanItems;  // segment scan: elem
 constexpr int kCountItems = 16;
 constexpr u64 kCountTile = (u64)kScanThreads * kCountItems;  // tile-count scan: messages per workgroup
 constexpr u64 kFlagAggregate = 1, kFlagInclusive = 2;
-constexpr u64 kChunkHints = 4;  // chunk-index entries written per message (crc32_ragged_count_scan_kernel)
 
 // Sum of u64 values below 2^62 (tile counts): flag in the top two bits.
 struct SumOp {
@@ -191,8 +189,7 @@ __device__ __forceinline__ u64 msg_tiles(u64 s, u64 len) { return len ? (len + (
 __global__ __launch_bounds__(kScanThreads) void crc32_ragged_count_scan_kernel(
     const u64* __restrict__ offsets, u32 ostride, const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
     u32 final_xor, u64* __restrict__ tile_base, u32* __restrict__ out, u32* __restrict__ zero_word,
-    u64* __restrict__ status, u32* __restrict__ ticket, u32* __restrict__ chunk_msg, u64 nchunks,
-    FaultRef fault) {
+    u64* __restrict__ status, u32* __restrict__ ticket, u32* __restrict__ wide, FaultRef fault) {
   __shared__ u64 sx[kCountTile];  // striped (coalesced) global order <-> per-thread runs
   bool stale;
   const u64 tile = scan_ticket(ticket, fault, &stale);
@@ -204,29 +201,24 @@ __global__ __launch_bounds__(kScanThreads) void crc32_ragged_count_scan_kernel(
     const u64 i = base + (u64)(j * kScanThreads + tid);
     u64 nt = 0;
     if (i < count) {
-      nt = msg_tiles(offsets[i * ostride], lengths[i * lstride]);
+      const u64 so = offsets[i * ostride];
+      nt = msg_tiles(so, lengths[i * lstride]);
       out[i] = nt == 0 ? init ^ final_xor : 0u;
+      // a tile the 8-B descriptor cannot hold (crc_ragged.hip TileDesc8): the call keeps 16 B
+      if (nt && ((((so & ~(u64)15) + ((nt - 1) << 13)) >> kDesc8StartBits) | ((nt - 1) >> kDesc8AfterBits)))
+        *wide = 1u;
     } else if (i == count && zero_word) {
       *zero_word = 0u;  // a slot batch's mismatch count (no separate memset)
     }
     sx[j * kScanThreads + tid] = nt;
   }
   __syncthreads();
-  u64 x[kCountItems], nt[kCountItems];
+  u64 x[kCountItems];
 #pragma unroll
-  for (int j = 0; j < kCountItems; j++) x[j] = nt[j] = sx[tid * kCountItems + j];
+  for (int j = 0; j < kCountItems; j++) x[j] = sx[tid * kCountItems + j];
   scan_tile_lookback<SumOp, kCountItems>(x, tile, status, fault);  // synchronises before returning
 #pragma unroll
-  for (int j = 0; j < kCountItems; j++) {
-    sx[tid * kCountItems + j] = x[j];
-    // chunk hints: chunks whose first tile lies in this message, [ceil(tb / C), (tb + nt - 1) / C],
-    // at most kChunkHints of them (a longer message's later chunks are found by search)
-    if (nt[j]) {
-      const u64 m = base + (u64)(tid * kCountItems + j);
-      const u64 c0 = (x[j] + kDescTilesPerWave - 1) / kDescTilesPerWave, c1 = (x[j] + nt[j] - 1) / kDescTilesPerWave;
-      for (u64 c = c0; c <= c1 && c < c0 + kChunkHints && c < nchunks; c++) chunk_msg[c] = (u32)m;
-    }
-  }
+  for (int j = 0; j < kCountItems; j++) sx[tid * kCountItems + j] = x[j];
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kCountItems; j++) {
@@ -245,9 +237,10 @@ __device__ __forceinline__ u64 tiles_present(const u64* total_ptr, u64 n) {
   return n;
 }
 
-// Wave-major tile values -> per-segment inclusive XOR scans in tile order (local) and the
-// XOR of every segment (segx, before its scan). Block (a, b) covers k in [64a, +64) and
-// w in [64b, +64); wave q scans the rows k = 64a + q + 4i.
+// Tile values -> per-segment inclusive XOR scans (local) and the XOR of every segment (segx,
+// before its scan). Block (a, b) is the 64 x 64 block of k in [64a, +64), w in [64b, +64): it
+// reads tilecrc's 16 KiB block (w-major) and writes local's (k-major), both contiguous
+// (crc_device.h tilecrc_index / local_index); wave q scans the rows k = 64a + q + 4i.
 __global__ __launch_bounds__(256) void tile_segment_scan_kernel(const u32* __restrict__ in, u32 nw, u32 nkmax,
                                                                 u32 nwb, const u64* __restrict__ total_ptr, u64 n_cap,
                                                                 u32* __restrict__ local, u32* __restrict__ segx) {
@@ -255,11 +248,12 @@ __global__ __launch_bounds__(256) void tile_segment_scan_kernel(const u32* __res
   const u64 n = tiles_present(total_ptr, n_cap);
   const u32 k0 = blockIdx.x * 64u, w0 = blockIdx.y * 64u;
   if ((u64)k0 * nw + w0 >= n) return;  // every tile of the block is past the batch
+  const u64 blk = ((u64)blockIdx.x * nwb + blockIdx.y) * 4096u;
   const u32 x = threadIdx.x & 63u, y0 = threadIdx.x >> 6;
 #pragma unroll
   for (u32 i = 0; i < 16u; i++) {  // row w0 + y, column k0 + x
     const u32 y = y0 + 4u * i, w = w0 + y, k = k0 + x;
-    t[y][x] = (w < nw && k < nkmax) ? in[(u64)w * nkmax + k] : 0u;
+    t[y][x] = (w < nw && k < nkmax) ? in[blk + 64u * y + x] : 0u;
   }
   __syncthreads();
 #pragma unroll 4
@@ -277,7 +271,7 @@ __global__ __launch_bounds__(256) void tile_segment_scan_kernel(const u32* __res
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
     const u64 tau = (u64)k * nw + w;
     if (k < nkmax) {
-      if (w < nw && tau < n) local[tau] = v;
+      if (w < nw && tau < n) local[blk + 64u * y + x] = v;
       if (x == 63u) segx[(u64)k * nwb + blockIdx.y] = v;
     }
   }

@@ -24,6 +24,7 @@ using u32 = uint32_t;
 using u64 = uint64_t;
 using i64 = int64_t;
 using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+using u32x2 = __attribute__((ext_vector_type(2))) unsigned int;
 
 constexpr u32 kLdsTables = 0;
 constexpr u32 kLdsOps = 128u * 1024u;  // operator area; opmul slot s = 512 B at kLdsOps + 512*s
@@ -101,7 +102,9 @@ __device__ __forceinline__ void raise_scan_fault(FaultRef f, u32 bit) {
 }
 // A look-back scan of this call gave up: its tile_base is not to be trusted.
 __device__ __forceinline__ bool scan_faulted(FaultRef f) {
-  return f.word && __hip_atomic_load(f.word + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == f.gen;
+  // a plain load: the word is written by an earlier kernel of the call (a look-back scan that
+  // gave up), and the kernel boundary orders it
+  return f.word && f.word[1] == f.gen;
 }
 // Spin bound of every bounded wait, far beyond any real one: the look-back scans poll an
 // uncached status word up to 2^20 times without sleeping (~1 s, tests/test_gpu_fault.py); the
@@ -172,10 +175,10 @@ struct SmallArgs {
                      // the slot's payload area); ~0 for slot lists
 };
 
-// Ragged path: tiles per wave of the descriptor kernel, = the chunk of the tile-count scan's
-// chunk index (chunk_msg[c] = the message holding tile c * kDescTilesPerWave).
-constexpr u64 kDescTilesPerWave = 256;
-static_assert(kDescTilesPerWave % 64 == 0, "descriptor windows are 64-tile aligned");
+// 8-B tile descriptors (crc_ragged.hip TileDesc8) hold tile starts below 2^39 bytes and up to
+// 2^23 - 1 tiles after a tile; the tile-count scan flags a batch with any tile beyond that.
+constexpr u32 kDesc8StartBits = 39;
+constexpr u32 kDesc8AfterBits = 23;
 
 // Ragged kernel head seeds of one call: v[r] = Z_r^{-1}(init), r = 0..15 (a kernel argument).
 struct HeadSeeds {
@@ -417,10 +420,22 @@ __device__ __forceinline__ void issue_prio_lo() {
 // the XOR of every segment before tau's (segx, exclusive) and of tau's segment up to tau
 // (local). A segment is 64 consecutive tiles of one sweep row, s = k*nwb + w/64
 // (crc_combine.hip). tau < 2^32 (workspace capacities are bounded on the host).
+// Blocked layout of the per-tile values (tilecrc, written by the main kernels' flushes) and of
+// their segment prefixes (local, crc_combine.hip): 64 x 64 blocks of (wave w, sweep row k),
+// block (k >> 6, w >> 6) at (k >> 6) * nwb + (w >> 6), 16 KiB each. tilecrc holds a block
+// w-major (a flush of 64 tiles of one wave is 256 contiguous bytes), local k-major (a segment,
+// 64 tiles of one row, is 256 contiguous bytes): the segment scan reads and writes whole 16 KiB
+// blocks (tile order and wave-major order cost it 256-B runs at 8-30 KiB strides, r04q).
+__device__ __forceinline__ u64 tilecrc_index(u64 w, u64 k, u32 nwb) {
+  return ((((k >> 6) * nwb + (w >> 6)) << 6 | (w & 63)) << 6) | (k & 63);
+}
+__device__ __forceinline__ u64 local_index(u64 w, u64 k, u32 nwb) {
+  return ((((k >> 6) * nwb + (w >> 6)) << 6 | (k & 63)) << 6) | (w & 63);
+}
 __device__ __forceinline__ u32 tile_prefix(const u32* __restrict__ local, const u32* __restrict__ segx, u32 nw,
                                            u32 nwb, u64 tau) {
   const u32 t = (u32)tau, k = t / nw, w = t - k * nw;
-  return segx[(u64)k * nwb + (w >> 6)] ^ local[t];
+  return segx[(u64)k * nwb + (w >> 6)] ^ local[local_index(w, k, nwb)];
 }
 
 // Zero a look-back scan's status words and ticket (grid-stride) from a kernel that runs

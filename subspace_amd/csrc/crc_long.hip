@@ -14,7 +14,7 @@
 //  * combine exactly as crc_ragged.hip: per-lane line-shift operators Z_{128*(31-l)} and a
 //    DPP reduction give the two 4 KiB halves in lanes 31 and 63; tiles are parked one per
 //    lane and finished every 64 tiles: Z_{8192 * (P-1-j)}( Z_4096(h0) ^ h1 ), final XOR on
-//    the message's first piece, stored to tilecrc wave-major (w * nkmax + k);
+//    the message's first piece, stored to tilecrc blocked (tilecrc_index, crc_device.h);
 //  * message m's CRC = XOR of its P values = P((m+1)P - 1) ^ P(mP - 1) over the inclusive
 //    XOR prefix of the values in tile order (crc_combine.hip; crc32_long_final_kernel).
 #include "crc_device.h"
@@ -25,7 +25,7 @@ template <int WG>
 __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restrict__ base, u64 stride, u32 pieces,
                                                         u32 count, const u32* __restrict__ gtab,
                                                         const u32* __restrict__ gops, u32 init, u32 final_xor,
-                                                        u32* __restrict__ tilecrc, u32 nkmax) {
+                                                        u32* __restrict__ tilecrc, u32 nwb) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
   const int lane = threadIdx.x & 63;
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(WG) void crc32_long_kernel(const uint8_t* __restric
       rem >>= 1;
     }
     if (AF >> 31) c ^= final_xor;
-    if (valid) tilecrc[(u64)w * nkmax + kf + (u32)lane] = c;  // wave-major (crc_combine.hip)
+    if (valid) tilecrc[tilecrc_index(w, kf + (u32)lane, nwb)] = c;  // blocked (crc_device.h)
   };
 
   LdsFill<WG, kRagLdsOpWords / 128> fill;

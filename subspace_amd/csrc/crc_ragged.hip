@@ -20,8 +20,9 @@
 //    inverse operators Z_{2^b}^{-1} (b = 0..12; Z_n is invertible since P has an x^0 term)
 //    before the final XOR.
 //  * Waves stream the global tile list in sweep order (tau = k*nw + w), one tile of
-//    loads in flight ahead. Per-tile 16-B descriptors (tile start, tiles after, first-tile
-//    flag, bytes in the tile and mis) are precomputed by crc32_ragged_desc_kernel.
+//    loads in flight ahead. Per-tile 8-B descriptors (tile start, tiles after, first-tile
+//    flag, bytes in the last tile and mis; 16 B for batches beyond 2^39 bytes or with messages
+//    of 2^23 tiles and more) are precomputed by crc32_ragged_desc_kernel.
 //  * Per tile, lane l of half h applies its own line-shift operator Z_{128*(31-l)} (the
 //    uniform kernel's conflict-free [nibble][value][lane] tables) and a DPP reduction
 //    leaves the two half-tile values in lanes 31 and 63. They are parked, one tile per
@@ -49,6 +50,34 @@ struct TileDesc {
 };
 static_assert(sizeof(TileDesc) == 16, "TileDesc is 16 B");
 constexpr u32 kFirstTile = 0x80000000u;
+
+// 8 B per tile, the form every batch takes whose tile starts lie below 2^39 bytes and whose
+// messages have fewer than 2^23 + 1 tiles (the tile-count scan flags any other batch, which
+// keeps TileDesc): lo = bits 4..35 of the tile start; hi = bits 36..38 of it [2:0], mis [6:3],
+// the first-tile flag [7] and [31:8] either the tiles after this one or, for a message's last
+// tile, kLastTile8 | its bytes (only a last tile can be short; the count needs 14 bits).
+// Half the descriptor kernel's stores and the main kernel's descriptor loads.
+struct TileDesc8 {
+  u32 lo, hi;
+};
+static_assert(sizeof(TileDesc8) == 8, "TileDesc8 is 8 B");
+constexpr u32 kLastTile8 = 1u << kDesc8AfterBits;
+
+__device__ __forceinline__ TileDesc8 pack_desc8(const TileDesc& d) {
+  const u64 s16 = d.tile_start >> 4;
+  const u32 after = d.after & ~kFirstTile, len = d.len & 0xFFFFu, mis = d.len >> 16;
+  const u32 x = (after == 0u || len == 0u) ? (kLastTile8 | len) : after;  // len 0: a defensive empty tile
+  return TileDesc8{(u32)s16, ((u32)(s16 >> 32) & 7u) | (mis << 3) | ((d.after & kFirstTile) ? 0x80u : 0u) | (x << 8)};
+}
+__device__ __forceinline__ TileDesc unpack_desc8(u32 lo, u32 hi) {
+  TileDesc t;
+  t.tile_start = ((u64)(hi & 7u) << 36) | ((u64)lo << 4);
+  const u32 x = hi >> 8;
+  const bool last = (x & kLastTile8) != 0u;
+  t.after = (last ? 0u : x) | ((hi & 0x80u) ? kFirstTile : 0u);
+  t.len = (last ? (x & 0x3FFFu) : 8192u) | (((hi >> 3) & 15u) << 16);
+  return t;
+}
 
 __device__ inline u64 find_msg(const u64* __restrict__ tile_base, u64 count, u64 tau) {
   // last m with tile_base[m] <= tau (skips zero-tile messages, whose base equals the next one's)
@@ -87,71 +116,125 @@ __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, u32 ostrid
 }
 
 
-// Per tile (up to `capacity`): its descriptor. Sets *overflow if the batch has more tiles.
-// Wave g covers tiles [g*kDescTilesPerWave, +kDescTilesPerWave). The message of its first
-// tile comes from the tile-count scan's chunk hint (chunk_msg[g], crc_combine.hip: one load
-// instead of a 20-step binary search), checked with the first window's candidates and
-// replaced by a search where it does not hold (chunks deep inside a long message get no
-// hint); then per 64-tile window lane l holds tile_base[m0 + l]
-// (one coalesced load) and each lane finds its tile's message with a 6-step shuffle search
-// over those 64 bases. Only a window whose 64 candidates do not reach a lane's tile (runs of
-// zero-length messages) searches globally for that lane. A search per tile (the first form)
-// cost 20 dependent loads per tile (0.25 ms on config C); a binary search per wave for its
-// first tile's message (before the chunk index) 14 us more per config-C call (r02f).
+// Per tile (up to `capacity`): its descriptor, 8 B unless the tile-count scan flagged the batch
+// wide (overflow[1]). Sets overflow[0] if the batch has more tiles (then nothing is written:
+// the main kernel searches). Message-centric: thread m of column x reads its message's tile
+// range and (offset, length) with coalesced loads -- no search -- and stores the descriptors of
+// its first kLaneTiles tiles itself (neighbouring lanes hold neighbouring messages, so for small
+// messages a wave's stores are contiguous); the later tiles of a longer message are stored by
+// the whole wave, 64 per store, one message after the other, store i of a message by the
+// workgroup row y = i mod gridDim.y (the host adds rows when a batch has few, long messages:
+// config D). The 8-B form of a later tile is built incrementally from the message's first
+// (a dozen VALU ops per store: the kernel is VALU-bound). The tile-parallel form (a 64-candidate
+// shuffle search per tile from chunk hints) ran 63-72 us per config-C call.
+constexpr u32 kLaneTiles = 2;  // 1, 4, 8: slower (r04o, r04p)
 __global__ __launch_bounds__(256) void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, u32 ostride,
                                                                 const u64* __restrict__ lengths, u32 lstride,
                                                                 const u64* __restrict__ tile_base, u64 count,
-                                                                u64 capacity, const u32* __restrict__ chunk_msg,
-                                                                TileDesc* __restrict__ desc, u32* __restrict__ overflow, u64* scan_status,
+                                                                u64 capacity, TileDesc* __restrict__ desc,
+                                                                u32* __restrict__ overflow, u64* scan_status,
                                                                 u64 scan_words, u32* scan_ticket, FaultRef fault) {
-  reset_scan_state(scan_status, scan_words, scan_ticket);  // the tile-count scan is done
+  if (blockIdx.y == 0) reset_scan_state(scan_status, scan_words, scan_ticket);  // the tile-count scan is done
   if (scan_faulted(fault)) return;
   const u64 total = tile_base[count];
-  const u64 limit = total < capacity ? total : capacity;
-  const int lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *overflow = total > capacity ? 1u : 0u;
-  const u64 g = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const u64 t_begin = g * kDescTilesPerWave;
-  if (t_begin >= limit) return;  // wave-uniform
-  const u64 t_end = t_begin + kDescTilesPerWave < limit ? t_begin + kDescTilesPerWave : limit;
-  u64 m0 = chunk_msg[g];  // a hint: tile_base[m0] <= t_begin < tile_base[m0 + 1] if it holds
-  for (u64 t0 = t_begin; t0 < t_end; t0 += 64) {
-    const u64 tau = t0 + (u64)lane;
-    u64 mc = m0 + (u64)lane;
-    // nondecreasing over lanes; tile_base[count] = total > every tile, past it: +inf
-    u64 cand = mc <= count ? tile_base[mc] : ~(u64)0;
-    if (t0 == t_begin) {  // check the hint (lanes 0, 1 hold tile_base[m0], tile_base[m0 + 1])
-      const u64 b0 = __shfl(cand, 0, 64), b1 = __shfl(cand, 1, 64);
-      if (!(m0 < count && b0 <= t_begin && t_begin < b1)) {
-        m0 = find_msg(tile_base, count, t_begin);
-        mc = m0 + (u64)lane;
-        cand = mc <= count ? tile_base[mc] : ~(u64)0;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) overflow[0] = total > capacity ? 1u : 0u;
+  if (total > capacity) return;  // the search path: no descriptors
+  const bool wide = overflow[1] != 0u;
+  TileDesc8* const desc8 = reinterpret_cast<TileDesc8*>(desc);
+  const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  u64 t0 = 0, nt = 0, so = 0, L = 0;
+  if (m < count) {
+    t0 = tile_base[m];
+    nt = tile_base[m + 1] - t0;
+    so = offsets[m * ostride];
+    L = lengths[m * lstride];
+  }
+  // tile j of the message at so with length tL, first tile tt0 and tnt tiles (any form)
+  auto put = [&](u64 tso, u64 tL, u64 tt0, u64 tnt, u64 j) {
+    const u32 mis = (u32)(tso & 15);
+    const u64 rest = tL + mis - (j << 13);
+    TileDesc d;
+    d.tile_start = (tso & ~(u64)15) + (j << 13);
+    d.after = (u32)(tnt - 1 - j) | (j == 0 ? kFirstTile : 0u);
+    d.len = (rest < 8192 ? (u32)rest : 8192u) | (mis << 16);
+    if (wide) desc[tt0 + j] = d;
+    else desc8[tt0 + j] = pack_desc8(d);
+  };
+  if (blockIdx.y == 0) {
+#pragma unroll
+    for (u32 j = 0; j < kLaneTiles; j++)
+      if (j < nt) put(so, L, t0, nt, j);
+  }
+  // longer messages: the wave stores tiles kLaneTiles.. of each, lanes along the tiles
+  const u32 lane = threadIdx.x & 63u;
+  const u32 y = rfl(blockIdx.y), ystep = 64u * rfl(gridDim.y);  // in SGPRs, read once
+  if (!wide) {
+    // Load-balanced expansion: the later tiles of the wave's 64 messages are numbered q = 0 ..
+    // W - 1 in message order (an exclusive wave scan of b = nt - kLaneTiles); lane l of round r
+    // stores tile q = 64 (y + r gridDim.y) + l, its message found by a 6-step binary search over
+    // the 64 scan values in LDS. Every store has 64 useful lanes, and a wave takes W / 64
+    // rounds instead of one round per long message.
+    __shared__ u32 sx[4][8][64];  // per wave: excl, s16 lo, s16 hi, mis << 3, last, last_len, t0 lo, t0 hi
+    const u32 wv = threadIdx.x >> 6;
+    const u32 b = nt > kLaneTiles ? (u32)nt - kLaneTiles : 0u;
+    u32 incl = b;
+#pragma unroll
+    for (u32 d = 1; d < 64; d <<= 1) {
+      const u32 t = (u32)__shfl_up((int)incl, d, 64);
+      if (lane >= d) incl += t;
+    }
+    const u32 W = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+    if (W == 0u) return;  // wave-uniform
+    const u32 mis = (u32)(so & 15), last = (u32)nt - 1u;
+    const u64 s16 = so >> 4;
+    sx[wv][0][lane] = incl - b;
+    sx[wv][1][lane] = (u32)s16;
+    sx[wv][2][lane] = (u32)(s16 >> 32);
+    sx[wv][3][lane] = mis << 3;
+    sx[wv][4][lane] = last;
+    sx[wv][5][lane] = (u32)(L + mis - ((u64)last << 13));
+    sx[wv][6][lane] = (u32)t0;
+    sx[wv][7][lane] = (u32)(t0 >> 32);
+    wave_lds_sync();
+    for (u32 q0 = 64u * y; q0 < W; q0 += ystep) {
+      const u32 q = q0 + lane;
+      u32 o = 0;
+#pragma unroll
+      for (u32 st = 32; st; st >>= 1)
+        if (sx[wv][0][o + st] <= q) o += st;
+      if (q < W) {
+        const u32 j = kLaneTiles + q - sx[wv][0][o];
+        const u64 t16 = (((u64)sx[wv][2][o] << 32) | sx[wv][1][o]) + ((u64)j << 9);
+        const u32 ol = sx[wv][4][o];
+        const u32 x = j == ol ? (kLastTile8 | sx[wv][5][o]) : ol - j;
+        const u64 ot0 = ((u64)sx[wv][7][o] << 32) | sx[wv][6][o];
+        desc8[ot0 + j] = TileDesc8{(u32)t16, ((u32)(t16 >> 32) & 7u) | sx[wv][3][o] | (x << 8)};
       }
     }
-    int lo = 0;  // last lane with cand <= tau (lane 0 always: cand_0 <= t0 <= tau)
-#pragma unroll
-    for (int step = 32; step; step >>= 1) {
-      const u64 v = __shfl(cand, lo + step, 64);
-      if (v <= tau) lo += step;
-    }
-    // lo < 63: cand_{lo+1} > tau, so m0 + lo is tau's message. lo = 63: not known whether
-    // message m0 + 64 starts at or before tau; search for it (mc <= count for all lanes here).
-    u64 m = m0 + (u64)lo;
-    if (lo == 63 && tau < t_end) m = find_msg(tile_base, count, tau);
-    if (tau < t_end) desc[tau] = make_desc(offsets, ostride, lengths, lstride, tile_base, m, tau);
-    m0 = __shfl(m, 63, 64);  // message of tile t0 + 63, the next window's first candidate
+    return;
+  }
+  // wide batches (16-B descriptors): one long message after the other, 64 tiles per store
+  u64 big = __ballot(nt > kLaneTiles);
+  while (big) {
+    const int src = __ffsll((unsigned long long)big) - 1;
+    big &= big - 1;
+    const u64 bt0 = __shfl(t0, src, 64), bnt = __shfl(nt, src, 64);
+    const u64 bso = __shfl(so, src, 64), bL = __shfl(L, src, 64);
+    for (u64 j = kLaneTiles + 64ull * y + lane; j < bnt; j += ystep) put(bso, bL, bt0, bnt, j);
   }
 }
 
 // ------------------------------------------------------------------ main kernel
 
-template <int WG, bool DESC>
+// MODE: kDescSearch (no descriptors: every tile located by binary search), kDesc16, kDesc8.
+constexpr int kDescSearch = 0, kDesc16 = 1, kDesc8 = 2;
+template <int WG, int MODE>
 __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, const u64* __restrict__ offsets,
                                             u32 ostride, const u64* __restrict__ lengths, u32 lstride,
                                             const u64* __restrict__ tile_base, u64 count,
                                             const TileDesc* __restrict__ desc, const u32* __restrict__ gtab,
                                             const u32* __restrict__ gops, const HeadSeeds& seeds,
-                                            u32* __restrict__ out, u32* __restrict__ tilecrc, u64 nkmax,
+                                            u32* __restrict__ out, u32* __restrict__ tilecrc, u32 nwb,
                                             u32 sbase) {
   const int lane = threadIdx.x & 63;
   const u32 wid = rfl(threadIdx.x >> 6);
@@ -169,13 +252,18 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
   u32 vzero;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
 
-  // Descriptor of tile k as raw dwords (a vector load; DESC false: built by search, with
+  // Descriptor of tile k as raw dwords (a vector load; kDescSearch: built by search, with
   // the message id for the atomic path). Past the wave's last tile it is clamped to that
   // tile; a wave without tiles uses the batch's last tile, so every load the kernel issues
   // stays inside a real message.
+  constexpr bool DESC = MODE != kDescSearch;
   auto fetch_desc = [&](u64 k, u32x4& d, u32& dm) {
     const u64 tau = nk ? (k < nk ? k : nk - 1) * nw + w : total - 1;
-    if (DESC) {
+    if (MODE == kDesc8) {
+      const u32x2 v = *reinterpret_cast<const u32x2*>(reinterpret_cast<const TileDesc8*>(desc) + tau + vzero);
+      d = u32x4{v[0], v[1], 0u, 0u};
+      dm = 0;
+    } else if (MODE == kDesc16) {
       d = *reinterpret_cast<const u32x4*>(desc + tau + vzero);
       dm = 0;
     } else {
@@ -186,6 +274,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
     }
   };
   auto unpack = [&](const u32x4& d) {
+    if constexpr (MODE == kDesc8) return unpack_desc8(rfl(d[0]), rfl(d[1]));
     TileDesc t;
     t.tile_start = rfl64(d[0], d[1]);
     t.after = rfl(d[2]);
@@ -261,7 +350,7 @@ __device__ __forceinline__ void ragged_body(const uint8_t* __restrict__ base, co
       rem >>= 1;
     }
     if (valid) {
-      if (DESC) tilecrc[w * nkmax + kf + (u64)lane] = c;  // wave-major: contiguous per flush
+      if (DESC) tilecrc[tilecrc_index(w, kf + (u64)lane, nwb)] = c;  // blocked: contiguous per flush
       else atomicXor(&out[MG], c);
     }
   };
@@ -328,23 +417,26 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
                                                           const u32* __restrict__ overflow,
                                                           const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                           HeadSeeds seeds, u32* __restrict__ out,
-                                                          u32* __restrict__ tilecrc, u64 nkmax, FaultRef fault) {
+                                                          u32* __restrict__ tilecrc, u32 nwb, FaultRef fault) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
   if (scan_faulted(fault)) return;  // workgroup-uniform, before any barrier
-  // Precomputed descriptors unless the batch had more tiles than the workspace holds
-  // (overlapping messages); then every tile is located by binary search.
-  if (*overflow == 0u)
-    ragged_body<WG, true>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, seeds, out,
-                          tilecrc, nkmax, sbase);
+  // Precomputed descriptors (8 B, or 16 B for a wide batch) unless the batch had more tiles
+  // than the workspace holds (overlapping messages); then every tile is located by binary search.
+  if (overflow[0] != 0u)
+    ragged_body<WG, kDescSearch>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, seeds,
+                                 out, tilecrc, nwb, sbase);
+  else if (overflow[1] != 0u)
+    ragged_body<WG, kDesc16>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, seeds, out,
+                             tilecrc, nwb, sbase);
   else
-    ragged_body<WG, false>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, seeds, out,
-                           tilecrc, nkmax, sbase);
+    ragged_body<WG, kDesc8>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, seeds, out,
+                            tilecrc, nwb, sbase);
 }
 
 template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
                                                   const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds,
-                                                  u32*, u32*, u64, FaultRef);
+                                                  u32*, u32*, u32, FaultRef);
 
 // Per message with tiles: its padded CRC = XOR of its tiles' values = P(t1 - 1) ^ P(t0 - 1)
 // (P = inclusive XOR prefix of the tile values in tile order, crc_combine.hip), or the XOR
@@ -354,10 +446,14 @@ template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u3
 __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, const u64* __restrict__ offsets,
                                           u32 ostride, const u64* __restrict__ lengths, u32 lstride, u64 count,
                                           const u32* __restrict__ local, const u32* __restrict__ segx, u32 nw, u32 nwb,
-                                          const u32* __restrict__ overflow, const u32* __restrict__ gops,
+                                          u32* __restrict__ overflow, const u32* __restrict__ gops,
                                           u32 final_xor, u32* __restrict__ out, u64* scan_status, u64 scan_words,
                                           u32* scan_ticket, FaultRef fault) {
   reset_scan_state(scan_status, scan_words, scan_ticket);  // the segment scan is done
+  // the wide flag (overflow[1]): set by the tile-count scan, read by the descriptor and main
+  // kernels, zero again for the next call (a call that faulted before this point leaves it
+  // set: the next call then takes 16-B descriptors, correct either way)
+  if (blockIdx.x == 0 && threadIdx.x == 0) overflow[1] = 0u;
   if (scan_faulted(fault)) return;
   // the 13 inverse operators (6.5 KiB) staged in LDS: up to 104 dependent table lookups
   // per message read from global memory took 61 us for config C's 1 Mi messages (r01bu)
@@ -365,11 +461,17 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
   for (u32 i = threadIdx.x; i < kNumInvOps * 128u; i += blockDim.x) inv[i] = gops[kRagInvOps + i];
   __syncthreads();
   const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= count) return;
-  const u64 t0 = tile_base[m], t1 = tile_base[m + 1];
-  if (t1 == t0) return;  // empty message: written by the count kernel
-  u32 v = *overflow ? out[m]
-                    : tile_prefix(local, segx, nw, nwb, t1 - 1) ^ (t0 ? tile_prefix(local, segx, nw, nwb, t0 - 1) : 0u);
+  const bool live = m < count;
+  const u64 t0 = live ? tile_base[m] : 0, t1 = live ? tile_base[m + 1] : 0;
+  const bool ovf = *overflow != 0u;
+  // P(t1 - 1) of every message (empty ones included), and P(t0 - 1) = the previous message's
+  // P(t1 - 1) from the neighbouring lane: one prefix gather per message instead of two (lane 0
+  // gathers its own)
+  const u32 pe = (!ovf && live && t1) ? tile_prefix(local, segx, nw, nwb, t1 - 1) : 0u;
+  u32 pb = (u32)__shfl_up((int)pe, 1, 64);
+  if ((threadIdx.x & 63u) == 0u) pb = (!ovf && live && t0) ? tile_prefix(local, segx, nw, nwb, t0 - 1) : 0u;
+  if (!live || t1 == t0) return;  // empty message: written by the count kernel
+  u32 v = ovf ? out[m] : pe ^ pb;
   const u32 pad = (u32)(0 - (lengths[m * lstride] + (offsets[m * ostride] & 15))) & 8191u;
 #pragma unroll 1
   for (int b = 0; b < kNumInvOps; b++) {

@@ -2,6 +2,9 @@
 crc_ragged.hip make_desc + load_line, crc_uniform.hip load_tile, and the sweep
 front mapping): every byte any load can read lies inside the caller's messages, every
 message byte is read, every tile is visited exactly once. Runs without a GPU."""
+import collections
+import itertools
+
 import numpy as np
 import pytest
 
@@ -196,63 +199,47 @@ def test_xcd_group_slot_is_a_bijection(wg, grid):
         assert len({xcd[16 * g + i] for i in range(16)}) == 1
 
 
-def chunk_index(ntiles, nchunks, per_wave=256, hints=4, stale=None):
-    """Replays the chunk hints crc32_ragged_count_scan_kernel writes: for every message with
-    tiles, chunk_msg[c] = m for the first `hints` chunks c whose first tile c * per_wave lies
-    in it. Other entries keep what an earlier call left (`stale`, default garbage)."""
-    tb = np.concatenate([[0], np.cumsum(ntiles, dtype=np.int64)])
-    chunk = np.array(stale if stale is not None else np.full(nchunks, 2**32 - 1), dtype=np.int64)
-    for m, nt in enumerate(ntiles):
-        if nt:
-            c0, c1 = -(-int(tb[m]) // per_wave), (int(tb[m]) + int(nt) - 1) // per_wave
-            for c in range(c0, min(c1, c0 + hints - 1, nchunks - 1) + 1):
-                chunk[c] = m
-    return chunk
-
-
-def desc_kernel_messages(ntiles, capacity, per_wave=256, stale=None):
-    """Replays crc32_ragged_desc_kernel's message lookup: per wave, its first tile's message
-    from the chunk index, then per 64-tile window a search over the 64 candidate bases
-    tile_base[m0 + l] (+inf past tile_base[count]), the global search when the last candidate
-    is reached, and the next window's m0 = lane 63's message. Returns ({tile: message},
-    tile_base)."""
+def desc_kernel_stores(ntiles, capacity, lane_tiles=2, rows=1):
+    """Replays crc32_ragged_desc_kernel (crc_ragged.hip, message-centric): thread m stores
+    tiles tile_base[m] + j of its message for j < min(nt, kLaneTiles); then per wave, for each
+    wave, the later tiles of its 64 messages in the load-balanced expansion below. Nothing is
+    stored when the batch has more tiles than the capacity. Returns ({tile: (message, j)} with every store counted, tile_base)."""
     count = len(ntiles)
-    tb = np.concatenate([[0], np.cumsum(ntiles, dtype=np.int64)])  # tile_base, count + 1 entries
+    tb = np.concatenate([[0], np.cumsum(ntiles, dtype=np.int64)])
     total = int(tb[count])
-    limit = min(total, capacity)
-    chunk = chunk_index(ntiles, -(-capacity // per_wave), per_wave, stale=stale)
+    stores = collections.Counter()
+    owner = {}
+    if total > capacity:
+        return owner, stores, tb
+    for w0 in range(0, count, 64):
+        ms = range(w0, min(w0 + 64, count))
+        for m in ms:
+            for j in range(min(int(ntiles[m]), lane_tiles)):
+                owner[int(tb[m]) + j] = (m, j)
+                stores[int(tb[m]) + j] += 1
+        # SUBSPACE_DESC_EXPAND: later tiles numbered q in message order (exclusive scan of
+        # b = nt - kLaneTiles), round r of row y stores q = 64 (y + r rows) + lane, its message by a
+        # 6-step binary search over the 64 scan values (lanes past the wave's messages: b = 0)
+        b = [max(int(ntiles[m]) - lane_tiles, 0) for m in ms] + [0] * (64 - len(ms))
+        ex = list(itertools.accumulate([0] + b[:-1]))
+        W = ex[63] + b[63]
+        for y in range(rows):
+            for q0 in range(64 * y, W, 64 * rows):
+                for lane in range(64):
+                    q = q0 + lane
+                    o = 0
+                    for st in (32, 16, 8, 4, 2, 1):
+                        if ex[o + st] <= q:
+                            o += st
+                    if q < W:
+                        m, j = w0 + o, lane_tiles + q - ex[o]
+                        owner[int(tb[m]) + j] = (m, j)
+                        stores[int(tb[m]) + j] += 1
+    return owner, stores, tb
 
-    def find_msg(tau):  # last m < count with tb[m] <= tau
-        return int(np.searchsorted(tb[:count], tau, side="right")) - 1
 
-    got = {}
-    for t_begin in range(0, limit, per_wave):
-        t_end = min(t_begin + per_wave, limit)
-        m0 = int(chunk[t_begin // per_wave])  # a hint, checked against the first window
-        for t0 in range(t_begin, t_end, 64):
-            cand = [int(tb[m0 + l]) if m0 + l <= count else 1 << 62 for l in range(64)]
-            if t0 == t_begin and not (m0 < count and cand[0] <= t_begin < cand[1]):
-                m0 = find_msg(t_begin)
-                cand = [int(tb[m0 + l]) if m0 + l <= count else 1 << 62 for l in range(64)]
-            ms = []
-            for lane in range(64):
-                tau = t0 + lane
-                lo = 0
-                for step in (32, 16, 8, 4, 2, 1):
-                    if cand[lo + step] <= tau:
-                        lo += step
-                m = m0 + lo
-                if lo == 63 and tau < t_end:
-                    m = find_msg(tau)
-                if tau < t_end:
-                    got[tau] = m
-                ms.append(m)
-            m0 = ms[63]
-    return got, tb
-
-
-@pytest.mark.parametrize("seed", range(8))
-def test_desc_window_search_matches_binary_search(seed):
+@pytest.mark.parametrize("seed,rows", [(s, 1) for s in range(6)] + [(6, 3), (7, 64)])
+def test_desc_kernel_stores_every_tile_once(seed, rows):
     rng = np.random.default_rng(seed)
     parts = []
     for _ in range(40):
@@ -261,12 +248,15 @@ def test_desc_window_search_matches_binary_search(seed):
         parts.append(rng.integers(3, 300, int(rng.integers(0, 3))))        # multi-tile messages
     ntiles = np.concatenate(parts).astype(np.int64)
     total = int(ntiles.sum())
-    for capacity, stale in ((total, None), (total - 37, None), (64 * 5 + 3, None),
-                            (total, rng.integers(0, len(ntiles) + 5, -(-total // 256)))):
-        got, tb = desc_kernel_messages(ntiles, capacity, stale=stale)
-        assert sorted(got) == list(range(min(total, capacity)))
-        for tau, m in got.items():
-            assert tb[m] <= tau < tb[m + 1], (capacity, tau, m)
+    for capacity in (total, total + 1000, total - 1):
+        owner, stores, tb = desc_kernel_stores(ntiles, capacity, rows=rows)
+        if capacity < total:
+            assert not owner  # the search path: no descriptors
+            continue
+        assert sorted(owner) == list(range(total))
+        assert set(stores.values()) == {1}
+        for tau, (m, j) in owner.items():
+            assert tb[m] <= tau < tb[m + 1] and tau == tb[m] + j
 
 
 # ------------------------------------------------------------------ fused slot kernel
@@ -535,3 +525,97 @@ def test_host_slot_list_accesses_stay_in_registered_regions(seed, count, cs, ms)
             reg = regions[0]
         lo, hi = pages(reg)
         assert lo <= addr and addr + w <= hi, (kind, m, addr, reg)
+
+
+# ------------------------------------------------------------------ 8-B tile descriptors
+K_FIRST, K_LAST8 = 0x80000000, 1 << 23
+
+
+def pack_desc8(tile_start, after, first, length, mis):
+    """crc_ragged.hip pack_desc8 (TileDesc -> TileDesc8), restated."""
+    s16 = tile_start >> 4
+    x = (K_LAST8 | length) if (after == 0 or length == 0) else after
+    hi = ((s16 >> 32) & 7) | (mis << 3) | (0x80 if first else 0) | (x << 8)
+    return s16 & 0xFFFFFFFF, hi & 0xFFFFFFFF
+
+
+def unpack_desc8(lo, hi):
+    """crc_ragged.hip unpack_desc8, restated: (tile_start, after | first flag, len | mis << 16)."""
+    tile_start = ((hi & 7) << 36) | (lo << 4)
+    x = hi >> 8
+    last = (x & K_LAST8) != 0
+    after = (0 if last else x) | (K_FIRST if hi & 0x80 else 0)
+    length = ((x & 0x3FFF) if last else 8192) | (((hi >> 3) & 15) << 16)
+    return tile_start, after, length
+
+
+def wide_message(s, length):
+    """crc32_ragged_count_scan_kernel's flag: a tile of message (s, length) beyond the 8-B form."""
+    nt = (length + (s & 15) + 8191) >> 13 if length else 0
+    return nt > 0 and ((((s & ~15) + ((nt - 1) << 13)) >> 39) != 0 or ((nt - 1) >> 23) != 0)
+
+
+def descs_of(s, length):
+    """make_desc for every tile of one message: (tile_start, after, first, bytes, mis)."""
+    mis = s & 15
+    nt = (length + mis + 8191) >> 13
+    for j in range(nt):
+        rest = length + mis - (j << 13)
+        yield (s & ~15) + (j << 13), nt - 1 - j, j == 0, min(rest, 8192), mis
+
+
+@pytest.mark.parametrize("s,length", [(0, 1), (15, 1), (3, 8189), (3, 8190), (0, 8192), (1, 8192), (7, 3 * 8192 + 5),
+                                      ((1 << 39) - 8192 - 16, 8192), ((1 << 39) - 8192 - 16 + 9, 8183),
+                                      ((1 << 38) + 17, 5 << 13), (4096, (1 << 23) << 13)])
+def test_desc8_round_trip_or_flagged(s, length):
+    """Every tile of a message that the count scan does not flag round-trips through the 8-B
+    form exactly; a flagged message is one whose tiles would not."""
+    if wide_message(s, length):
+        nt = (length + (s & 15) + 8191) >> 13
+        last_start = (s & ~15) + ((nt - 1) << 13)
+        assert last_start >= 1 << 39 or nt - 1 >= 1 << 23
+        return
+    n = 0
+    for tile_start, after, first, nbytes, mis in descs_of(s, length):
+        lo, hi = pack_desc8(tile_start, after, first, nbytes, mis)
+        want = (tile_start, after | (K_FIRST if first else 0), nbytes | (mis << 16))
+        assert unpack_desc8(lo, hi) == want
+        n += 1
+        if n > 64:  # long messages: the first 64 tiles and the last one
+            mis = s & 15
+            nt = (length + mis + 8191) >> 13
+            last = ((s & ~15) + ((nt - 1) << 13), 0, nt == 1, length + mis - ((nt - 1) << 13), mis)
+            assert unpack_desc8(*pack_desc8(*last)) == (last[0], last[1] | (K_FIRST if last[2] else 0),
+                                                          last[3] | (last[4] << 16))
+            break
+
+
+def test_desc8_flag_edges():
+    # the last tile start 2^39 - 16 fits; 2^39 does not
+    assert not wide_message((1 << 39) - 16, 1)
+    assert wide_message(1 << 39, 1)
+    assert wide_message((1 << 39) - 8192, 8193)  # second tile starts at 2^39
+    # 2^23 tiles: after up to 2^23 - 1 fits
+    assert not wide_message(0, (1 << 23) << 13)
+    assert wide_message(0, ((1 << 23) << 13) + 1)
+    assert not wide_message(0, 0)
+
+
+def desc8_incremental(so, length, j):
+    """crc32_ragged_desc_kernel's later tiles (j >= kLaneTiles), built from the message's first."""
+    mis = so & 15
+    nt = (length + mis + 8191) >> 13
+    last = nt - 1
+    last_len = length + mis - (last << 13)
+    t16 = (so >> 4) + (j << 9)
+    x = (K_LAST8 | last_len) if j == last else last - j
+    return t16 & 0xFFFFFFFF, ((t16 >> 32) & 7) | (mis << 3) | (x << 8)
+
+
+@pytest.mark.parametrize("so,length", [(0, 3 * 8192), (5, 3 * 8192), (4095, 100000), ((1 << 39) - (40 << 13) + 3, 30 << 13),
+                                       ((1 << 36) - 8192 * 2 - 1, 9 * 8192 + 1), (1 << 32, (1 << 20) + 7)])
+def test_desc8_incremental_matches_pack(so, length):
+    assert not wide_message(so, length)
+    tiles = list(descs_of(so, length))
+    for j in range(2, len(tiles)):
+        assert desc8_incremental(so, length, j) == pack_desc8(*tiles[j]), j

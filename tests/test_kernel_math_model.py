@@ -196,39 +196,57 @@ def test_uniform_per_lane_operators_and_dpp_reduction():
         assert red[31] == ref(init, msgs[0]) and red[63] == ref(init, msgs[1])
 
 
+def tilecrc_index(w, k, nwb):
+    """crc_device.h tilecrc_index: 64 x 64 blocks of (w, k), w-major inside a block."""
+    return ((((k >> 6) * nwb + (w >> 6)) << 6 | (w & 63)) << 6) | (k & 63)
+
+
+def local_index(w, k, nwb):
+    """crc_device.h local_index: the same blocks, k-major inside a block."""
+    return ((((k >> 6) * nwb + (w >> 6)) << 6 | (k & 63)) << 6) | (w & 63)
+
+
 def _segment_combine_model(values_tau, nw):
-    """Replay of crc_combine.hip on the CPU: the wave-major array the main kernels write
-    (tile tau = k*nw + w at w*nkmax + k), tile_segment_scan_kernel (64-tile row segments,
-    inclusive XOR scan per segment, segment XORs), segment_prefix_kernel (exclusive XOR scan
-    of the segment XORs) and tile_prefix (crc_device.h)."""
+    """Replay of crc_combine.hip on the CPU: the blocked tile-value array the main kernels write
+    (tile tau = k*nw + w at tilecrc_index(w, k)), tile_segment_scan_kernel (block (a, b): 64-tile
+    row segments, inclusive XOR scan per segment into local_index(w, k), segment XORs),
+    segment_prefix_kernel (exclusive XOR scan of the segment XORs) and tile_prefix (crc_device.h)."""
     n = len(values_tau)
     nkmax = -(-max(n, 1) // nw)
     nwb = -(-nw // 64)
-    wave_major = np.zeros(nw * nkmax, dtype=np.uint32)
-    tau = np.arange(n)
-    wave_major[(tau % nw) * nkmax + tau // nw] = values_tau
-    local = np.zeros(n, dtype=np.uint32)
+    nblk = -(-nkmax // 64) * nwb
+    tilecrc = np.full(nblk * 4096, 0xDEADBEEF, dtype=np.uint32)  # never-written entries: garbage
+    for t in range(n):
+        tilecrc[tilecrc_index(t % nw, t // nw, nwb)] = values_tau[t]
+    local = np.full(nblk * 4096, 0xDEADBEEF, dtype=np.uint32)
     segx = np.zeros(nkmax * nwb, dtype=np.uint32)
-    for k in range(nkmax):
+    for a in range(-(-nkmax // 64)):
         for b in range(nwb):
-            row = np.zeros(64, dtype=np.uint32)
-            for x in range(64):
-                w = 64 * b + x
-                if w < nw:
-                    row[x] = wave_major[w * nkmax + k]
-            scan = np.bitwise_xor.accumulate(row)
-            for x in range(64):
-                w = 64 * b + x
-                t = k * nw + w
-                if w < nw and t < n:
-                    local[t] = scan[x]
-            segx[k * nwb + b] = scan[63]
+            blk = (a * nwb + b) * 4096
+            tile = np.zeros((64, 64), dtype=np.uint32)  # t[y][x]: w = 64 b + y, k = 64 a + x
+            for y in range(64):
+                for x in range(64):
+                    w, k = 64 * b + y, 64 * a + x
+                    if w < nw and k < nkmax:
+                        assert blk + 64 * y + x == tilecrc_index(w, k, nwb)
+                        tile[y][x] = tilecrc[blk + 64 * y + x]
+            for y in range(64):  # row k = 64 a + y
+                k = 64 * a + y
+                if k >= nkmax:
+                    continue
+                scan = np.bitwise_xor.accumulate(tile[:, y])
+                for x in range(64):
+                    w = 64 * b + x
+                    if w < nw and k * nw + w < n:
+                        assert blk + 64 * y + x == local_index(w, k, nwb)
+                        local[blk + 64 * y + x] = scan[x]
+                segx[k * nwb + b] = scan[63]
     excl = np.zeros_like(segx)
     excl[1:] = np.bitwise_xor.accumulate(segx)[:-1]
 
     def tile_prefix(t):
         k, w = t // nw, t % nw
-        return int(excl[k * nwb + (w >> 6)] ^ local[t])
+        return int(excl[k * nwb + (w >> 6)] ^ local[local_index(w, k, nwb)])
     return tile_prefix
 
 
