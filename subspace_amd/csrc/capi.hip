@@ -85,9 +85,11 @@ uintptr_t host_alias(uintptr_t p, uint64_t n) {
     if (p >= r.host && p - r.host <= r.bytes && n <= r.bytes - (p - r.host)) return r.dev + (p - r.host);
   return 0;
 }
+#ifndef SUBSPACE_DESC_ROWS_MIN
+#define SUBSPACE_DESC_ROWS_MIN 1  // A/B: rows of the descriptor kernel's grid at least
+#endif
 constexpr size_t kTileDescBytes = 16;  // the wide form; 8 B (TileDesc8) for most batches
 constexpr u64 kScanTile = 4096;   // segments per workgroup of the segment scan (crc_combine.hip)
-constexpr u64 kCountTile = 4096;  // messages per workgroup of the tile-count scan
 constexpr u64 ceil_div(u64 a, u64 b) { return (a + b - 1) / b; }
 
 }  // namespace
@@ -394,7 +396,7 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   // batch has few messages for its tiles (config D: 256 x 8,192 tiles: 2,048 rows), up to ~8 Ki
   // waves and no more rows than tiles per message
   const u64 dx = ceil_div(count, 256), waves_x = ceil_div(count, 64);
-  const u64 dy = std::max<u64>(1, std::min<u64>({4096, ceil_div(8192, waves_x), cap / count}));
+  const u64 dy = std::max<u64>(SUBSPACE_DESC_ROWS_MIN, std::min<u64>({4096, ceil_div(8192, waves_x), cap / count}));
   crc32_ragged_desc_kernel<<<dim3((unsigned)dx, (unsigned)dy), 256, 0, st>>>(
       offsets, ostride, lengths, lstride, c->d_tbase, count, cap, reinterpret_cast<TileDesc*>(c->d_desc),
       c->d_overflow, c->d_scan_state + 1, ceil_div(n1, kCountTile), tickets, fr);
@@ -412,7 +414,7 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   // tile's zero padding and applies the final XOR
   rc = combine_tiles(c, g, c->d_tbase + count, cap, fr, st);
   if (rc) return rc;
-  crc32_ragged_final_kernel<<<(unsigned)ceil_div(count, 256), 256, 0, st>>>(
+  crc32_ragged_final_kernel<<<(unsigned)ceil_div(count, 1024), 1024, 0, st>>>(
       c->d_tbase, offsets, ostride, lengths, lstride, count, c->d_local, c->d_segx, (u32)g.nw, (u32)g.nwb,
       c->d_overflow, c->d_rops, final_xor, out, c->d_scan_state + 1 + c->scan_a_words, ceil_div(g.nseg, kScanTile),
       tickets + 1, fr);
@@ -604,6 +606,9 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
     nibble_tables(inverse(z_bytes(c->host_tab, 1ull << b)), &rops[kRagInvOps + 128 * b]);
   std::copy(rops.begin() + kRagInvOps, rops.begin() + kRagInvOps + 128 * kSmallInvOps,
             laneops.begin() + 128 * kSmallOpInv);
+  for (int k = 0; k < 3; k++)
+    for (u64 d = 1; d < 16; d++)
+      nibble_tables(inverse(z_bytes(c->host_tab, d << (4 * k))), &rops[kRagNibInvOps + 128 * (15 * k + (int)d - 1)]);
 
   hipError_t e = hipMalloc(&c->d_tab, tab.size() * 4);
   if (e == hipSuccess) e = hipMalloc(&c->d_laneops, laneops.size() * 4);

@@ -42,8 +42,8 @@ namespace subspace_amd {
 constexpr int kScanThreads = 256;
 constexpr int kScanItems = 16;
 constexpr u64 kScanTile = (u64)kScanThreads * kScanItems;  // segment scan: elements per workgroup
-constexpr int kCountItems = 16;
-constexpr u64 kCountTile = (u64)kScanThreads * kCountItems;  // tile-count scan: messages per workgroup
+constexpr int kCountItems = (int)(kCountTile / kScanThreads);
+static_assert(kCountTile % kScanThreads == 0, "tile-count scan: whole items per thread");
 constexpr u64 kFlagAggregate = 1, kFlagInclusive = 2;
 
 // Sum of u64 values below 2^62 (tile counts): flag in the top two bits.
@@ -245,20 +245,32 @@ __global__ __launch_bounds__(256) void tile_segment_scan_kernel(const u32* __res
                                                                 u32 nwb, const u64* __restrict__ total_ptr, u64 n_cap,
                                                                 u32* __restrict__ local, u32* __restrict__ segx) {
   __shared__ u32 t[64][65];
+  __shared__ u32 s2[64][64 + 4];  // the scanned block, k-major (16-B aligned rows)
   const u64 n = tiles_present(total_ptr, n_cap);
   const u32 k0 = blockIdx.x * 64u, w0 = blockIdx.y * 64u;
   if ((u64)k0 * nw + w0 >= n) return;  // every tile of the block is past the batch
   const u64 blk = ((u64)blockIdx.x * nwb + blockIdx.y) * 4096u;
   const u32 x = threadIdx.x & 63u, y0 = threadIdx.x >> 6;
+  // 16 B per lane: thread (y4, x4) loads columns 4 x4 .. +3 of rows y4 + 16 i
+  {
+    const u32 x4 = threadIdx.x & 15u, y4 = threadIdx.x >> 4;
+    u32x4 v[4];
 #pragma unroll
-  for (u32 i = 0; i < 16u; i++) {  // row w0 + y, column k0 + x
-    const u32 y = y0 + 4u * i, w = w0 + y, k = k0 + x;
-    t[y][x] = (w < nw && k < nkmax) ? in[blk + 64u * y + x] : 0u;
+    for (u32 i = 0; i < 4u; i++) v[i] = *reinterpret_cast<const u32x4*>(in + blk + 64u * (y4 + 16u * i) + 4u * x4);
+#pragma unroll
+    for (u32 i = 0; i < 4u; i++) {
+      const u32 y = y4 + 16u * i, w = w0 + y;
+#pragma unroll
+      for (u32 c = 0; c < 4u; c++) {
+        const u32 k = k0 + 4u * x4 + c;
+        t[y][4u * x4 + c] = (w < nw && k < nkmax) ? v[i][c] : 0u;
+      }
+    }
   }
   __syncthreads();
 #pragma unroll 4
   for (u32 i = 0; i < 16u; i++) {  // row k = k0 + y: tiles tau = k*nw + w0 + x
-    const u32 y = y0 + 4u * i, w = w0 + x, k = k0 + y;
+    const u32 y = y0 + 4u * i, k = k0 + y;
     u32 v = t[x][y];  // 0 past nw
     // inclusive XOR scan over the 64 lanes: DPP row shifts within each 16-lane row (source
     // lanes out of the row read as 0), then rows 1, 3 take lane 15 of rows 0, 2 and rows
@@ -269,10 +281,22 @@ __global__ __launch_bounds__(256) void tile_segment_scan_kernel(const u32* __res
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
-    const u64 tau = (u64)k * nw + w;
     if (k < nkmax) {
-      if (w < nw && tau < n) local[blk + 64u * y + x] = v;
+      s2[y][x] = v;
       if (x == 63u) segx[(u64)k * nwb + blockIdx.y] = v;
+    }
+  }
+  {
+    // the block of local[] (k-major) as 16-B stores; entries past the batch or past nw hold
+    // values no reader uses (the allocation covers whole blocks)
+    __syncthreads();
+    const u32 x4 = threadIdx.x & 15u, y4 = threadIdx.x >> 4;
+#pragma unroll
+    for (u32 i = 0; i < 4u; i++) {
+      const u32 y = y4 + 16u * i;
+      if (k0 + y < nkmax)
+        *reinterpret_cast<u32x4*>(local + blk + 64u * y + 4u * x4) =
+            u32x4{s2[y][4u * x4], s2[y][4u * x4 + 1u], s2[y][4u * x4 + 2u], s2[y][4u * x4 + 3u]};
     }
   }
 }

@@ -131,7 +131,12 @@ constexpr int kRagLdsOpWords = kRagZ64Words + 512;
 constexpr int kRagHighOps = kRagLdsOpWords;  // word offset of Z_{8192 * 2^21} in the device array
 constexpr int kNumInvOps = 13;
 constexpr int kRagInvOps = kRagHighOps + (31 - kNumTileOps) * 128;  // word offset of Z_1^{-1}
-constexpr int kRagOpWords = kRagInvOps + kNumInvOps * 128;
+// then the ragged final kernel's nibble inverses Z_{d 16^k}^{-1}, k = 0..2, d = 1..15 (slot
+// 15 k + d - 1): a padding p < 8192 is undone in at most four steps, its three low nibbles and
+// then bit 12 (Z_4096^{-1}, the last bit inverse)
+constexpr int kRagNibInvOps = kRagInvOps + kNumInvOps * 128;
+constexpr int kNumNibInvOps = 45;
+constexpr int kRagOpWords = kRagNibInvOps + kNumNibInvOps * 128;
 constexpr size_t ragged_lds_bytes() { return kLdsOps + (size_t)kRagLdsOpWords * 4u; }
 static_assert(ragged_lds_bytes() <= 160u * 1024u, "ragged kernel LDS exceeds 160 KiB");
 
@@ -175,6 +180,11 @@ struct SmallArgs {
                      // the slot's payload area); ~0 for slot lists
 };
 
+// Messages per workgroup of the tile-count scan (crc_combine.hip, 256 threads)
+#ifndef SUBSPACE_COUNT_TILE
+#define SUBSPACE_COUNT_TILE 4096
+#endif
+constexpr u64 kCountTile = SUBSPACE_COUNT_TILE;
 // 8-B tile descriptors (crc_ragged.hip TileDesc8) hold tile starts below 2^39 bytes and up to
 // 2^23 - 1 tiles after a tile; the tile-count scan flags a batch with any tile beyond that.
 constexpr u32 kDesc8StartBits = 39;

@@ -171,10 +171,13 @@ __global__ __launch_bounds__(256) void crc32_ragged_desc_kernel(const u64* __res
   if (!wide) {
     // Load-balanced expansion: the later tiles of the wave's 64 messages are numbered q = 0 ..
     // W - 1 in message order (an exclusive wave scan of b = nt - kLaneTiles); lane l of round r
-    // stores tile q = 64 (y + r gridDim.y) + l, its message found by a 6-step binary search over
-    // the 64 scan values in LDS. Every store has 64 useful lanes, and a wave takes W / 64
-    // rounds instead of one round per long message.
-    __shared__ u32 sx[4][8][64];  // per wave: excl, s16 lo, s16 hi, mis << 3, last, last_len, t0 lo, t0 hi
+    // stores tile q = 64 (y + r gridDim.y) + l. Every store has 64 useful lanes, and a wave takes
+    // W / 64 rounds instead of one round per long message. The message of lane
+    // l's q: with one row, each message starting in the round marks its first position in LDS
+    // and a max-scan over the lanes (DPP) carries the marks forward from the previous round's
+    // last message (three LDS operations a round); with more rows (config D) a 6-step binary
+    // search over the 64 scan values.
+    __shared__ u32 sx[4][9][64];  // per wave: excl, s16 lo, s16 hi, mis << 3, last, last_len, t0 lo, t0 hi, marks
     const u32 wv = threadIdx.x >> 6;
     const u32 b = nt > kLaneTiles ? (u32)nt - kLaneTiles : 0u;
     u32 incl = b;
@@ -196,12 +199,32 @@ __global__ __launch_bounds__(256) void crc32_ragged_desc_kernel(const u64* __res
     sx[wv][6][lane] = (u32)t0;
     sx[wv][7][lane] = (u32)(t0 >> 32);
     wave_lds_sync();
+    const u32 ex = incl - b;
+    u32 carry = (u32)__ffsll((unsigned long long)__ballot(b != 0u));  // (first long message) + 1
     for (u32 q0 = 64u * y; q0 < W; q0 += ystep) {
       const u32 q = q0 + lane;
-      u32 o = 0;
+      u32 o;
+      if (ystep == 64u) {
+        sx[wv][8][lane] = 0u;
+        wave_lds_sync();
+        if (b != 0u && ex >= q0 && ex < q0 + 64u) sx[wv][8][ex - q0] = lane + 1u;
+        wave_lds_sync();
+        u32 v = sx[wv][8][lane];
+        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
+        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
+        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
+        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
+        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+        v = max(v, carry);
+        carry = (u32)__builtin_amdgcn_readlane((int)v, 63);
+        o = v - 1u;
+      } else {
+        o = 0;
 #pragma unroll
-      for (u32 st = 32; st; st >>= 1)
-        if (sx[wv][0][o + st] <= q) o += st;
+        for (u32 st = 32; st; st >>= 1)
+          if (sx[wv][0][o + st] <= q) o += st;
+      }
       if (q < W) {
         const u32 j = kLaneTiles + q - sx[wv][0][o];
         const u64 t16 = (((u64)sx[wv][2][o] << 32) | sx[wv][1][o]) + ((u64)j << 9);
@@ -455,10 +478,13 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
   // set: the next call then takes 16-B descriptors, correct either way)
   if (blockIdx.x == 0 && threadIdx.x == 0) overflow[1] = 0u;
   if (scan_faulted(fault)) return;
-  // the 13 inverse operators (6.5 KiB) staged in LDS: up to 104 dependent table lookups
-  // per message read from global memory took 61 us for config C's 1 Mi messages (r01bu)
-  __shared__ u32 inv[kNumInvOps * 128];
-  for (u32 i = threadIdx.x; i < kNumInvOps * 128u; i += blockDim.x) inv[i] = gops[kRagInvOps + i];
+  // the padding inverses staged in LDS, per 1,024-message workgroup: the 45 nibble inverses
+  // and Z_4096^{-1} (23 KiB; from global memory, up to 104 dependent lookups per message took
+  // 61 us for config C, r01bu). Four steps of 8 lookups undo any padding (the 13 bit inverses:
+  // 13 steps, every one taken by some lane of a wave)
+  __shared__ u32 inv[(kNumNibInvOps + 1) * 128];
+  for (u32 i = threadIdx.x; i < kNumNibInvOps * 128u; i += blockDim.x) inv[i] = gops[kRagNibInvOps + i];
+  for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) inv[kNumNibInvOps * 128 + i] = gops[kRagInvOps + 128 * 12 + i];
   __syncthreads();
   const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = m < count;
@@ -473,16 +499,19 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
   if (!live || t1 == t0) return;  // empty message: written by the count kernel
   u32 v = ovf ? out[m] : pe ^ pb;
   const u32 pad = (u32)(0 - (lengths[m * lstride] + (offsets[m * ostride] & 15))) & 8191u;
-#pragma unroll 1
-  for (int b = 0; b < kNumInvOps; b++) {
-    if ((pad >> b) & 1u) {
-      const u32* op = inv + 128 * b;
-      u32 r = op[v & 15u];
+  auto undo = [&](u32 slot, u32 x) {
+    const u32* op = inv + 128 * slot;
+    u32 r = op[x & 15u];
 #pragma unroll
-      for (int k = 1; k < 8; k++) r ^= op[16 * k + ((v >> (4 * k)) & 15u)];
-      v = r;
-    }
+    for (int k = 1; k < 8; k++) r ^= op[16 * k + ((x >> (4 * k)) & 15u)];
+    return r;
+  };
+#pragma unroll
+  for (u32 k = 0; k < 3; k++) {
+    const u32 d = (pad >> (4 * k)) & 15u;
+    if (d) v = undo(15 * k + d - 1, v);
   }
+  if (pad & 0x1000u) v = undo(kNumNibInvOps, v);
   out[m] = v ^ final_xor;
 }
 

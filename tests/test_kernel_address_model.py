@@ -223,14 +223,28 @@ def desc_kernel_stores(ntiles, capacity, lane_tiles=2, rows=1):
         b = [max(int(ntiles[m]) - lane_tiles, 0) for m in ms] + [0] * (64 - len(ms))
         ex = list(itertools.accumulate([0] + b[:-1]))
         W = ex[63] + b[63]
+        # one row: messages starting in the round mark their first position, a max-scan over
+        # the lanes carries the marks on from the previous round's last message
+        long_lanes = [i for i in range(64) if b[i]]
         for y in range(rows):
+            carry = long_lanes[0] + 1 if long_lanes else 0
             for q0 in range(64 * y, W, 64 * rows):
+                if rows == 1:
+                    marks = [0] * 64
+                    for i in long_lanes:
+                        if q0 <= ex[i] < q0 + 64:
+                            marks[ex[i] - q0] = i + 1
+                    owners = [max(carry, *marks[:lane + 1]) - 1 for lane in range(64)]
+                    carry = owners[63] + 1
                 for lane in range(64):
                     q = q0 + lane
-                    o = 0
-                    for st in (32, 16, 8, 4, 2, 1):
-                        if ex[o + st] <= q:
-                            o += st
+                    if rows == 1:
+                        o = owners[lane]
+                    else:
+                        o = 0
+                        for st in (32, 16, 8, 4, 2, 1):
+                            if ex[o + st] <= q:
+                                o += st
                     if q < W:
                         m, j = w0 + o, lane_tiles + q - ex[o]
                         owner[int(tb[m]) + j] = (m, j)
