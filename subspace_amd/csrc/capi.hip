@@ -21,6 +21,9 @@ __global__ void crc32_uniform4k_kernel(const uint8_t*, u64, u64, const u32*, con
                                        SlotArgs);
 
 struct TileDesc;
+struct TileDesc8;
+__global__ void crc32_ragged_count_desc_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
+                                               u64*, u32*, u64, TileDesc8*, u32*, FaultRef);
 __global__ void crc32_ragged_count_scan_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
                                                u64*, u32*, u32*, FaultRef);
 __global__ void tile_segment_scan_kernel(const u32*, u32, u32, u32, const u64*, u64, u32*, u32*);
@@ -30,7 +33,7 @@ __global__ void crc32_ragged_desc_kernel(const u64*, u32, const u64*, u32, const
 template <int WG>
 __global__ void crc32_ragged_kernel(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
                                     const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds, u32*, u32*, u32,
-                                    FaultRef);
+                                    u64*, u64, u32*, FaultRef);
 __global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, const u64*, u32, u64, const u32*, const u32*,
                                           u32, u32, u32*, const u32*, u32, u32*, u64*, u64, u32*, FaultRef);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, u64, int, int, u32,
@@ -85,9 +88,6 @@ uintptr_t host_alias(uintptr_t p, uint64_t n) {
     if (p >= r.host && p - r.host <= r.bytes && n <= r.bytes - (p - r.host)) return r.dev + (p - r.host);
   return 0;
 }
-#ifndef SUBSPACE_DESC_ROWS_MIN
-#define SUBSPACE_DESC_ROWS_MIN 1  // A/B: rows of the descriptor kernel's grid at least
-#endif
 constexpr size_t kTileDescBytes = 16;  // the wide form; 8 B (TileDesc8) for most batches
 constexpr u64 kScanTile = 4096;   // segments per workgroup of the segment scan (crc_combine.hip)
 constexpr u64 ceil_div(u64 a, u64 b) { return (a + b - 1) / b; }
@@ -131,7 +131,8 @@ struct subspace_crc_ctx {
   u64 scan_a_words = 0, scan_b_words = 0;
   bool scan_dirty = false;
   u64 mem_tiles = 0;  // device memory / 8 KiB: bounds the descriptor workspace
-  u32* d_overflow = nullptr;
+  u32* d_overflow = nullptr;  // [0] overflow, [1] wide batch, [2] a tile past the fused kernel's 8-B range
+  bool fused_prep = true;     // knob "fused_prep": known-arena batches take crc32_ragged_count_desc_kernel
   int uniform_wg = 512;    // workgroup size of the uniform kernel (256/512/640/768/1024)
   int uniform_blocks = 0;  // 0 = one workgroup per CU
   int uniform_order = 0;   // tile order: 0 XCD-spread sweep, 1 per-workgroup region, 2 plain sweep, 3 XCD-grouped
@@ -374,7 +375,7 @@ int grid_for(subspace_crc_ctx* c, u64 work_units, int waves_per_block) {
 // Offsets/lengths are read with element strides (1 = plain arrays, 3 = slot records).
 // `cap` sizes the descriptor workspace; a batch with more tiles takes the search path.
 int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* offsets, u32 ostride, const u64* lengths,
-               u32 lstride, u64 count, u32 init, u32 final_xor, u32* out, hipStream_t st) {
+               u32 lstride, u64 count, u32 init, u32 final_xor, u32* out, hipStream_t st, u64 arena) {
   int rc = use_workspace(c, st);
   if (rc) return rc;
   cap = clamp_capacity(c, cap, count);
@@ -387,27 +388,41 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   c->scan_dirty = true;  // until the final kernel is launched
   const FaultRef fr = new_call_fault(c);
   u32* tickets = reinterpret_cast<u32*>(c->d_scan_state);
-  crc32_ragged_count_scan_kernel<<<(unsigned)ceil_div(n1, kCountTile), 256, 0, st>>>(
-      offsets, ostride, lengths, lstride, count, init, final_xor, c->d_tbase, out, c->zero_word, c->d_scan_state + 1,
-      reinterpret_cast<u32*>(c->d_scan_state), c->d_overflow + 1, fr);
-  c->zero_word = nullptr;
-  HIP_TRY(hipGetLastError());
-  // one thread per message; rows of workgroups share the later tiles of long messages when a
-  // batch has few messages for its tiles (config D: 256 x 8,192 tiles: 2,048 rows), up to ~8 Ki
-  // waves and no more rows than tiles per message
-  const u64 dx = ceil_div(count, 256), waves_x = ceil_div(count, 64);
-  const u64 dy = std::max<u64>(SUBSPACE_DESC_ROWS_MIN, std::min<u64>({4096, ceil_div(8192, waves_x), cap / count}));
-  crc32_ragged_desc_kernel<<<dim3((unsigned)dx, (unsigned)dy), 256, 0, st>>>(
-      offsets, ostride, lengths, lstride, c->d_tbase, count, cap, reinterpret_cast<TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_scan_state + 1, ceil_div(n1, kCountTile), tickets, fr);
-  HIP_TRY(hipGetLastError());
+  // a known arena of at most 2^37 bytes: every tile fits the 8-B descriptor (its start is below
+  // the arena's end, its message shorter than the arena), so the tile-count scan writes the
+  // descriptors itself (crc32_ragged_count_desc_kernel); a many-long-message batch (few
+  // messages per tile: config D) keeps the separate kernel, whose rows share the long messages
+  const bool fused = c->fused_prep && arena != 0 && arena <= (1ull << kDesc8StartBits) && cap / count <= 64;
+  if (fused) {
+    crc32_ragged_count_desc_kernel<<<(unsigned)ceil_div(n1, kCountTile), 1024, 0, st>>>(
+        offsets, ostride, lengths, lstride, count, init, final_xor, c->d_tbase, out, c->zero_word, c->d_scan_state + 1,
+        reinterpret_cast<u32*>(c->d_scan_state), cap, reinterpret_cast<TileDesc8*>(c->d_desc), c->d_overflow, fr);
+    c->zero_word = nullptr;
+    HIP_TRY(hipGetLastError());
+  } else {
+    crc32_ragged_count_scan_kernel<<<(unsigned)ceil_div(n1, kCountTile), 256, 0, st>>>(
+        offsets, ostride, lengths, lstride, count, init, final_xor, c->d_tbase, out, c->zero_word, c->d_scan_state + 1,
+        reinterpret_cast<u32*>(c->d_scan_state), c->d_overflow + 1, fr);
+    c->zero_word = nullptr;
+    HIP_TRY(hipGetLastError());
+    // one thread per message; rows of workgroups share the later tiles of long messages when a
+    // batch has few messages for its tiles (config D: 256 x 8,192 tiles: 2,048 rows), up to ~8 Ki
+    // waves and no more rows than tiles per message
+    const u64 dx = ceil_div(count, 256), waves_x = ceil_div(count, 64);
+    const u64 dy = std::max<u64>(1, std::min<u64>({4096, ceil_div(8192, waves_x), cap / count}));
+    crc32_ragged_desc_kernel<<<dim3((unsigned)dx, (unsigned)dy), 256, 0, st>>>(
+        offsets, ostride, lengths, lstride, c->d_tbase, count, cap, reinterpret_cast<TileDesc*>(c->d_desc),
+        c->d_overflow, c->d_scan_state + 1, ceil_div(n1, kCountTile), tickets, fr);
+    HIP_TRY(hipGetLastError());
+  }
   const int blocks = c->num_cus;  // persistent: one 8-wave workgroup per CU
   HeadSeeds seeds;  // Z_r^{-1}(init), r = 0..15: the seed of a message's first line, mis = r
   seeds.v[0] = init;
   for (int r = 1; r < 16; r++) seeds.v[r] = apply(c->zinv1, seeds.v[r - 1]);
   crc32_ragged_kernel<kRaggedWG><<<blocks, kRaggedWG, ragged_lds_bytes(), st>>>(
       base, offsets, ostride, lengths, lstride, c->d_tbase, count, reinterpret_cast<const TileDesc*>(c->d_desc),
-      c->d_overflow, c->d_tab, c->d_rops, seeds, out, c->d_tilecrc, (u32)g.nwb, fr);
+      c->d_overflow, c->d_tab, c->d_rops, seeds, out, c->d_tilecrc, (u32)g.nwb, c->d_scan_state + 1,
+      ceil_div(n1, kCountTile), tickets, fr);
   HIP_TRY(hipGetLastError());
   // padded message CRC = XOR of its tiles' values = difference of two entries of their
   // XOR prefix (only the batch's real tiles are combined); the final kernel undoes the last
@@ -740,7 +755,7 @@ int subspace_crc32_batch(subspace_crc_ctx* c, const void* dev_base, uint64_t are
   // (a message's tiles cover its extended length L + (offset & 15))
   const u64 cap = (arena_bytes + 15 * count) / 8192 + count + 1;
   return ragged_run(c, static_cast<const uint8_t*>(dev_base), cap, dev_offsets, 1, dev_lengths, 1, count, init,
-                    final_xor, dev_out, st);
+                    final_xor, dev_out, st, arena_bytes);
 }
 
 int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint64_t stride, uint64_t length,
@@ -874,7 +889,7 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
     rc = small_run(c, nullptr, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st);
   } else {
     const u64 cap = count * ((max_message_size + 15 + 8191) / 8192) + 1;
-    rc = ragged_run(c, nullptr, cap, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st);
+    rc = ragged_run(c, nullptr, cap, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st, 0);  // absolute addresses
   }
   const bool zeroed = was_zeroed(c, dev_error_count);
   if (rc) return rc;
@@ -956,7 +971,8 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
       rc = small_run(c, buf, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st);
     } else {
       const u64 cap = (slot_stride * count + 15 * count) / 8192 + count + 1;
-      rc = ragged_run(c, buf, cap, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st);
+      rc = ragged_run(c, buf, cap, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st,
+                      slot_stride * count);
     }
   } else {
     rc = subspace_crc32_batch_uniform(c, buf + prefix_size, slot_stride, message_size, count, 0u, 0u, c->d_crc0,
@@ -1236,6 +1252,8 @@ int subspace_crc32_host_slot_list(subspace_crc_ctx* c, const subspace_crc_slot* 
 //                  0 they take the ragged path
 //   "fused_slots": 1 (default) contiguous 4 KiB slot batches without metadata take the
 //                  fused slot kernel, 0 the payload kernel + crc32_slot_finish_kernel
+//   "fused_prep":  1 (default) ragged batches with a known arena of at most 2^37 bytes take the
+//                  fused tile-count scan + descriptor kernel, 0 the two kernels
 int subspace_crc_testutil_set(subspace_crc_ctx* c, const char* key, int value) {
   if (!c || !key) return SUBSPACE_CRC_EINVAL;
   CallScope scope(c);
@@ -1255,6 +1273,10 @@ int subspace_crc_testutil_set(subspace_crc_ctx* c, const char* key, int value) {
   }
   if (!std::strcmp(key, "fused_slots")) {
     c->fused_slots = value != 0;
+    return SUBSPACE_CRC_OK;
+  }
+  if (!std::strcmp(key, "fused_prep")) {  // 0: every ragged batch takes the separate descriptor kernel
+    c->fused_prep = value != 0;
     return SUBSPACE_CRC_OK;
   }
   if (!std::strcmp(key, "small_path")) {  // 0: messages <= 4 KiB take the ragged path (A/B, parity)

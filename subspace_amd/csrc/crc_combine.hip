@@ -35,7 +35,7 @@
 // by the next kernel of the call that runs after the scan (reset_scan_state, crc_device.h:
 // the descriptor kernel for the tile-count scan, the final kernels for the segment scan),
 // so every call -- and every replay of a captured hipGraph -- starts from a zeroed state.
-#include "crc_device.h"
+#include "crc_desc.h"
 
 namespace subspace_amd {
 
@@ -106,10 +106,10 @@ __device__ __forceinline__ u64 scan_ticket(u32* ticket, FaultRef fault, bool* st
 // state: it cannot happen in a correct call) ends the wait after a bound and raises
 // kFaultLookbackSpin in the context's fault word, so the call reports an error
 // (subspace_crc_ctx_check) instead of returning wrong CRCs as OK, and the GPU never hangs.
-template <class Op, int ITEMS>
+template <class Op, int ITEMS, int THREADS = kScanThreads>
 __device__ __forceinline__ void scan_tile_lookback(typename Op::T (&x)[ITEMS], u64 tile, u64* status, FaultRef fault) {
   using T = typename Op::T;
-  __shared__ T s_wave[kScanThreads / 64];
+  __shared__ T s_wave[THREADS / 64];
   __shared__ T s_prefix;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   T agg = Op::identity();
@@ -127,7 +127,7 @@ __device__ __forceinline__ void scan_tile_lookback(typename Op::T (&x)[ITEMS], u
   __syncthreads();
   T wpre = Op::identity(), total = Op::identity();
 #pragma unroll
-  for (int q = 0; q < kScanThreads / 64; q++) {
+  for (int q = 0; q < THREADS / 64; q++) {
     if (q < wid) wpre = Op::op(wpre, s_wave[q]);
     total = Op::op(total, s_wave[q]);
   }
@@ -224,6 +224,67 @@ __global__ __launch_bounds__(kScanThreads) void crc32_ragged_count_scan_kernel(
   for (int j = 0; j < kCountItems; j++) {
     const u64 i = base + (u64)(j * kScanThreads + tid);
     if (i <= count) tile_base[i] = sx[j * kScanThreads + tid];
+  }
+}
+
+// The tile-count scan and the 8-B descriptors in one kernel, for batches whose arena (the bytes
+// from the base every message lies in) is at most 2^37 bytes, so every tile fits the 8-B form
+// (crc_desc.h). 1,024 threads x 4 messages per workgroup (the same 4,096-message scan tiles as
+// crc32_ragged_count_scan_kernel, whose work this does first); after the look-back each wave
+// writes the descriptors of its 4 x 64 messages (desc8_wave), which saves the separate
+// descriptor kernel's launch, its reloads and half its latency-bound rounds.
+// A message outside the 8-B range (a caller's arena bound broken) sets overflow[2]: the main
+// kernel then locates every tile by search (correct for any batch).
+constexpr int kFusedThreads = 1024;
+constexpr int kFusedItems = (int)(kCountTile / kFusedThreads);
+static_assert(kCountTile % kFusedThreads == 0, "fused scan: whole items per thread");
+__global__ __launch_bounds__(kFusedThreads) void crc32_ragged_count_desc_kernel(
+    const u64* __restrict__ offsets, u32 ostride, const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
+    u32 final_xor, u64* __restrict__ tile_base, u32* __restrict__ out, u32* __restrict__ zero_word,
+    u64* __restrict__ status, u32* __restrict__ ticket, u64 capacity, TileDesc8* __restrict__ desc8,
+    u32* __restrict__ overflow, FaultRef fault) {
+  __shared__ u64 sx[kCountTile];
+  __shared__ u32 sw[kFusedThreads / 64][kDesc8WaveWords][64];
+  bool stale;
+  const u64 tile = scan_ticket(ticket, fault, &stale);
+  if (stale) return;
+  const u64 base = tile * kCountTile;
+  const int tid = threadIdx.x;
+  u64 so[kFusedItems], L[kFusedItems], nt[kFusedItems];
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < kFusedItems; j++) {
+    const u64 i = base + (u64)(j * kFusedThreads + tid);
+    so[j] = L[j] = nt[j] = 0;
+    if (i < count) {
+      so[j] = offsets[i * ostride];
+      L[j] = lengths[i * lstride];
+      nt[j] = msg_tiles(so[j], L[j]);
+      out[i] = nt[j] == 0 ? init ^ final_xor : 0u;
+      if (nt[j] && ((((so[j] & ~(u64)15) + ((nt[j] - 1) << 13)) >> kDesc8StartBits) | ((nt[j] - 1) >> kDesc8AfterBits)))
+        bad = true;
+    } else if (i == count && zero_word) {
+      *zero_word = 0u;  // a slot batch's mismatch count (no separate memset)
+    }
+    sx[j * kFusedThreads + tid] = nt[j];
+  }
+  if (bad) overflow[2] = 1u;
+  __syncthreads();
+  u64 x[kFusedItems];
+#pragma unroll
+  for (int j = 0; j < kFusedItems; j++) x[j] = sx[tid * kFusedItems + j];
+  scan_tile_lookback<SumOp, kFusedItems, kFusedThreads>(x, tile, status, fault);  // synchronises before returning
+#pragma unroll
+  for (int j = 0; j < kFusedItems; j++) sx[tid * kFusedItems + j] = x[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kFusedItems; j++) {
+    const u64 i = base + (u64)(j * kFusedThreads + tid);
+    const u64 tb = sx[j * kFusedThreads + tid];
+    if (i <= count) tile_base[i] = tb;
+    if (i == count) overflow[0] = tb > capacity ? 1u : 0u;
+    // the wave's 64 consecutive messages i (j fixed): their descriptors below the capacity
+    desc8_wave(desc8, capacity, tb, nt[j], so[j], L[j], 0u, 64u, sw[tid >> 6], true);
   }
 }
 

@@ -185,10 +185,18 @@ struct SmallArgs {
 #define SUBSPACE_COUNT_TILE 4096
 #endif
 constexpr u64 kCountTile = SUBSPACE_COUNT_TILE;
-// 8-B tile descriptors (crc_ragged.hip TileDesc8) hold tile starts below 2^39 bytes and up to
-// 2^23 - 1 tiles after a tile; the tile-count scan flags a batch with any tile beyond that.
-constexpr u32 kDesc8StartBits = 39;
-constexpr u32 kDesc8AfterBits = 23;
+// 8-B tile descriptors (crc_ragged.hip TileDesc8) hold tile starts below 2^37 bytes (128 GiB)
+// and up to 2^25 - 1 tiles after a tile; a batch with any tile beyond that keeps 16 B (the
+// tile-count scan flags it) or, through the fused count + descriptor kernel, is searched.
+// hi word: start bits 36.. [kD8StartHiBits), mis [4), the first-tile flag, then X (26 bits):
+// the tiles after the tile, or kLastTile8 | the last tile's bytes.
+constexpr u32 kDesc8StartBits = 37;
+constexpr u32 kDesc8AfterBits = 25;
+constexpr u32 kD8StartHiBits = kDesc8StartBits - 36;
+constexpr u32 kD8MisShift = kD8StartHiBits;
+constexpr u32 kD8FirstBit = 1u << (kD8MisShift + 4);
+constexpr u32 kD8XShift = kD8MisShift + 5;
+static_assert(kD8XShift + kDesc8AfterBits + 1 == 32, "8-B descriptor fields fill 64 bits");
 
 // Ragged kernel head seeds of one call: v[r] = Z_r^{-1}(init), r = 0..15 (a kernel argument).
 struct HeadSeeds {

@@ -38,46 +38,9 @@
 //    (Batches whose tiles overflow the workspace -- overlapping messages -- fall back to
 //    atomicXor into pre-zeroed words.)
 //  * Loads never touch a 16-B block that holds no byte of the message.
-#include "crc_device.h"
+#include "crc_desc.h"
 
 namespace subspace_amd {
-
-// 16 B per tile: one vector load and four readfirstlanes per tile in the main kernel.
-struct TileDesc {
-  u64 tile_start;  // absolute offset (from base) of the tile's first byte (16-B aligned)
-  u32 after;       // tiles after this one in the message | kFirstTile for its first tile
-  u32 len;         // bytes of the extended message in the tile (1..8192) | mis << 16
-};
-static_assert(sizeof(TileDesc) == 16, "TileDesc is 16 B");
-constexpr u32 kFirstTile = 0x80000000u;
-
-// 8 B per tile, the form every batch takes whose tile starts lie below 2^39 bytes and whose
-// messages have fewer than 2^23 + 1 tiles (the tile-count scan flags any other batch, which
-// keeps TileDesc): lo = bits 4..35 of the tile start; hi = bits 36..38 of it [2:0], mis [6:3],
-// the first-tile flag [7] and [31:8] either the tiles after this one or, for a message's last
-// tile, kLastTile8 | its bytes (only a last tile can be short; the count needs 14 bits).
-// Half the descriptor kernel's stores and the main kernel's descriptor loads.
-struct TileDesc8 {
-  u32 lo, hi;
-};
-static_assert(sizeof(TileDesc8) == 8, "TileDesc8 is 8 B");
-constexpr u32 kLastTile8 = 1u << kDesc8AfterBits;
-
-__device__ __forceinline__ TileDesc8 pack_desc8(const TileDesc& d) {
-  const u64 s16 = d.tile_start >> 4;
-  const u32 after = d.after & ~kFirstTile, len = d.len & 0xFFFFu, mis = d.len >> 16;
-  const u32 x = (after == 0u || len == 0u) ? (kLastTile8 | len) : after;  // len 0: a defensive empty tile
-  return TileDesc8{(u32)s16, ((u32)(s16 >> 32) & 7u) | (mis << 3) | ((d.after & kFirstTile) ? 0x80u : 0u) | (x << 8)};
-}
-__device__ __forceinline__ TileDesc unpack_desc8(u32 lo, u32 hi) {
-  TileDesc t;
-  t.tile_start = ((u64)(hi & 7u) << 36) | ((u64)lo << 4);
-  const u32 x = hi >> 8;
-  const bool last = (x & kLastTile8) != 0u;
-  t.after = (last ? 0u : x) | ((hi & 0x80u) ? kFirstTile : 0u);
-  t.len = (last ? (x & 0x3FFFu) : 8192u) | (((hi >> 3) & 15u) << 16);
-  return t;
-}
 
 __device__ inline u64 find_msg(const u64* __restrict__ tile_base, u64 count, u64 tau) {
   // last m with tile_base[m] <= tau (skips zero-tile messages, whose base equals the next one's)
@@ -119,15 +82,11 @@ __device__ inline TileDesc make_desc(const u64* __restrict__ offsets, u32 ostrid
 // Per tile (up to `capacity`): its descriptor, 8 B unless the tile-count scan flagged the batch
 // wide (overflow[1]). Sets overflow[0] if the batch has more tiles (then nothing is written:
 // the main kernel searches). Message-centric: thread m of column x reads its message's tile
-// range and (offset, length) with coalesced loads -- no search -- and stores the descriptors of
-// its first kLaneTiles tiles itself (neighbouring lanes hold neighbouring messages, so for small
-// messages a wave's stores are contiguous); the later tiles of a longer message are stored by
-// the whole wave, 64 per store, one message after the other, store i of a message by the
-// workgroup row y = i mod gridDim.y (the host adds rows when a batch has few, long messages:
-// config D). The 8-B form of a later tile is built incrementally from the message's first
-// (a dozen VALU ops per store: the kernel is VALU-bound). The tile-parallel form (a 64-candidate
-// shuffle search per tile from chunk hints) ran 63-72 us per config-C call.
-constexpr u32 kLaneTiles = 2;  // 1, 4, 8: slower (r04o, r04p)
+// range and (offset, length) with coalesced loads -- no search -- and the wave writes its 64
+// messages' descriptors (crc_desc.h desc8_wave; 16-B ones one long message after the other);
+// workgroup rows y share the later tiles of long messages (the host adds rows when a batch
+// has few, long messages: config D). (Batches with a known arena below 2^37 bytes take the
+// fused tile-count scan + descriptor kernel instead, crc_combine.hip.)
 __global__ __launch_bounds__(256) void crc32_ragged_desc_kernel(const u64* __restrict__ offsets, u32 ostride,
                                                                 const u64* __restrict__ lengths, u32 lstride,
                                                                 const u64* __restrict__ tile_base, u64 count,
@@ -149,7 +108,7 @@ __global__ __launch_bounds__(256) void crc32_ragged_desc_kernel(const u64* __res
     so = offsets[m * ostride];
     L = lengths[m * lstride];
   }
-  // tile j of the message at so with length tL, first tile tt0 and tnt tiles (any form)
+  // tile j of the message at so with length tL, first tile tt0 and tnt tiles (16-B form)
   auto put = [&](u64 tso, u64 tL, u64 tt0, u64 tnt, u64 j) {
     const u32 mis = (u32)(tso & 15);
     const u64 rest = tL + mis - (j << 13);
@@ -157,84 +116,19 @@ __global__ __launch_bounds__(256) void crc32_ragged_desc_kernel(const u64* __res
     d.tile_start = (tso & ~(u64)15) + (j << 13);
     d.after = (u32)(tnt - 1 - j) | (j == 0 ? kFirstTile : 0u);
     d.len = (rest < 8192 ? (u32)rest : 8192u) | (mis << 16);
-    if (wide) desc[tt0 + j] = d;
-    else desc8[tt0 + j] = pack_desc8(d);
+    desc[tt0 + j] = d;
   };
+  const u32 lane = threadIdx.x & 63u;
+  const u32 y = rfl(blockIdx.y), ystep = 64u * rfl(gridDim.y);  // in SGPRs, read once
+  if (!wide) {
+    __shared__ u32 sxa[4][kDesc8WaveWords][64];
+    desc8_wave(desc8, capacity, t0, nt, so, L, y, ystep, sxa[threadIdx.x >> 6], blockIdx.y == 0);
+    return;
+  }
   if (blockIdx.y == 0) {
 #pragma unroll
     for (u32 j = 0; j < kLaneTiles; j++)
       if (j < nt) put(so, L, t0, nt, j);
-  }
-  // longer messages: the wave stores tiles kLaneTiles.. of each, lanes along the tiles
-  const u32 lane = threadIdx.x & 63u;
-  const u32 y = rfl(blockIdx.y), ystep = 64u * rfl(gridDim.y);  // in SGPRs, read once
-  if (!wide) {
-    // Load-balanced expansion: the later tiles of the wave's 64 messages are numbered q = 0 ..
-    // W - 1 in message order (an exclusive wave scan of b = nt - kLaneTiles); lane l of round r
-    // stores tile q = 64 (y + r gridDim.y) + l. Every store has 64 useful lanes, and a wave takes
-    // W / 64 rounds instead of one round per long message. The message of lane
-    // l's q: with one row, each message starting in the round marks its first position in LDS
-    // and a max-scan over the lanes (DPP) carries the marks forward from the previous round's
-    // last message (three LDS operations a round); with more rows (config D) a 6-step binary
-    // search over the 64 scan values.
-    __shared__ u32 sx[4][9][64];  // per wave: excl, s16 lo, s16 hi, mis << 3, last, last_len, t0 lo, t0 hi, marks
-    const u32 wv = threadIdx.x >> 6;
-    const u32 b = nt > kLaneTiles ? (u32)nt - kLaneTiles : 0u;
-    u32 incl = b;
-#pragma unroll
-    for (u32 d = 1; d < 64; d <<= 1) {
-      const u32 t = (u32)__shfl_up((int)incl, d, 64);
-      if (lane >= d) incl += t;
-    }
-    const u32 W = (u32)__builtin_amdgcn_readlane((int)incl, 63);
-    if (W == 0u) return;  // wave-uniform
-    const u32 mis = (u32)(so & 15), last = (u32)nt - 1u;
-    const u64 s16 = so >> 4;
-    sx[wv][0][lane] = incl - b;
-    sx[wv][1][lane] = (u32)s16;
-    sx[wv][2][lane] = (u32)(s16 >> 32);
-    sx[wv][3][lane] = mis << 3;
-    sx[wv][4][lane] = last;
-    sx[wv][5][lane] = (u32)(L + mis - ((u64)last << 13));
-    sx[wv][6][lane] = (u32)t0;
-    sx[wv][7][lane] = (u32)(t0 >> 32);
-    wave_lds_sync();
-    const u32 ex = incl - b;
-    u32 carry = (u32)__ffsll((unsigned long long)__ballot(b != 0u));  // (first long message) + 1
-    for (u32 q0 = 64u * y; q0 < W; q0 += ystep) {
-      const u32 q = q0 + lane;
-      u32 o;
-      if (ystep == 64u) {
-        sx[wv][8][lane] = 0u;
-        wave_lds_sync();
-        if (b != 0u && ex >= q0 && ex < q0 + 64u) sx[wv][8][ex - q0] = lane + 1u;
-        wave_lds_sync();
-        u32 v = sx[wv][8][lane];
-        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
-        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
-        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
-        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
-        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
-        v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
-        v = max(v, carry);
-        carry = (u32)__builtin_amdgcn_readlane((int)v, 63);
-        o = v - 1u;
-      } else {
-        o = 0;
-#pragma unroll
-        for (u32 st = 32; st; st >>= 1)
-          if (sx[wv][0][o + st] <= q) o += st;
-      }
-      if (q < W) {
-        const u32 j = kLaneTiles + q - sx[wv][0][o];
-        const u64 t16 = (((u64)sx[wv][2][o] << 32) | sx[wv][1][o]) + ((u64)j << 9);
-        const u32 ol = sx[wv][4][o];
-        const u32 x = j == ol ? (kLastTile8 | sx[wv][5][o]) : ol - j;
-        const u64 ot0 = ((u64)sx[wv][7][o] << 32) | sx[wv][6][o];
-        desc8[ot0 + j] = TileDesc8{(u32)t16, ((u32)(t16 >> 32) & 7u) | sx[wv][3][o] | (x << 8)};
-      }
-    }
-    return;
   }
   // wide batches (16-B descriptors): one long message after the other, 64 tiles per store
   u64 big = __ballot(nt > kLaneTiles);
@@ -440,13 +334,18 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
                                                           const u32* __restrict__ overflow,
                                                           const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                           HeadSeeds seeds, u32* __restrict__ out,
-                                                          u32* __restrict__ tilecrc, u32 nwb, FaultRef fault) {
+                                                          u32* __restrict__ tilecrc, u32 nwb, u64* scan_status,
+                                                          u64 scan_words, u32* scan_ticket, FaultRef fault) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   const u32 sbase = (u32)(uintptr_t)smem;
+  // the tile-count scan's state (when the fused count + descriptor kernel ran, no other kernel
+  // of the call follows that scan)
+  reset_scan_state(scan_status, scan_words, scan_ticket);
   if (scan_faulted(fault)) return;  // workgroup-uniform, before any barrier
   // Precomputed descriptors (8 B, or 16 B for a wide batch) unless the batch had more tiles
-  // than the workspace holds (overlapping messages); then every tile is located by binary search.
-  if (overflow[0] != 0u)
+  // than the workspace holds (overlapping messages) or the fused kernel met a message past the
+  // 8-B range; then every tile is located by binary search.
+  if (overflow[0] != 0u || overflow[2] != 0u)
     ragged_body<WG, kDescSearch>(base, offsets, ostride, lengths, lstride, tile_base, count, desc, gtab, gops, seeds,
                                  out, tilecrc, nwb, sbase);
   else if (overflow[1] != 0u)
@@ -459,7 +358,7 @@ __global__ __launch_bounds__(WG) void crc32_ragged_kernel(const uint8_t* __restr
 
 template __global__ void crc32_ragged_kernel<512>(const uint8_t*, const u64*, u32, const u64*, u32, const u64*, u64,
                                                   const TileDesc*, const u32*, const u32*, const u32*, HeadSeeds,
-                                                  u32*, u32*, u32, FaultRef);
+                                                  u32*, u32*, u32, u64*, u64, u32*, FaultRef);
 
 // Per message with tiles: its padded CRC = XOR of its tiles' values = P(t1 - 1) ^ P(t0 - 1)
 // (P = inclusive XOR prefix of the tile values in tile order, crc_combine.hip), or the XOR
@@ -473,10 +372,10 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
                                           u32 final_xor, u32* __restrict__ out, u64* scan_status, u64 scan_words,
                                           u32* scan_ticket, FaultRef fault) {
   reset_scan_state(scan_status, scan_words, scan_ticket);  // the segment scan is done
-  // the wide flag (overflow[1]): set by the tile-count scan, read by the descriptor and main
-  // kernels, zero again for the next call (a call that faulted before this point leaves it
-  // set: the next call then takes 16-B descriptors, correct either way)
-  if (blockIdx.x == 0 && threadIdx.x == 0) overflow[1] = 0u;
+  // the wide flag (overflow[1], set by the tile-count scan) and the fused kernel's out-of-range
+  // flag (overflow[2]): zero again for the next call (a call that faulted before this point
+  // leaves them set: the next call then takes 16-B descriptors or the search, correct either way)
+  if (blockIdx.x == 0 && threadIdx.x == 0) overflow[1] = overflow[2] = 0u;
   if (scan_faulted(fault)) return;
   // the padding inverses staged in LDS, per 1,024-message workgroup: the 45 nibble inverses
   // and Z_4096^{-1} (23 KiB; from global memory, up to 104 dependent lookups per message took

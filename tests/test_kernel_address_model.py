@@ -542,31 +542,35 @@ def test_host_slot_list_accesses_stay_in_registered_regions(seed, count, cs, ms)
 
 
 # ------------------------------------------------------------------ 8-B tile descriptors
-K_FIRST, K_LAST8 = 0x80000000, 1 << 23
+# crc_device.h kDesc8* / kD8*: tile starts < 2^37, after < 2^25
+START_BITS, AFTER_BITS = 37, 25
+HI_START = START_BITS - 36
+MIS_SHIFT, FIRST_BIT, X_SHIFT = HI_START, 1 << (HI_START + 4), HI_START + 5
+K_FIRST, K_LAST8 = 0x80000000, 1 << AFTER_BITS
 
 
 def pack_desc8(tile_start, after, first, length, mis):
     """crc_ragged.hip pack_desc8 (TileDesc -> TileDesc8), restated."""
     s16 = tile_start >> 4
     x = (K_LAST8 | length) if (after == 0 or length == 0) else after
-    hi = ((s16 >> 32) & 7) | (mis << 3) | (0x80 if first else 0) | (x << 8)
+    hi = ((s16 >> 32) & ((1 << HI_START) - 1)) | (mis << MIS_SHIFT) | (FIRST_BIT if first else 0) | (x << X_SHIFT)
     return s16 & 0xFFFFFFFF, hi & 0xFFFFFFFF
 
 
 def unpack_desc8(lo, hi):
     """crc_ragged.hip unpack_desc8, restated: (tile_start, after | first flag, len | mis << 16)."""
-    tile_start = ((hi & 7) << 36) | (lo << 4)
-    x = hi >> 8
+    tile_start = ((hi & ((1 << HI_START) - 1)) << 36) | (lo << 4)
+    x = hi >> X_SHIFT
     last = (x & K_LAST8) != 0
-    after = (0 if last else x) | (K_FIRST if hi & 0x80 else 0)
-    length = ((x & 0x3FFF) if last else 8192) | (((hi >> 3) & 15) << 16)
+    after = (0 if last else x) | (K_FIRST if hi & FIRST_BIT else 0)
+    length = ((x & 0x3FFF) if last else 8192) | (((hi >> MIS_SHIFT) & 15) << 16)
     return tile_start, after, length
 
 
 def wide_message(s, length):
     """crc32_ragged_count_scan_kernel's flag: a tile of message (s, length) beyond the 8-B form."""
     nt = (length + (s & 15) + 8191) >> 13 if length else 0
-    return nt > 0 and ((((s & ~15) + ((nt - 1) << 13)) >> 39) != 0 or ((nt - 1) >> 23) != 0)
+    return nt > 0 and ((((s & ~15) + ((nt - 1) << 13)) >> START_BITS) != 0 or ((nt - 1) >> AFTER_BITS) != 0)
 
 
 def descs_of(s, length):
@@ -579,15 +583,15 @@ def descs_of(s, length):
 
 
 @pytest.mark.parametrize("s,length", [(0, 1), (15, 1), (3, 8189), (3, 8190), (0, 8192), (1, 8192), (7, 3 * 8192 + 5),
-                                      ((1 << 39) - 8192 - 16, 8192), ((1 << 39) - 8192 - 16 + 9, 8183),
-                                      ((1 << 38) + 17, 5 << 13), (4096, (1 << 23) << 13)])
+                                      ((1 << 37) - 8192 - 16, 8192), ((1 << 37) - 8192 - 16 + 9, 8183),
+                                      ((1 << 36) + 17, 5 << 13), (4096, (1 << 25) << 13), (0, (1 << 25) << 13)])
 def test_desc8_round_trip_or_flagged(s, length):
     """Every tile of a message that the count scan does not flag round-trips through the 8-B
     form exactly; a flagged message is one whose tiles would not."""
     if wide_message(s, length):
         nt = (length + (s & 15) + 8191) >> 13
         last_start = (s & ~15) + ((nt - 1) << 13)
-        assert last_start >= 1 << 39 or nt - 1 >= 1 << 23
+        assert last_start >= 1 << START_BITS or nt - 1 >= 1 << AFTER_BITS
         return
     n = 0
     for tile_start, after, first, nbytes, mis in descs_of(s, length):
@@ -605,13 +609,15 @@ def test_desc8_round_trip_or_flagged(s, length):
 
 
 def test_desc8_flag_edges():
-    # the last tile start 2^39 - 16 fits; 2^39 does not
-    assert not wide_message((1 << 39) - 16, 1)
-    assert wide_message(1 << 39, 1)
-    assert wide_message((1 << 39) - 8192, 8193)  # second tile starts at 2^39
-    # 2^23 tiles: after up to 2^23 - 1 fits
-    assert not wide_message(0, (1 << 23) << 13)
-    assert wide_message(0, ((1 << 23) << 13) + 1)
+    # the last tile start 2^37 - 16 fits; 2^37 does not
+    assert not wide_message((1 << 37) - 16, 1)
+    assert wide_message(1 << 37, 1)
+    assert wide_message((1 << 37) - 8192, 8193)  # second tile starts at 2^37
+    # 2^25 tiles: after up to 2^25 - 1 fits (a message of 2^25 tiles starting at 0 ends at 2^38:
+    # its last tile start is past 2^37, so that one is flagged by the start)
+    assert wide_message(0, (1 << 25) << 13)
+    assert not wide_message(0, (1 << 24) << 13)
+    assert wide_message(0, ((1 << 25) << 13) + 1)
     assert not wide_message(0, 0)
 
 
@@ -623,10 +629,10 @@ def desc8_incremental(so, length, j):
     last_len = length + mis - (last << 13)
     t16 = (so >> 4) + (j << 9)
     x = (K_LAST8 | last_len) if j == last else last - j
-    return t16 & 0xFFFFFFFF, ((t16 >> 32) & 7) | (mis << 3) | (x << 8)
+    return t16 & 0xFFFFFFFF, ((t16 >> 32) & ((1 << HI_START) - 1)) | (mis << MIS_SHIFT) | (x << X_SHIFT)
 
 
-@pytest.mark.parametrize("so,length", [(0, 3 * 8192), (5, 3 * 8192), (4095, 100000), ((1 << 39) - (40 << 13) + 3, 30 << 13),
+@pytest.mark.parametrize("so,length", [(0, 3 * 8192), (5, 3 * 8192), (4095, 100000), ((1 << 37) - (40 << 13) + 3, 30 << 13),
                                        ((1 << 36) - 8192 * 2 - 1, 9 * 8192 + 1), (1 << 32, (1 << 20) + 7)])
 def test_desc8_incremental_matches_pack(so, length):
     assert not wide_message(so, length)

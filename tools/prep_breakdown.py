@@ -21,7 +21,7 @@ def main(path):
         if "subspace_amd" not in name:
             continue
         short = name.split("(")[0].replace("void ", "").replace("subspace_amd::", "")
-        if "count_scan" in name or "crc32_long_kernel" in name:
+        if "count_scan" in name or "count_desc" in name or "crc32_long_kernel" in name:
             cur = collections.OrderedDict()
             calls.append(cur)
         if cur is not None:
