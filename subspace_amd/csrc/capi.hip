@@ -88,8 +88,10 @@ uintptr_t host_alias(uintptr_t p, uint64_t n) {
     if (p >= r.host && p - r.host <= r.bytes && n <= r.bytes - (p - r.host)) return r.dev + (p - r.host);
   return 0;
 }
+#ifndef SUBSPACE_FINAL_BLOCKS_PER_CU
+#define SUBSPACE_FINAL_BLOCKS_PER_CU 2  // ragged final kernel: a persistent grid (0: one workgroup per 1,024 messages)
+#endif
 constexpr size_t kTileDescBytes = 16;  // the wide form; 8 B (TileDesc8) for most batches
-constexpr u64 kScanTile = 4096;   // segments per workgroup of the segment scan (crc_combine.hip)
 constexpr u64 ceil_div(u64 a, u64 b) { return (a + b - 1) / b; }
 
 }  // namespace
@@ -429,7 +431,9 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   // tile's zero padding and applies the final XOR
   rc = combine_tiles(c, g, c->d_tbase + count, cap, fr, st);
   if (rc) return rc;
-  crc32_ragged_final_kernel<<<(unsigned)ceil_div(count, 1024), 1024, 0, st>>>(
+  const u64 fb = SUBSPACE_FINAL_BLOCKS_PER_CU ? std::min<u64>(ceil_div(count, 1024), (u64)SUBSPACE_FINAL_BLOCKS_PER_CU * c->num_cus)
+                                              : ceil_div(count, 1024);
+  crc32_ragged_final_kernel<<<(unsigned)fb, 1024, 0, st>>>(
       c->d_tbase, offsets, ostride, lengths, lstride, count, c->d_local, c->d_segx, (u32)g.nw, (u32)g.nwb,
       c->d_overflow, c->d_rops, final_xor, out, c->d_scan_state + 1 + c->scan_a_words, ceil_div(g.nseg, kScanTile),
       tickets + 1, fr);

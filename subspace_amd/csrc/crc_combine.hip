@@ -40,8 +40,8 @@
 namespace subspace_amd {
 
 constexpr int kScanThreads = 256;
-constexpr int kScanItems = 16;
-constexpr u64 kScanTile = (u64)kScanThreads * kScanItems;  // segment scan: elements per workgroup
+constexpr int kScanItems = (int)(kScanTile / kScanThreads);  // segment-prefix scan: elements per thread
+static_assert(kScanTile % kScanThreads == 0, "segment-prefix scan: whole items per thread");
 constexpr int kCountItems = (int)(kCountTile / kScanThreads);
 static_assert(kCountTile % kScanThreads == 0, "tile-count scan: whole items per thread");
 constexpr u64 kFlagAggregate = 1, kFlagInclusive = 2;

@@ -180,6 +180,11 @@ struct SmallArgs {
                      // the slot's payload area); ~0 for slot lists
 };
 
+// Segments per workgroup of the segment-prefix look-back scan (crc_combine.hip, 256 threads)
+#ifndef SUBSPACE_SCAN_TILE
+#define SUBSPACE_SCAN_TILE 2048
+#endif
+constexpr u64 kScanTile = SUBSPACE_SCAN_TILE;
 // Messages per workgroup of the tile-count scan (crc_combine.hip, 256 threads)
 #ifndef SUBSPACE_COUNT_TILE
 #define SUBSPACE_COUNT_TILE 4096

@@ -385,19 +385,6 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
   for (u32 i = threadIdx.x; i < kNumNibInvOps * 128u; i += blockDim.x) inv[i] = gops[kRagNibInvOps + i];
   for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) inv[kNumNibInvOps * 128 + i] = gops[kRagInvOps + 128 * 12 + i];
   __syncthreads();
-  const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = m < count;
-  const u64 t0 = live ? tile_base[m] : 0, t1 = live ? tile_base[m + 1] : 0;
-  const bool ovf = *overflow != 0u;
-  // P(t1 - 1) of every message (empty ones included), and P(t0 - 1) = the previous message's
-  // P(t1 - 1) from the neighbouring lane: one prefix gather per message instead of two (lane 0
-  // gathers its own)
-  const u32 pe = (!ovf && live && t1) ? tile_prefix(local, segx, nw, nwb, t1 - 1) : 0u;
-  u32 pb = (u32)__shfl_up((int)pe, 1, 64);
-  if ((threadIdx.x & 63u) == 0u) pb = (!ovf && live && t0) ? tile_prefix(local, segx, nw, nwb, t0 - 1) : 0u;
-  if (!live || t1 == t0) return;  // empty message: written by the count kernel
-  u32 v = ovf ? out[m] : pe ^ pb;
-  const u32 pad = (u32)(0 - (lengths[m * lstride] + (offsets[m * ostride] & 15))) & 8191u;
   auto undo = [&](u32 slot, u32 x) {
     const u32* op = inv + 128 * slot;
     u32 r = op[x & 15u];
@@ -405,13 +392,33 @@ __global__ void crc32_ragged_final_kernel(const u64* __restrict__ tile_base, con
     for (int k = 1; k < 8; k++) r ^= op[16 * k + ((x >> (4 * k)) & 15u)];
     return r;
   };
+  const bool ovf = *overflow != 0u;
+  // grid-stride over the messages (the host sizes the grid: SUBSPACE_FINAL_BLOCKS_PER_CU)
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 m0 = (u64)blockIdx.x * blockDim.x; m0 < count; m0 += stride) {
+    const u64 m = m0 + threadIdx.x;
+    const bool live = m < count;
+    // every load of the message at once: its tile range, length and start
+    const u64 t0 = live ? tile_base[m] : 0, t1 = live ? tile_base[m + 1] : 0;
+    const u64 Lm = live ? lengths[m * lstride] : 0, sm = live ? offsets[m * ostride] : 0;
+    // P(t1 - 1) of every message (empty ones included), and P(t0 - 1) = the previous message's
+    // P(t1 - 1) from the neighbouring lane: one prefix gather per message instead of two (lane 0
+    // gathers its own)
+    const u32 pe = (!ovf && live && t1) ? tile_prefix(local, segx, nw, nwb, t1 - 1) : 0u;
+    u32 pb = (u32)__shfl_up((int)pe, 1, 64);
+    if ((threadIdx.x & 63u) == 0u) pb = (!ovf && live && t0) ? tile_prefix(local, segx, nw, nwb, t0 - 1) : 0u;
+    if (live && t1 != t0) {  // (an empty message's result was written by the count kernel)
+      u32 v = ovf ? out[m] : pe ^ pb;
+      const u32 pad = (u32)(0 - (Lm + (sm & 15))) & 8191u;
 #pragma unroll
-  for (u32 k = 0; k < 3; k++) {
-    const u32 d = (pad >> (4 * k)) & 15u;
-    if (d) v = undo(15 * k + d - 1, v);
+      for (u32 k = 0; k < 3; k++) {
+        const u32 d = (pad >> (4 * k)) & 15u;
+        if (d) v = undo(15 * k + d - 1, v);
+      }
+      if (pad & 0x1000u) v = undo(kNumNibInvOps, v);
+      out[m] = v ^ final_xor;
+    }
   }
-  if (pad & 0x1000u) v = undo(kNumNibInvOps, v);
-  out[m] = v ^ final_xor;
 }
 
 }  // namespace subspace_amd
