@@ -96,8 +96,10 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* ctx, const void* dev_base, ui
                                  uint64_t count, uint32_t init, uint32_t flags, uint32_t* dev_out, void* stream);
 
 /* Ragged batch: message i is the dev_lengths[i] bytes at dev_base + dev_offsets[i].
- * arena_bytes = bytes readable from dev_base (every message must lie inside it).
- * dev_offsets / dev_lengths are device arrays of `count` uint64. */
+ * arena_bytes = bytes readable from dev_base (every message must lie inside it). It sizes the
+ * tile workspace and, up to 2^37 bytes, selects the one-kernel tile-count scan + 8-byte tile
+ * descriptors; a message found outside it still gets its correct CRC (the kernel then locates
+ * every tile by search, slower). dev_offsets / dev_lengths are device arrays of `count` uint64. */
 int subspace_crc32_batch(subspace_crc_ctx* ctx, const void* dev_base, uint64_t arena_bytes,
                          const uint64_t* dev_offsets, const uint64_t* dev_lengths, uint64_t count, uint32_t init,
                          uint32_t flags, uint32_t* dev_out, void* stream);
