@@ -503,29 +503,38 @@ def launch_rate_steady(blocks, window_s=1.0, tol=0.003):
     return per(newer) >= per(older) * (1.0 - tol)
 
 
+def settle_steps(step, sync, settle, warmup, settle_s, block=50, cap_s=None):
+    """Untimed settle launches before a timed region: at least `settle` - `warmup` of them and
+    at least `settle_s` seconds of them, and, up to SETTLE_CAP_S, until the launch rate is
+    steady (launch_rate_steady: the mean time per launch of the last 0.5 s within 0.3 % of the
+    0.5 s before). VRAM freed to the driver (by this or an earlier process, e.g. a test run's
+    118 GB config-C buffer) is wiped in the background for several seconds, and every HBM-bound
+    kernel runs 2-4 % slower meanwhile (profiles/DESIGN_r01-r03.md 6, tools/s_launches.py,
+    r03s4-r03s6). `step(i)` launches one step, `sync()` waits for it; the clock is read after
+    every `block` back-to-back launches. The headline, the N > 1 solo leg and the CPU dry run's
+    solo leg all settle by this rule. Returns (launches run, seconds spent)."""
+    n, t0 = 0, time.perf_counter()
+    cap = SETTLE_CAP_S if cap_s is None else cap_s
+    blocks = []  # (seconds, launches) per block of back-to-back launches
+    while (n < max(0, settle - warmup) or time.perf_counter() - t0 < settle_s or
+           (settle_s > 0 and not launch_rate_steady(blocks) and time.perf_counter() - t0 < cap)):
+        t_blk = time.perf_counter()
+        for _ in range(block):
+            step(n)
+            n += 1
+        sync()
+        blocks.append((time.perf_counter() - t_blk, block))
+    return n, time.perf_counter() - t0
+
+
 def run_timed(wl, steps, warmup, settle, streams, world, dist, event_every=0, region_marks=None, settle_s=0.0):
-    """W untimed warm-up steps (after settle launches: at least `settle` - W of them and at
-    least `settle_s` seconds of them), then EXACTLY `steps` steps between barrier +
-    synchronize on both sides. Returns (max-over-ranks seconds, HIP-event span of the region
-    / steps in ms, sampled per-launch ms or None, settle launches run, this rank's own
-    seconds)."""
+    """W untimed warm-up steps (after the settle launches of settle_steps), then EXACTLY
+    `steps` steps between barrier + synchronize on both sides. Returns (max-over-ranks seconds,
+    HIP-event span of the region / steps in ms, sampled per-launch ms or None, settle launches
+    run, this rank's own seconds)."""
     import torch
     stream = streams[0]
-    n_settle, t_settle = 0, time.perf_counter()
-    # ... and, up to SETTLE_CAP_S, until the launch rate is steady: the mean time per launch of
-    # the last 0.5 s within 0.3 % of the 0.5 s before. VRAM freed to the driver (by this or an
-    # earlier process, e.g. a test run's 118 GB config-C buffer) is wiped in the background for
-    # several seconds, and every HBM-bound kernel runs 2-4 % slower meanwhile (profiles/DESIGN_r01-r03.md 6,
-    # tools/s_launches.py, r03s4-r03s6)
-    blocks = []  # (seconds, launches) per block of back-to-back launches
-    while (n_settle < max(0, settle - warmup) or time.perf_counter() - t_settle < settle_s or
-           (settle_s > 0 and not launch_rate_steady(blocks) and time.perf_counter() - t_settle < SETTLE_CAP_S)):
-        t_blk = time.perf_counter()
-        for _ in range(50):  # back to back; the clock is read with a sync every 50 launches
-            wl.step(n_settle, streams)
-            n_settle += 1
-        torch.cuda.synchronize()
-        blocks.append((time.perf_counter() - t_blk, 50))
+    n_settle, _ = settle_steps(lambda i: wl.step(i, streams), torch.cuda.synchronize, settle, warmup, settle_s)
     for i in range(warmup):
         wl.step(i, streams)
     torch.cuda.synchronize()
@@ -683,6 +692,24 @@ def secondary_configs(ctx, dev, names, iters) -> dict:
     return res
 
 
+def slot_leg_check(mode, buf, n, stride, ps, size, cs, ms_, status, errs, rng):
+    """A slot leg's bit-exactness: a publish (CALCULATE) leaves 64 sampled slots of `buf` with the
+    flag set and the host drop-in's CalculateCRC32Checksum<3> over GetMessageChecksumData
+    (include/subspace/checksum.h; the channel's prefixes start without valid checksums); a
+    verify passes every slot. Returns (ok, what was checked)."""
+    from subspace_amd import checksum, gpu
+    if mode == gpu.SLOT_VERIFY:
+        return int(errs.item()) == 0 and bool((status == 0).all().item()), "verify passes every slot"
+    chan = buf.cpu().numpy()
+    ok = True
+    for k in rng.choice(n, 64, replace=False):
+        pre = chan[k * stride:k * stride + ps]
+        pay = chan[k * stride + ps:k * stride + ps + size]
+        want = checksum.calculate_crc32_checksum(checksum.get_message_checksum_data(pre, pay, size, cs, ms_))
+        ok = ok and bytes(pre[48:52]) == want and bool(pre[32] & 4)
+    return ok, "64 sampled slots hold the flag and the host drop-in's CalculateCRC32Checksum<3>"
+
+
 def slot_configs(ctx, dev, iters) -> dict:
     """Config S: config B in the reference's slot layout on the device (65,536 slots of
     PrefixSize 64 + 4 KiB payload, stride 4,160, 4 rotated channel buffers), the full 3-span
@@ -712,38 +739,64 @@ def slot_configs(ctx, dev, iters) -> dict:
                                     status=status if mode == gpu.SLOT_VERIFY else None,
                                     error_count=errs if mode == gpu.SLOT_VERIFY else None)
         ms = time_calls(call, 400)
-        ok = None
-        if mode == gpu.SLOT_VERIFY:
-            torch.cuda.synchronize()
-            ok = int(errs.item()) == 0 and bool((status == 0).all().item())
+        torch.cuda.synchronize()
+        ok, check = slot_leg_check(mode, bufs[0], n, stride, ps, size, cs, ms_, status, errs, rng)
+        res[key] = config_line(nbytes, ms, ok, "subspace_crc32_slots_strided", {
+            "workload": "S: 65,536 slots (prefix 64 B + 4 KiB payload, stride 4,160), 3-span checksum, " +
+                        ("publish: flag + checksum stored" if mode == gpu.SLOT_CALCULATE else
+                         "verify: per-slot status + mismatch count"),
+            "check": check})
+    # S_list: the same channels drained as device slot lists in shuffled order (a subscriber's
+    # read order over several wrap-arounds), one list per channel copy, rotated like S (round 4
+    # timed one copy only: 273 MB, most of it served from the 256 MB MALL -- 51.0 against 66.7
+    # us per call for the round-4 kernel, r05a): subspace_crc32_slots, publish (flag + checksum
+    # of every slot cleared on the device first, so the sampled check sees this leg's stores)
+    # then verify
+    order = rng.permutation(n).astype(np.uint64)
+
+    def list_recs(b):
+        b0 = np.uint64(b.data_ptr())
+        r = np.stack([b0 + order * np.uint64(stride), b0 + order * np.uint64(stride) + np.uint64(ps),
+                      np.full(n, size, dtype=np.uint64)], axis=1)
+        return torch.from_numpy(np.ascontiguousarray(r).view(np.int64)).to(dev)
+
+    d_recs = [list_recs(b) for b in bufs]
+    for b in bufs:
+        pre = b.view(n, stride)
+        pre[:, 48:52].zero_()                # the stored checksum
+        pre[:, 32].bitwise_and_(0xFB)        # kMessageHasChecksum (flags, offset 32)
+    torch.cuda.synchronize()
+    list_kernel = "subspace_crc32_slots: subspace_amd::crc32_small_kernel<512, true> (one launch, slots finished in it; " \
+                  "crc_small.hip)"
+    for mode, key in ((gpu.SLOT_CALCULATE, "S_list_publish"), (gpu.SLOT_VERIFY, "S_list_verify")):
+        i = [0]
+        errs.zero_()
+
+        def call():
+            r = d_recs[i[0] % nbuf]
+            i[0] += 1
+            ctx.crc32_slots(r, max_message_size=size, checksum_size=cs, metadata_size=ms_, mode=mode, status=status,
+                            error_count=errs if mode == gpu.SLOT_VERIFY else None)
+        ms = time_calls(call, 400)
+        torch.cuda.synchronize()
+        if mode == gpu.SLOT_CALCULATE:
+            ok = bool((status == 0).all().item())
             chan = bufs[0].cpu().numpy()
             for k in rng.choice(n, 64, replace=False):
                 pre = chan[k * stride:k * stride + ps]
                 pay = chan[k * stride + ps:k * stride + ps + size]
                 want = checksum.calculate_crc32_checksum(checksum.get_message_checksum_data(pre, pay, size, cs, ms_))
-                ok = ok and bytes(pre[48:52]) == want
-        res[key] = config_line(nbytes, ms, ok, "subspace_crc32_slots_strided", {
-            "workload": "S: 65,536 slots (prefix 64 B + 4 KiB payload, stride 4,160), 3-span checksum, " +
-                        ("publish: flag + checksum stored" if mode == gpu.SLOT_CALCULATE else
-                         "verify: per-slot status + mismatch count"),
-            "check": "verify passes all slots and 64 sampled stored checksums equal the host drop-in's"})
-    # S_list: the same channel drained as a device slot list in shuffled order (a subscriber's
-    # read order over several wrap-arounds): subspace_crc32_slots, verify
-    order = rng.permutation(n).astype(np.uint64)
-    base0 = np.uint64(bufs[0].data_ptr())
-    recs = np.stack([base0 + order * np.uint64(stride), base0 + order * np.uint64(stride) + np.uint64(ps),
-                     np.full(n, size, dtype=np.uint64)], axis=1)
-    d_recs = torch.from_numpy(np.ascontiguousarray(recs).view(np.int64)).to(dev)
-    errs.zero_()
-    ms = time_calls(lambda: ctx.crc32_slots(d_recs, max_message_size=size, checksum_size=cs, metadata_size=ms_,
-                                            mode=gpu.SLOT_VERIFY, status=status, error_count=errs), 50)
-    torch.cuda.synchronize()
-    ok = int(errs.item()) == 0 and bool((status == 0).all().item())
-    res["S_list_verify"] = config_line(nbytes, ms, ok, "subspace_crc32_slots: subspace_amd::crc32_small_kernel<512, "
-                                      "true> (one launch, slots finished in it; crc_small.hip)", {
-        "workload": "S_list: config S's 65,536 slots as a device slot list (subspace_crc_slot records) in "
-                    "shuffled order, verify",
-        "check": "every slot passes"})
+                ok = ok and bytes(pre[48:52]) == want and bool(pre[32] & 4)
+            check = "64 sampled slots of copy 0 (flag + checksum cleared before the leg) hold the host drop-in's " \
+                    "CalculateCRC32Checksum<3> and the flag"
+        else:
+            ok = int(errs.item()) == 0 and bool((status == 0).all().item())
+            check = "every slot passes"
+        res[key] = config_line(nbytes, ms, ok, list_kernel, {
+            "workload": "S_list: config S's 65,536 slots as device slot lists (subspace_crc_slot records) in shuffled "
+                        "order, one per channel copy, 4 copies rotated, " +
+                        ("publish" if mode == gpu.SLOT_CALCULATE else "verify"),
+            "check": check})
     del bufs, d_recs
     # S_meta: 16 B of user metadata per slot (SetMetadataSize, client/options.h:375-391):
     # ComputePrefixSize(4, 16) = 128, stride 4,224; spans 44 + 16 + 4,096 B
@@ -765,20 +818,12 @@ def slot_configs(ctx, dev, iters) -> dict:
                                     error_count=errs if mode == gpu.SLOT_VERIFY else None)
         errs.zero_()
         ms = time_calls(call, 200)
-        ok = None
-        if mode == gpu.SLOT_VERIFY:
-            torch.cuda.synchronize()
-            ok = int(errs.item()) == 0 and bool((status == 0).all().item())
-            chan = bufs[0].cpu().numpy()
-            for k in rng.choice(n, 64, replace=False):
-                pre = chan[k * stride:k * stride + ps]
-                pay = chan[k * stride + ps:k * stride + ps + size]
-                want = checksum.calculate_crc32_checksum(checksum.get_message_checksum_data(pre, pay, size, cs, ms_))
-                ok = ok and bytes(pre[48:52]) == want
+        torch.cuda.synchronize()
+        ok, check = slot_leg_check(mode, bufs[0], n, stride, ps, size, cs, ms_, status, errs, rng)
         res[key] = config_line(nbytes, ms, ok, "subspace_crc32_slots_strided", {
             "workload": "S_meta: 65,536 slots (prefix 128 B with 16 B metadata + 4 KiB payload, stride 4,224), "
                         "3-span checksum, " + ("publish" if mode == gpu.SLOT_CALCULATE else "verify"),
-            "check": "verify passes all slots and 64 sampled stored checksums equal the host drop-in's"})
+            "check": check})
     del bufs
     return res
 
@@ -837,6 +882,40 @@ def dry_run_cpu(args, world, rank) -> int:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # N > 1: rank 0 alone over the whole workload (the N = 1 configuration), settled by the
+    # headline's rule (settle_steps; on the CPU at most 2 s of it), for the efficiency -- the
+    # GPU run's solo leg, rehearsed
+    solo = None
+    if world > 1 and not args.no_solo:
+        dist.barrier()
+        if rank == 0:
+            if wl == "E":
+                alld = synth.host_uniform(GOLD["B"]["seed"], np.arange(count, dtype=np.uint64), MSG_BYTES)
+                allm = [alld[j] for j in range(count)]
+            elif wl == "C":
+                offs1, arena1 = synth.packed_offsets(lengths, 64)
+                alld = synth.host_ragged(synth.SEED_C, np.arange(count), lengths, offs1, arena1)
+                allm = [alld[int(o):int(o) + int(n)] for o, n in zip(offs1, lengths)]
+            else:
+                allm = msgs
+            all_out = np.zeros(len(allm), dtype=np.uint32)
+
+            def solo_step(_i):
+                for j, m in enumerate(allm):
+                    all_out[j] = checksum.subspace_crc32(0xFFFFFFFF, m)
+
+            settle_s = min(args.settle_s, 2.0) if args.settle > 0 else 0.0
+            n1, t1 = settle_steps(solo_step, lambda: None, min(args.settle, 2), 0, settle_s, block=1,
+                                  cap_s=2 * settle_s)
+            ts = time.perf_counter()
+            for i in range(args.steps):
+                solo_step(i)
+            el1 = time.perf_counter() - ts
+            sb = sum(int(m.nbytes) for m in allm)
+            solo = {"value": round(sb * args.steps / el1 / 2**30, 3), "steps": args.steps,
+                    "settle_launches": n1, "settle_s": round(t1, 3),
+                    "bitexact_vs_golden": digest(all_out) == GOLD[key]["sha256_le_u32"] if wl != "B" else None}
+        dist.barrier()
     tl = torch.from_numpy(local[:len(msgs)].view(np.int32).copy())
     tg = time.perf_counter()
     # the same gather helpers as the GPU run (here on CPU tensors over gloo)
@@ -872,6 +951,8 @@ def dry_run_cpu(args, world, rank) -> int:
             "rank_step_ms": {"min": min(r["step_ms"] for r in everyone), "max": max(r["step_ms"] for r in everyone)},
             "rccl_world": dist.get_world_size() if world > 1 else 1,
             "backend": dist.get_backend() if world > 1 else None,
+            "single_gpu": solo,
+            "efficiency": round(value / (world * solo["value"]), 4) if solo else None,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -966,10 +1047,16 @@ def main():
                 one = Workload(args.workload, ctx, dev, 1, 0)
                 torch.cuda.synchronize()
                 solo_steps = max(1, min(args.steps, 200 if args.workload == "B" else 20))
-                el1, avg1, _, _, _ = run_timed(one, solo_steps, min(args.warmup, 3), 0, [stream], 1, None)
+                # the headline's settle rule: the buffers were just allocated
+                # and filled, and the N-rank region's frees may still be wiped in the background
+                el1, avg1, _, n1, _ = run_timed(one, solo_steps, min(args.warmup, 3), args.settle, [stream], 1, None,
+                                                settle_s=args.settle_s if args.settle > 0 else 0.0)
                 ok1, _ = one.check(None)
                 solo = {"value": round(one.total_bytes * solo_steps / el1 / 2**30, 2), "steps": solo_steps,
                         "ms_per_step": round(el1 / solo_steps * 1e3, 4), "bitexact_vs_golden": ok1,
+                        "settle_launches": max(0, n1 - min(args.warmup, 3)),
+                        "settle_rule": f">= {args.settle} launches and >= {args.settle_s if args.settle > 0 else 0} s, "
+                                       "then a steady launch rate (the headline's)",
                         "what": f"workload {args.workload} at N = 1 (the whole batch) on rank 0's GPU, timed after "
                                 "the N-rank region while the other ranks wait"}
                 one.free()

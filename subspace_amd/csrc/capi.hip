@@ -38,12 +38,12 @@ __global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, const u64
                                           u32, u32, u32*, const u32*, u32, u32*, u64*, u64, u32*, FaultRef);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, u64, int, int, u32,
                                          const u32*, const u32*, const u32*, u32*, u32*, u32*);
-__global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*);
+__global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*, const u64*, u64, u64*);
 __global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* offsets, u64* lengths);
 template <int WG>
 __global__ void crc32_long_kernel(const uint8_t*, u64, u32, u32, const u32*, const u32*, u32, u32, u32*, u32);
 __global__ void crc32_long_final_kernel(const u32*, const u32*, u32, u32, u32, u32, u32*, u64*, u64, u32*);
-template <int WG, bool SLOT>
+template <int WG, bool SLOT, bool PROBE>
 __global__ void crc32_small_kernel(const u32*, const u32*, SmallArgs);
 
 }  // namespace subspace_amd
@@ -166,6 +166,7 @@ struct subspace_crc_ctx {
   u64 l_capacity = 0;
   u32* d_crc0 = nullptr;  // slot batches: payload CRCs from init 0
   u64* d_soff = nullptr;  // slot batches: payload offsets of the contiguous layout
+  u64* d_slen = nullptr;  // strided slots with per-slot sizes: the sizes, an oversize one as 0
   u64 s_capacity = 0;
   // fused slot kernel: a ring of counter words, (workgroups done << 32) | mismatches, each 0
   // between calls (the last workgroup resets its word); consecutive calls take consecutive
@@ -249,14 +250,23 @@ int fault_status(subspace_crc_ctx* c, hipStream_t st) {
   HIP_TRY(hipMemcpyAsync(&f, c->d_fault, sizeof(u32), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (f == 0) return SUBSPACE_CRC_OK;
-  // (rare path) a fused slot kernel of this context may still run on another stream, and it
-  // owns a counter word and may raise more bits: let every stream finish before the reset
-  // (ADVICE r03), then report everything raised
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(&f, c->d_fault, sizeof(u32), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemset(c->d_fault, 0, 2 * sizeof(u32)));
-  HIP_TRY(hipMemset(c->d_slot_counter, 0, kSlotCounters * sizeof(u64)));
-  HIP_TRY(hipDeviceSynchronize());
+  if (f & kFaultSlotRing) {
+    // (rarest path) a fused slot kernel gave up on its ring: its counter word may be left
+    // non-zero, and fused slot kernels of this context on other streams (they record nothing)
+    // may still hold the others -- let every stream finish before the counters are reset
+    // (ADVICE r03), then report everything raised
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(&f, c->d_fault, sizeof(u32), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(c->d_slot_counter, 0, kSlotCounters * sizeof(u64)));
+    HIP_TRY(hipDeviceSynchronize());
+  }
+  // a scan fault: the scan kernels of this context run on the workspace stream, which st
+  // follows (use_workspace) -- the reset is ordered on st, no device-wide synchronisation (a
+  // hipDeviceSynchronize would stall other contexts' streams and break another thread's
+  // global-mode graph capture). A bit raised by a kernel still running elsewhere
+  // is reported by the next check.
+  HIP_TRY(hipMemsetAsync(c->d_fault, 0, 2 * sizeof(u32), st));
+  HIP_TRY(hipStreamSynchronize(st));
   c->scan_dirty = true;
   return fail(SUBSPACE_CRC_EFAULT, "device fault 0x%x: %s; the results of the calls since the last check are not valid",
               f, fault_text(f));
@@ -474,6 +484,7 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
   a.out = out;
   a.rops = c->d_rops;
   a.pow2 = c->d_pow2;
+  a.probe = c->probe;
   // one workgroup per CU, or more, so that no wave gets more than one ring window of tiles
   // (the kernel's in-loop flush then never runs: crc_small.hip)
   const u64 tiles = (count + 1) / 2;
@@ -492,11 +503,14 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
     a.crc_out = slot->crc_out;
     a.error_count = slot->error_count;
     a.counter = c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters);
-    crc32_small_kernel<512, true><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
+    if (c->probe)  // experiment hook: the timestamp-recording instantiation (tools/small_timeline.py)
+      crc32_small_kernel<512, true, true><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
+    else
+      crc32_small_kernel<512, true, false><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
   } else {
     a.zero_word = c->zero_word;
     c->zero_word = nullptr;
-    crc32_small_kernel<512, false><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
+    crc32_small_kernel<512, false, false><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
   }
   HIP_TRY(hipGetLastError());
   return SUBSPACE_CRC_OK;
@@ -513,11 +527,14 @@ int ensure_slot_ws(subspace_crc_ctx* c, u64 count) {
   if (count <= c->s_capacity) return SUBSPACE_CRC_OK;
   (void)hipFree(c->d_crc0);
   (void)hipFree(c->d_soff);
+  (void)hipFree(c->d_slen);
   c->d_crc0 = nullptr;
   c->d_soff = nullptr;
+  c->d_slen = nullptr;
   c->s_capacity = 0;
   HIP_TRY(hipMalloc(&c->d_crc0, count * sizeof(u32)));
   HIP_TRY(hipMalloc(&c->d_soff, count * sizeof(u64)));
+  HIP_TRY(hipMalloc(&c->d_slen, count * sizeof(u64)));
   c->s_capacity = count;
   return SUBSPACE_CRC_OK;
 }
@@ -666,10 +683,13 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
     e = hipFuncSetAttribute((const void*)crc32_long_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)ragged_lds_bytes());
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)small_lds_bytes() + 16);
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)small_lds_bytes() + 16);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)small_lds_bytes() + 16);
   if (e != hipSuccess) {
     subspace_crc_ctx_destroy(c);
@@ -706,6 +726,7 @@ void subspace_crc_ctx_destroy(subspace_crc_ctx* c) {
   (void)hipFree(c->d_laneops);
   (void)hipFree(c->d_crc0);
   (void)hipFree(c->d_soff);
+  (void)hipFree(c->d_slen);
   (void)hipFree(c->d_tbase);
   (void)hipFree(c->d_desc);
   (void)hipFree(c->d_tilecrc);
@@ -959,8 +980,12 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
   if (rc) return rc;
   want_zeroed(c, dev_error_count);
   if (dev_message_sizes) {
-    slot_payload_offsets_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(slot_stride, prefix_size, count,
-                                                                                c->d_soff);
+    // payload offsets, and the sizes with every one beyond the slot's payload area as 0: the
+    // payload kernels read nothing of an oversize slot (its bytes would run into the next slot
+    // or past the buffer), slot_finish labels it from the raw sizes
+    const u64 area = count > 1 ? slot_stride - prefix_size : ~0ull;
+    slot_payload_offsets_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(
+        slot_stride, prefix_size, count, c->d_soff, dev_message_sizes, area, c->d_slen);
     HIP_TRY(hipGetLastError());
     const bool aligned = slot_stride % 16 == 0 && ((uintptr_t)(buf + prefix_size) % 16) == 0;
     if (count > 1 && small_fits(slot_stride - prefix_size, aligned) && c->small_path) {
@@ -972,10 +997,10 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
                            dev_status, dev_crc_out, dev_error_count};
         return small_run(c, buf, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, nullptr, st, &ss);
       }
-      rc = small_run(c, buf, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st);
+      rc = small_run(c, buf, c->d_soff, 1, c->d_slen, 1, count, 0u, 0u, c->d_crc0, st);
     } else {
       const u64 cap = (slot_stride * count + 15 * count) / 8192 + count + 1;
-      rc = ragged_run(c, buf, cap, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, c->d_crc0, st,
+      rc = ragged_run(c, buf, cap, c->d_soff, 1, c->d_slen, 1, count, 0u, 0u, c->d_crc0, st,
                       slot_stride * count);
     }
   } else {

@@ -90,9 +90,20 @@ __device__ __forceinline__ typename Op::T shfl_xor_t(typename Op::T v, int m) {
 // beyond the grid means the counter was not zero at launch (stale state, or a call racing
 // another on the context's workspace): kFaultTicket is raised and the caller leaves at once
 // (its status word would lie past the scan's words), workgroup-uniformly.
-__device__ __forceinline__ u64 scan_ticket(u32* ticket, FaultRef fault, bool* stale) {
+// first_scan (the tile-count scan, a ragged call's first kernel): the workgroup holding ticket
+// 0 clears the fault mark word[1] when it holds this call's generation -- left by an earlier
+// replay of the same captured hipGraph (its generation is a kernel argument), whose fault must
+// not make every later replay skip its work. No scan of this call can have marked
+// it yet: with a stale counter no workgroup holds ticket 0, and a look-back wait gives up only
+// after kSpinBound polls, long after ticket 0's workgroup started.
+__device__ __forceinline__ u64 scan_ticket(u32* ticket, FaultRef fault, bool* stale, bool first_scan = false) {
   __shared__ u32 s_tile;
-  if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+  if (threadIdx.x == 0) {
+    s_tile = atomicAdd(ticket, 1u);
+    if (first_scan && s_tile == 0 && fault.word &&
+        __hip_atomic_load(fault.word + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fault.gen)
+      __hip_atomic_store(fault.word + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __syncthreads();
   const u64 t = s_tile;
   *stale = t >= gridDim.x;
@@ -192,7 +203,7 @@ __global__ __launch_bounds__(kScanThreads) void crc32_ragged_count_scan_kernel(
     u64* __restrict__ status, u32* __restrict__ ticket, u32* __restrict__ wide, FaultRef fault) {
   __shared__ u64 sx[kCountTile];  // striped (coalesced) global order <-> per-thread runs
   bool stale;
-  const u64 tile = scan_ticket(ticket, fault, &stale);
+  const u64 tile = scan_ticket(ticket, fault, &stale, true);
   if (stale) return;
   const u64 base = tile * kCountTile;
   const int tid = threadIdx.x;
@@ -246,7 +257,7 @@ __global__ __launch_bounds__(kFusedThreads) void crc32_ragged_count_desc_kernel(
   __shared__ u64 sx[kCountTile];
   __shared__ u32 sw[kFusedThreads / 64][kDesc8WaveWords][64];
   bool stale;
-  const u64 tile = scan_ticket(ticket, fault, &stale);
+  const u64 tile = scan_ticket(ticket, fault, &stale, true);
   if (stale) return;
   const u64 base = tile * kCountTile;
   const int tid = threadIdx.x;

@@ -178,6 +178,8 @@ struct SmallArgs {
   const u32* pow2;   // SLOT: Z_{2^k}, k < 64 (a long message's Z_L)
   u64 max_len;       // SLOT: a larger message size is SUBSPACE_CRC_SLOT_OVERSIZE (strided layouts:
                      // the slot's payload area); ~0 for slot lists
+  u64* probe;        // experiment hook (subspace_crc_testutil_probe), else null: kProbeWords realtime
+                     // stamps per wave, stored at exit (tools/small_timeline.py)
 };
 
 // Segments per workgroup of the segment-prefix look-back scan (crc_combine.hip, 256 threads)

@@ -21,8 +21,9 @@
 //    before the final XOR.
 //  * Waves stream the global tile list in sweep order (tau = k*nw + w), one tile of
 //    loads in flight ahead. Per-tile 8-B descriptors (tile start, tiles after, first-tile
-//    flag, bytes in the last tile and mis; 16 B for batches beyond 2^39 bytes or with messages
-//    of 2^23 tiles and more) are precomputed by crc32_ragged_desc_kernel.
+//    flag, bytes in the last tile and mis; 16 B for batches with a tile start at or beyond 2^37
+//    bytes or with 2^25 tiles after a tile: kDesc8StartBits / kDesc8AfterBits, crc_device.h) are
+//    precomputed by crc32_ragged_desc_kernel (or the fused count + descriptor kernel).
 //  * Per tile, lane l of half h applies its own line-shift operator Z_{128*(31-l)} (the
 //    uniform kernel's conflict-free [nibble][value][lane] tables) and a DPP reduction
 //    leaves the two half-tile values in lanes 31 and 63. They are parked, one tile per

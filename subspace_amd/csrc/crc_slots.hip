@@ -103,10 +103,16 @@ __global__ __launch_bounds__(kSlotWG) void crc32_slot_finish_kernel(
   }
 }
 
-// Payload offsets of the contiguous layout (relative to the first prefix).
-__global__ void slot_payload_offsets_kernel(u64 stride, u64 prefix_size, u64 count, u64* __restrict__ offsets) {
+// Payload offsets of the contiguous layout (relative to the first prefix), and the per-slot
+// sizes the payload kernels read: a size beyond the slot's payload area (max_len) as 0, so no
+// kernel reads an oversize slot's bytes (crc32_slot_finish_kernel labels it OVERSIZE).
+__global__ void slot_payload_offsets_kernel(u64 stride, u64 prefix_size, u64 count, u64* __restrict__ offsets,
+                                            const u64* __restrict__ sizes, u64 max_len, u64* __restrict__ clamped) {
   const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count) offsets[i] = i * stride + prefix_size;
+  if (i >= count) return;
+  offsets[i] = i * stride + prefix_size;
+  const u64 L = sizes[i];
+  clamped[i] = L > max_len ? 0 : L;
 }
 
 }  // namespace subspace_amd

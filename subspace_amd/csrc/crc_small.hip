@@ -54,15 +54,27 @@
 //    (the fused uniform slot kernel's scheme: no fences, no memset).
 #include "crc_device.h"
 
+// Timing-only investigation builds (tools/ab_lib.sh -DSUBSPACE_SMALL_VARIANT=n; the product is
+// 0, the others compute nothing valid): 1 no prologue span loads / hash; 2 no flush; 3 tile 0's
+// loads in the FAST form when the wave is FAST.
+#ifndef SUBSPACE_SMALL_VARIANT
+#define SUBSPACE_SMALL_VARIANT 0
+#endif
+
 namespace subspace_amd {
 
-template <int WG, bool SLOT>
+template <int WG, bool SLOT, bool PROBE>
 __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                          SmallArgs a) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   constexpr int NPW = WG / 64;
   const u32 sbase = (u32)(uintptr_t)smem;
   const u32 smism = sbase + (u32)small_lds_bytes();  // SLOT: the workgroup's mismatch word
+  // experiment hook: realtime stamps (entry, window records landed, barrier, tile 0 landed,
+  // loop end, flush end, exit), stored at exit by lanes 0-7 (no store inside the stream)
+  u64 pt[7] = {0, 0, 0, 0, 0, 0, 0};
+  constexpr bool probe = PROBE;
+  if constexpr (probe) pt[0] = __builtin_amdgcn_s_memrealtime();
   LdsFill<WG, kSmallOpSlots> fill;
   fill.load(gtab, gops);
 
@@ -84,6 +96,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
 
   // this lane's message in tile k (present: k < nk and m < count)
   auto msg_of = [&](u32 k) __attribute__((always_inline)) { return 2 * (t0 + (u64)k * nw) + (u64)h; };
+  // Lane i's message of the first window (tile i / 2, half i & 1): the flush's message, and the
+  // record lane i holds for the tile loop (clamped into the batch like every record load)
+  const u64 fm = 2 * (t0 + (u64)((u32)lane >> 1) * nw) + ((u32)lane & 1u);
+  const bool flive = ((u32)lane >> 1) < nk && fm < count;
+  const u64 fmc = fm < count ? fm : count - 1;
   // The record of this lane's half in tile k, clamped into the batch (every record load reads
   // a real record; whether the half holds a message is decided from k and m when used).
   auto fetch = [&](u32 k, u64& s, u64& L) __attribute__((always_inline)) {
@@ -92,6 +109,22 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     m = m < count ? m : count - 1;
     s = a.offsets[m * a.ostride];
     L = a.lengths[m * a.lstride];
+  };
+  // The window's records, loaded once in the prologue (lane i: message i of the first window),
+  // and tile k's record for this lane's half broadcast from them (k < 32; clamped as fetch's)
+  u64 wS = 0, wL = 0;
+  auto readlane64 = [&](u64 v, int i) __attribute__((always_inline)) {
+    return ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), i) << 32) |
+           (u64)(u32)__builtin_amdgcn_readlane((int)(u32)v, i);
+  };
+  auto win_rec = [&](u32 k, u64& s, u64& L) __attribute__((always_inline)) {
+    u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
+    kk = kk < kSmallRingTiles ? kk : kSmallRingTiles - 1u;
+    const int i0 = (int)(2u * kk);
+    const u64 s0 = readlane64(wS, i0), s1 = readlane64(wS, i0 + 1);
+    const u64 L0 = readlane64(wL, i0), L1 = readlane64(wL, i0 + 1);
+    s = h ? s1 : s0;
+    L = h ? L1 : L0;
   };
   // Extended bytes this kernel reads for tile k's half as a half-tile (0: nothing -- no
   // message, an empty one, or one longer than a half-tile, computed apart: long_crc).
@@ -109,6 +142,21 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       D[b] = *reinterpret_cast<const u32x4*>(p0 + (off < lastb ? off : lastb));
     }
     // keep the loads at this point, in order (hipcc otherwise sinks them into the compute)
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // FAST path: the tile's line offset from base, computed (and pinned) before the wait for
+  // the previous tile, then 8 loads at immediate offsets (the uniform kernel's issue)
+  auto fast_off = [&](u32 k) __attribute__((always_inline)) {
+    u64 s, L;
+    win_rec(k, s, L);
+    u64 off = s + 128u * l;
+    asm volatile("" : "+v"(off));
+    return off;
+  };
+  auto load_at = [&](u32x4 (&D)[8], u64 off) __attribute__((always_inline)) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(base + off);
+#pragma unroll
+    for (int b = 0; b < 8; b++) D[b] = q[b];
     __builtin_amdgcn_sched_barrier(0);
   };
   // Z_{2^b}^{-1} applied for the set bits of `bits` (b < nb <= 12; wave-uniform loop over the
@@ -148,6 +196,10 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   };
   auto span_hash = [&](u32 (&w)[14], const u32 (&W1)[kW], u32& F, u32& S, bool& has) __attribute__((always_inline))
       -> u32 {
+    // w[0] (the padding) and w[13] (not hashed) stay live until here: hipcc reuses a dead
+    // destination of a pending prefix load for other values, and the reuse waits for that load
+    // (r05: a vmcnt wait that put the prefix round trip in front of tile 0's lines)
+    asm volatile("" ::"v"(w[0]), "v"(w[13]));
     has = (w[8] & 4u) != 0u;  // kMessageHasChecksum (common/channel.h:62-70)
     F = calc ? (w[8] | 4u) : w[8];
     w[8] = F;
@@ -290,10 +342,21 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     // lane 31 of each half: its message's value and code, one 8-B LDS store
     if (l == 31u) lds_st64(sring + 8u * (2u * (k & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
   };
-  // SLOT: lane i's message of the first window (tile i / 2, half i & 1): its record's prefix
-  // offset, and (after the barrier) the prefix terms, from words loaded in the prologue
-  const u64 fm = 2 * (t0 + (u64)((u32)lane >> 1) * nw) + ((u32)lane & 1u);
-  const bool flive = ((u32)lane >> 1) < nk && fm < count;
+  // FAST: a whole 16-B-aligned 4 KiB message per half (mis = 0, no padding: code 0); line 0 from
+  // init itself
+  auto process_fast = [&](const u32x4 (&cur)[8], u32 k) __attribute__((always_inline)) {
+    const u32 crc = line_crc32_2chain(cur, l == 0u ? a.init : 0u, lc0, lc1, z64);
+    u32 v = lane_shift(lop, crc);
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    const u32 code = (k < nk && msg_of(k) < count) ? 0u : kCodeSkip;
+    if (l == 31u) lds_st64(sring + 8u * (2u * (k & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
+  };
+  // SLOT: lane i's message of the first window (fm): its record's prefix offset, and (after
+  // the barrier) the prefix terms, from words loaded in the prologue
   u64 fpre = 0;
   u32 eF = 0, eS = 0, eH = 0;
   bool ehas = false;
@@ -345,58 +408,104 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   };
   constexpr u32 kWinMask = kSmallRingTiles - 1u;
 
-  // Prologue: table loads, tile 0's and 1's records, tile 0's lines, then the LDS stores and
-  // the barrier (tile 0's latency hides behind the fill).
+  // Prologue: table loads, the window's records (and SLOT its prefix offsets); the LDS fill while
+  // the records are in flight; then the first window's prefix words and tile 0's lines, the
+  // barrier (tile 0's latency hides behind it), and the span terms hashed under tile 0's flight.
+  wS = a.offsets[fmc * a.ostride];
+  wL = a.lengths[fmc * a.lstride];
+  if constexpr (SLOT) fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
+  fill.store(sbase);
+  if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
+  // FAST (wave-uniform): the window is every tile of the wave (at most 32: small_run's grid) and
+  // each of its messages is a whole 4 KiB payload on a 16-B boundary (SLOT: within max_len) --
+  // the fixed-size channel drain. Its loop is the uniform kernel's: the next tile's address from
+  // the window's records before the wait, one address and 8 loads at immediate offsets, no
+  // clamps, codes or records in the loop. (Measured on config S's channel, r05c: the general
+  // loop's 8 clamped per-block addresses read the same bytes ~50 % slower than one address with
+  // immediate offsets -- 67.5 against 44.1 us per 65,536 slots in the read probe, testutil.hip
+  // slot_list_read_kernel modes 2 and 3 -- and its address and code arithmetic made the kernel
+  // compute-bound, 6,759 VALU instructions per wave against the uniform kernel's 4,508.)
+  const bool conf = !flive || (wL == (u64)kSmallMaxExt && (wS & 15u) == 0 && (!SLOT || wL <= a.max_len));
+  const bool fast = nk <= kSmallRingTiles && __ballot(!conf) == 0;
+  if constexpr (probe) pt[1] = __builtin_amdgcn_s_memrealtime();
   u64 sA, LA, sB, LB;
-  fetch(0, sA, LA);
-  fetch(1, sB, LB);
+  win_rec(0, sA, LA);
+  win_rec(1, sB, LB);
   u32 pwords[14], pmeta[kW];
   if constexpr (SLOT) {
-    fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
-    span_load(flive ? base + fpre - a.pdelta : safe, pwords, pmeta);
+    if (SUBSPACE_SMALL_VARIANT != 1) span_load(flive ? base + fpre - a.pdelta : safe, pwords, pmeta);
     __builtin_amdgcn_sched_barrier(0);
   }
   u32x4 A[8], B[8];
   u64 sc = sA, Lc = LA;
-  load_lines(A, sc, ext(0, sc, Lc));
-  fill.store(sbase);
-  if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
+  if (SUBSPACE_SMALL_VARIANT == 3 && fast)
+    load_at(A, fast_off(0));
+  else
+    load_lines(A, sc, ext(0, sc, Lc));  // (FAST: the same addresses as load_at's)
   __syncthreads();
-  if constexpr (SLOT) eH = span_hash(pwords, pmeta, eF, eS, ehas);
+  if constexpr (probe) pt[2] = __builtin_amdgcn_s_memrealtime();
+  if constexpr (SLOT && SUBSPACE_SMALL_VARIANT != 1) eH = span_hash(pwords, pmeta, eF, eS, ehas);
 
-  // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines; the
-  // ring is finished whenever it holds 32 tiles, right after the next tile's loads are issued
-  // (so the stores retire during that tile's compute), and at the end (crc_ragged.hip's loop,
-  // without descriptors). Nothing else lives across the loop (register-parked
-  // values, 64-tile windows and a flush only after the loop each measured slower).
   u32 k = 0;
-  for (; k + 1 < nk; k += 2) {
-    issue_prio_hi();       // (crc_device.h)
-    drain_before_issue();  // tile k's lines and tile k+1's record
-    const u64 s1 = sB, L1 = LB;
-    fetch(k + 2, sA, LA);
-    load_lines(B, s1, ext(k + 1, s1, L1));
-    issue_prio_lo();
-    if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
-    process(A, sc, Lc, k);
-    issue_prio_hi();
-    drain_before_issue();
-    const u64 s2 = sA, L2 = LA;
-    fetch(k + 3, sB, LB);
-    load_lines(A, s2, ext(k + 2, s2, L2));
-    issue_prio_lo();
-    process(B, s1, L1, k + 1);
-    sc = s2;
-    Lc = L2;
-  }
-  if (k < nk) {
-    drain_before_issue();
-    if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
-    process(A, sc, Lc, k);
-  }
-  if (nk) {
-    const u32 kf = (nk - 1u) & ~kWinMask;  // the last window, not flushed yet
-    flush(kf, nk - kf);
+  if (fast) {
+    // ping-pong, unrolled by two, one tile in flight (crc_uniform.hip's loop)
+    for (; k + 1 < nk; k += 2) {
+      const u64 qB = fast_off(k + 1);
+      issue_prio_hi();
+      drain_before_issue();  // tile k's lines
+      load_at(B, qB);
+      issue_prio_lo();
+      process_fast(A, k);
+      const u64 qA = fast_off(k + 2);
+      issue_prio_hi();
+      drain_before_issue();
+      load_at(A, qA);
+      issue_prio_lo();
+      process_fast(B, k + 1);
+    }
+    if (k < nk) {
+      drain_before_issue();
+      process_fast(A, k);
+    }
+    if constexpr (probe) pt[4] = __builtin_amdgcn_s_memrealtime();
+    if (nk && SUBSPACE_SMALL_VARIANT != 2) flush(0, nk);
+    if constexpr (probe) pt[5] = __builtin_amdgcn_s_memrealtime();
+  } else {
+    // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines; the
+    // ring is finished whenever it holds 32 tiles, right after the next tile's loads are issued
+    // (so the stores retire during that tile's compute), and at the end (crc_ragged.hip's loop,
+    // without descriptors). Nothing else lives across the loop (register-parked
+    // values, 64-tile windows and a flush only after the loop each measured slower).
+    for (; k + 1 < nk; k += 2) {
+      issue_prio_hi();       // (crc_device.h)
+      drain_before_issue();  // tile k's lines and tile k+1's record
+      const u64 s1 = sB, L1 = LB;
+      fetch(k + 2, sA, LA);
+      load_lines(B, s1, ext(k + 1, s1, L1));
+      issue_prio_lo();
+      if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
+      process(A, sc, Lc, k);
+      issue_prio_hi();
+      drain_before_issue();
+      const u64 s2 = sA, L2 = LA;
+      fetch(k + 3, sB, LB);
+      load_lines(A, s2, ext(k + 2, s2, L2));
+      issue_prio_lo();
+      process(B, s1, L1, k + 1);
+      sc = s2;
+      Lc = L2;
+    }
+    if (k < nk) {
+      drain_before_issue();
+      if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
+      process(A, sc, Lc, k);
+    }
+    if constexpr (probe) pt[4] = __builtin_amdgcn_s_memrealtime();
+    if (nk) {
+      const u32 kf = (nk - 1u) & ~kWinMask;  // the last window, not flushed yet
+      flush(kf, nk - kf);
+    }
+    if constexpr (probe) pt[5] = __builtin_amdgcn_s_memrealtime();
   }
   if constexpr (SLOT) {
     if (a.error_count && lane == 0) {
@@ -423,9 +532,19 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     // a word the caller's next kernel accumulates into (a slot batch's mismatch count)
     if (a.zero_word != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.zero_word = 0u;
   }
+  if constexpr (probe) {
+    pt[6] = __builtin_amdgcn_s_memrealtime();
+    u64* r = a.probe + ((u64)blockIdx.x * NPW + wid) * kProbeWords;
+    const u64 xcc = (u64)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    const u64 v = lane == 0 ? pt[0] : lane == 1 ? pt[1] : lane == 2 ? pt[2] : lane == 3 ? pt[3]
+                : lane == 4 ? pt[4] : lane == 5 ? pt[5] : lane == 6 ? pt[6]
+                : (xcc | ((u64)nk << 32) | ((u64)fast << 48));
+    if (lane < kProbeWords) r[lane] = v;
+  }
 }
 
-template __global__ void crc32_small_kernel<512, false>(const u32*, const u32*, SmallArgs);
-template __global__ void crc32_small_kernel<512, true>(const u32*, const u32*, SmallArgs);
+template __global__ void crc32_small_kernel<512, false, false>(const u32*, const u32*, SmallArgs);
+template __global__ void crc32_small_kernel<512, true, false>(const u32*, const u32*, SmallArgs);
+template __global__ void crc32_small_kernel<512, true, true>(const u32*, const u32*, SmallArgs);
 
 }  // namespace subspace_amd

@@ -85,9 +85,160 @@ __global__ __launch_bounds__(512) void stream_read_lds_kernel(const u32x4* __res
   out[blockIdx.x * 512 + threadIdx.x] = acc;
 }
 
+// Slot-list read probe (S_list): the small-message kernel's access shape over a
+// device slot list (subspace_crc_slot records {prefix, payload, size}) with the CRC replaced by
+// an XOR fold -- the same grid rule (small_run: no wave gets more than 32 tiles), sweep front and
+// tile (lane l of half h reads line l of slot 2 tau + h), one tile in flight per wave, and the
+// first window's prefix words (56 B of each slot's MessagePrefix, one slot per lane) loaded in
+// the prologue after tile 0's lines. MODE (what differs, for the read ceiling and its causes):
+//   0  each tile's two records loaded one tile ahead, 8 clamped block addresses per lane
+//      (crc_small.hip's general loop)
+//   1  the wave's records in registers from the prologue, 8 clamped addresses
+//   2  no records: slot m's payload at recs[0].payload + m * stride, 8 clamped addresses
+//   3  as 2, one address and 8 immediate offsets (crc_uniform.hip's load issue)
+//   4  the window's records in registers, one address and 8 immediate offsets (crc_small.hip's
+//      FAST loop)
+template <int MODE>
+__global__ __launch_bounds__(512) void slot_list_read_kernel(const uint64_t* __restrict__ recs, uint64_t count,
+                                                             uint64_t stride, unsigned* __restrict__ out) {
+  using namespace subspace_amd;
+  extern __shared__ unsigned lds_unused2[];
+  const int lane = threadIdx.x & 63;
+  const u32 wid = rfl(threadIdx.x >> 6);
+  const u32 l = (u32)lane & 31u, h = (u32)lane >> 5;
+  const u64 ntiles = (count + 1) >> 1;
+  const u64 nw = (u64)gridDim.x * 8;
+  const u64 t0 = front_slot(blockIdx.x, gridDim.x, wid);
+  u32 nk = t0 < ntiles ? (u32)((ntiles - t0 + nw - 1) / nw) : 0u;
+  if (nk > 32u) nk = 32u;  // (the host's grid gives no wave more)
+  const u64 fm = 2 * (t0 + (u64)((u32)lane >> 1) * nw) + ((u32)lane & 1u);
+  const u64 fmc = fm < count ? fm : count - 1;
+  u64 wS = 0, wL = 0;
+  if (MODE == 1 || MODE == 4) {
+    wS = recs[3 * fmc + 1];
+    wL = recs[3 * fmc + 2];
+  }
+  const u64 s00 = recs[1];
+  const u64 fpre = recs[3 * fmc];
+  auto fetch = [&](u32 k, u64& s, u64& L) {
+    const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
+    if (MODE == 1 || MODE == 4) {
+      const int i0 = (int)(2u * kk);
+      const u64 s0 = ((u64)(u32)__builtin_amdgcn_readlane((int)(wS >> 32), i0) << 32) |
+                     (u64)(u32)__builtin_amdgcn_readlane((int)(u32)wS, i0);
+      const u64 s1 = ((u64)(u32)__builtin_amdgcn_readlane((int)(wS >> 32), i0 + 1) << 32) |
+                     (u64)(u32)__builtin_amdgcn_readlane((int)(u32)wS, i0 + 1);
+      const u32 L0 = (u32)__builtin_amdgcn_readlane((int)(u32)wL, i0);
+      const u32 L1 = (u32)__builtin_amdgcn_readlane((int)(u32)wL, i0 + 1);
+      s = h ? s1 : s0;
+      L = h ? L1 : L0;
+    } else {
+      u64 m = nk ? 2 * (t0 + (u64)kk * nw) + h : 0;
+      m = m < count ? m : count - 1;
+      if (MODE == 0) {
+        s = recs[3 * m + 1];
+        L = recs[3 * m + 2];
+      } else {
+        s = s00 + m * stride;
+        L = 4096;
+      }
+    }
+  };
+  // (global-address-space pointers: addresses built from integers are generic, and generic
+  // loads compile to flat loads, which the kernels' loads are not)
+  using gptr = const __attribute__((address_space(1))) u32x4*;
+  auto load_lines = [&](u32x4 (&D)[8], u64 s, u64 L) {
+    if (MODE >= 3) {
+      const gptr q = (gptr)(s + 128u * l);
+#pragma unroll
+      for (int b = 0; b < 8; b++) D[b] = q[b];
+    } else {
+      u64 E = L + (s & 15u);
+      E = E < 16 ? 16 : (E > 4096 ? 4096 : E);
+      const u64 p0 = s & ~(u64)15;
+      const u32 lastb = ((u32)E - 1u) & ~15u;
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const u32 off = 128u * l + 16u * (u32)b;
+        D[b] = *(gptr)(p0 + (off < lastb ? off : lastb));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  unsigned acc = 0;
+  auto fold = [&](const u32x4 (&D)[8]) {
+#pragma unroll
+    for (int b = 0; b < 8; b++) acc ^= D[b].x ^ D[b].y ^ D[b].z ^ D[b].w;
+  };
+  u64 sA, LA, sB, LB;
+  fetch(0, sA, LA);
+  fetch(1, sB, LB);
+  u32x4 A[8], B[8];
+  load_lines(A, sA, LA);
+  {
+    const __attribute__((address_space(1))) uint64_t* q = (const __attribute__((address_space(1))) uint64_t*)fpre;
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 7; i++) x ^= q[i];
+    acc ^= (unsigned)x ^ (unsigned)(x >> 32);
+  }
+  u32 k = 0;
+  for (; k + 1 < nk; k += 2) {
+    subspace_amd::drain_before_issue();
+    const u64 s1 = sB, L1 = LB;
+    fetch(k + 2, sA, LA);
+    load_lines(B, s1, L1);
+    fold(A);
+    subspace_amd::drain_before_issue();
+    const u64 s2 = sA, L2 = LA;
+    fetch(k + 3, sB, LB);
+    load_lines(A, s2, L2);
+    fold(B);
+  }
+  if (k < nk) {
+    subspace_amd::drain_before_issue();
+    fold(A);
+  }
+  if (acc == 0x12345678u && count == 1) lds_unused2[threadIdx.x] = acc;  // (keeps the allocation)
+  out[blockIdx.x * 512 + threadIdx.x] = acc;
+}
+
 }  // namespace
 
 extern "C" {
+
+// The slot-list read probe over `count` device records (MODE above; stride: modes 2 and 3's
+// channel stride; lds: allocate the small-message kernel's dynamic LDS, as it runs); dev_out holds
+// out_words >= grid * 512 words, grid = the small-message kernel's for this count on this device.
+int subspace_crc_testutil_slot_list_read(const void* dev_records, uint64_t count, uint32_t mode, uint64_t stride,
+                                         uint32_t lds, unsigned* dev_out, uint64_t out_words, void* stream) {
+  if (!dev_records || !dev_out || count == 0 || mode > 4) return -1;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -2;
+  const uint64_t tiles = (count + 1) / 2;
+  uint64_t grid = (tiles + 7) / 8;
+  if (grid > (uint64_t)cus) grid = (uint64_t)cus;
+  const uint64_t need = (tiles + 8 * 32 - 1) / (8 * 32);
+  if (grid < need) grid = need;
+  if (grid < 1) grid = 1;
+  if (out_words < grid * 512) return -1;
+  const auto* r = static_cast<const uint64_t*>(dev_records);
+  const size_t ldsb = lds ? subspace_amd::small_lds_bytes() + 16 : 0;
+  const void* fns[5] = {(const void*)slot_list_read_kernel<0>, (const void*)slot_list_read_kernel<1>,
+                        (const void*)slot_list_read_kernel<2>, (const void*)slot_list_read_kernel<3>,
+                        (const void*)slot_list_read_kernel<4>};
+  if (hipFuncSetAttribute(fns[mode], hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsb) != hipSuccess) return -2;
+  const hipStream_t st = (hipStream_t)stream;
+  switch (mode) {
+    case 0: slot_list_read_kernel<0><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
+    case 1: slot_list_read_kernel<1><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
+    case 2: slot_list_read_kernel<2><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
+    case 3: slot_list_read_kernel<3><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
+    default: slot_list_read_kernel<4><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 
 // bytes must be a multiple of 8 KiB; out holds 256 * 512 words.
 int subspace_crc_testutil_stream_read(const void* dev_base, uint64_t bytes, unsigned* dev_out, void* stream) {

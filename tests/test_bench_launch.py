@@ -31,11 +31,19 @@ def last_json(stdout: str) -> dict:
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("world,workload", [(2, "E"), (2, "C"), (3, "C")])
+@pytest.mark.parametrize("world,workload", [(2, "E"), (2, "C"), (3, "C"), (8, "E"), (8, "C")])
 def test_dry_run_spawns_ranks_and_matches_fixture(world, workload):
-    r = run_bench("--gpus", str(world), "--dry-run-cpu", "--workload", workload, "--steps", "2", "--warmup", "1")
+    """Worlds 2, 3 and the driver's 8. Rank 0's solo leg (the N = 1
+    configuration, the efficiency's denominator) settles by the headline's rule
+    (bench.settle_steps) before it is timed, and is bit-exact too."""
+    r = run_bench("--gpus", str(world), "--dry-run-cpu", "--workload", workload, "--steps", "2", "--warmup", "1",
+                  "--settle", "2", "--settle-s", "0.3")
     assert r.returncode == 0, r.stderr[-3000:]
     line = last_json(r.stdout)
+    solo = line["single_gpu"]
+    assert solo["settle_launches"] >= 2 and solo["settle_s"] >= 0.3
+    assert solo["bitexact_vs_golden"] is True and solo["value"] > 0
+    assert line["efficiency"] == pytest.approx(line["value"] / (world * solo["value"]), rel=1e-2)
     assert line["n_gpus"] == world
     assert line["bitexact_vs_golden"] is True
     assert line["scaling"] == "strong"
@@ -66,6 +74,22 @@ def _bench_module():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
+
+
+def test_solo_leg_settles_like_the_headline():
+    """The GPU run's N > 1 solo leg calls run_timed with the headline's settle arguments
+    (--settle, --settle-s), not a cold start; settle_steps honours both
+    bounds and reports the launches it ran."""
+    mod = _bench_module()
+    src = (ROOT / "bench.py").read_text()
+    solo = src[src.index("the headline's settle rule (VERDICT r04 item 4)"):]
+    call = solo[solo.index("run_timed(one,"):solo.index("ok1, _ = one.check")]
+    assert "args.settle," in call and "settle_s=args.settle_s" in call
+    calls = []
+    n, t = mod.settle_steps(lambda i: calls.append(i), lambda: None, 120, 20, 0.05, block=10)
+    assert n >= 100 and n == len(calls) and n % 10 == 0 and t >= 0.05
+    n, t = mod.settle_steps(lambda i: None, lambda: None, 0, 0, 0.0)
+    assert n == 0
 
 
 def test_settle_waits_for_a_steady_launch_rate():

@@ -96,3 +96,47 @@ def test_fault_marks_only_its_own_call(gpu_ctx, oracle):
         gpu_ctx.check()
     assert ei.value.code == gpu.EFAULT
     gpu_ctx.check()  # cleared
+
+
+def test_fault_mark_does_not_outlive_a_graph_replay(gpu_ctx, oracle):
+    """a captured ragged call replays the same generation every time. A scan fault
+    in one replay marks that generation; the next replay's tile-count scan (ticket 0) clears the
+    mark, so the replay after a faulted one computes every CRC without a check in between, and
+    the fault is still reported by the next check."""
+    lib = _lib.load()
+    n = 3 * 4096
+    buf, d_off, d_len, lengths = _ragged_batch(n, seed=0xFA19)
+    want = oracle.synth_crc_batch(0xFA19, lengths)
+    out = torch.zeros(n, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_ragged(buf, d_off, d_len, out)  # workspaces allocated before the capture
+    torch.cuda.synchronize()
+    gpu_ctx.check()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            gpu_ctx.crc32_ragged(buf, d_off, d_len, out, stream=s)
+    torch.cuda.synchronize()
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    gpu_ctx.check()
+    assert lib.subspace_crc_testutil_set(gpu_ctx._h, b"stale_ticket", 1 << 30) == 0
+    g.replay()  # faults: its kernels skip
+    torch.cuda.synchronize()
+    out.zero_()
+    torch.cuda.synchronize()
+    g.replay()  # the same generation, no check in between
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    with pytest.raises(gpu.CrcError) as ei:
+        gpu_ctx.check()
+    assert ei.value.code == gpu.EFAULT
+    gpu_ctx.check()  # cleared
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    gpu_ctx.check()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)

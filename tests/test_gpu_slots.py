@@ -530,13 +530,17 @@ def test_strided_oversize_sizes_are_flagged(gpu_ctx, oracle, slot_size, cs, ms):
     whose prefix a publish rewrites in the same (fused) launch. Such slots get
     SUBSPACE_CRC_SLOT_OVERSIZE and are left untouched, on every path: the fused small-slot
     kernel (1000 / 4000-B slots), small + finish kernels (metadata > 64 B), ragged + finish
-    (5000-B slots); every other slot is published and verified as the oracle's."""
+    (5000-B slots); every other slot is published and verified as the oracle's. ADVICE r04: no
+    payload kernel reads an oversize slot's bytes -- the last slot's size (2^40) points far past
+    the end of the buffer, and the middle slot's (2^33) past it too."""
     count = 900
     rng = np.random.default_rng(slot_size + ms)
     area = (slot_size + 63) & ~63
     sizes = rng.integers(0, area + 1, count).astype(np.uint64)
     big = rng.random(count) < 0.1
     sizes[big] = rng.integers(area + 1, area + 3000, int(big.sum()))
+    big[[count // 2, count - 1]] = True
+    sizes[count // 2], sizes[count - 1] = 1 << 33, 1 << 40
     host, ps, stride = build_channel(count, slot_size, cs, ms, sizes, seed=slot_size + cs + ms)
     assert stride - ps == area
     orig = host.copy()
