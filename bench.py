@@ -346,10 +346,26 @@ def end_to_end(ctx, gpu) -> dict:
         t_drain = sorted(ts)[2]
     finally:
         gpu.host_unregister(host)
+    # the box's plain pinned H2D copy rate for the same bytes (the end-to-end path's bound)
+    import torch
+    pinned = torch.empty(MSGS * stride, dtype=torch.uint8, pin_memory=True)
+    dst = torch.empty(MSGS * stride, dtype=torch.uint8, device="cuda")
+    dst.copy_(pinned, non_blocking=True)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(5):
+        dst.copy_(pinned, non_blocking=True)
+    b.record()
+    torch.cuda.synchronize()
+    h2d = MSGS * stride * 5 / (a.elapsed_time(b) * 1e-3) / 1e9
+    del pinned, dst
     return {"value": round(BATCH_BYTES / t_pub / 2**30, 2), "unit": "GiB/s",
             "verify_value": round(BATCH_BYTES / t_ver / 2**30, 2),
             "drain_hook_verify_value": round(BATCH_BYTES / t_drain / 2**30, 2),
             "slot_bytes_GBps": round(MSGS * stride / t_pub / 1e9, 2),
+            "pcie_h2d_GBps": round(h2d, 2),
+            "slot_bytes_frac_of_h2d": round(MSGS * stride / t_pub / 1e9 / h2d, 3),
             "path": "subspace_crc32_host_slots: 65,536 pinned host slots (stride 4,160) -> chunked H2D "
                     "overlapping the kernels -> 4 B per slot D2H -> flag + checksum written into each host "
                     "prefix (publish); value = payload GiB/s, median of 5 calls; drain_hook_verify_value: "
@@ -622,13 +638,30 @@ def time_calls(fn, iters, warm_ms=60.0):
     return a.elapsed_time(b) / iters
 
 
-def config_line(nbytes, ms, bitexact, kernel, extra=None):
+def config_traffic(name):
+    """(HBM bytes per call, source) of a secondary configuration from the committed PMC summary
+    (profiles/traffic_configs.json, tools/pmc_configs.sh + tools/summarize_configs_traffic.py:
+    separate rocprofv3 --pmc passes, not measured in this run), or (None, None)."""
+    f = ROOT / "profiles" / "traffic_configs.json"
+    try:
+        tj = json.loads(f.read_text())
+        c = tj["configs"][name]
+        return c["hbm_bytes_per_call"], (f"profiles/traffic_configs.json ({tj.get('source', '?')}; PMC FETCH_SIZE x2 + "
+                                         f"WRITE_SIZE per call, ratio {c['ratio']} of the algorithmic bytes; not "
+                                         f"measured in this run)")
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
+def config_line(nbytes, ms, bitexact, kernel, extra=None, name=None):
     gbs = nbytes / (ms * 1e-3) / 1e9
+    traffic, tsrc = config_traffic(name) if name else (None, None)
     line = {"value": round(nbytes / (ms * 1e-3) / 2**30, 1), "unit": "GiB/s", "bytes": int(nbytes),
             "ms_per_call": round(ms, 4), "pct_of_hbm_peak": round(100 * gbs / HBM_PEAK_GBS, 2),
             "bitexact_vs_golden": bitexact,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kernel,
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+                         "kernel": kernel,
                          "launch_ms_source": "HIP event span of back-to-back calls / calls (the whole C-ABI call: "
                                              "prep kernels + CRC kernel + combine)"}}
     if extra:
@@ -656,7 +689,7 @@ def secondary_configs(ctx, dev, names, iters) -> dict:
             out = torch.empty(len(lengths), dtype=torch.int32, device=dev)
             ms = time_calls(lambda: ctx.crc32_ragged(buf, d_off, d_len, out), iters)
             ok = digest(out.cpu().numpy().view(np.uint32)) == GOLD["C"]["sha256_le_u32"]
-            res[name] = config_line(int(lengths.sum()), ms, ok, "subspace_crc32_batch (ragged kernel)", {
+            res[name] = config_line(int(lengths.sum()), ms, ok, "subspace_crc32_batch (ragged kernel)", name=name, extra={
                 "workload": "C: 1 Mi messages, 64 B - 1 MiB log-uniform, " +
                             ("packed unaligned" if name == "Cu" else "64-B aligned offsets"),
                 "messages": len(lengths)})
@@ -675,7 +708,7 @@ def secondary_configs(ctx, dev, names, iters) -> dict:
                 ms = time_calls(lambda: ctx.crc32_uniform(buf, L, L, n, out), iters)
                 kern = "subspace_crc32_batch_uniform (long-message kernel)"
             ok = digest(out.cpu().numpy().view(np.uint32)) == GOLD["D"]["sha256_le_u32"]
-            res[name] = config_line(n * L, ms, ok, kern, {"workload": "D: 256 x 64 MiB", "messages": n})
+            res[name] = config_line(n * L, ms, ok, kern, {"workload": "D: 256 x 64 MiB", "messages": n}, name=name)
             del buf, out
         elif name == "S":
             res.update(slot_configs(ctx, dev, iters))
@@ -741,7 +774,7 @@ def slot_configs(ctx, dev, iters) -> dict:
         ms = time_calls(call, 400)
         torch.cuda.synchronize()
         ok, check = slot_leg_check(mode, bufs[0], n, stride, ps, size, cs, ms_, status, errs, rng)
-        res[key] = config_line(nbytes, ms, ok, "subspace_crc32_slots_strided", {
+        res[key] = config_line(nbytes, ms, ok, "subspace_crc32_slots_strided", name=key, extra={
             "workload": "S: 65,536 slots (prefix 64 B + 4 KiB payload, stride 4,160), 3-span checksum, " +
                         ("publish: flag + checksum stored" if mode == gpu.SLOT_CALCULATE else
                          "verify: per-slot status + mismatch count"),
@@ -792,7 +825,7 @@ def slot_configs(ctx, dev, iters) -> dict:
         else:
             ok = int(errs.item()) == 0 and bool((status == 0).all().item())
             check = "every slot passes"
-        res[key] = config_line(nbytes, ms, ok, list_kernel, {
+        res[key] = config_line(nbytes, ms, ok, list_kernel, name=key, extra={
             "workload": "S_list: config S's 65,536 slots as device slot lists (subspace_crc_slot records) in shuffled "
                         "order, one per channel copy, 4 copies rotated, " +
                         ("publish" if mode == gpu.SLOT_CALCULATE else "verify"),
@@ -820,7 +853,7 @@ def slot_configs(ctx, dev, iters) -> dict:
         ms = time_calls(call, 200)
         torch.cuda.synchronize()
         ok, check = slot_leg_check(mode, bufs[0], n, stride, ps, size, cs, ms_, status, errs, rng)
-        res[key] = config_line(nbytes, ms, ok, "subspace_crc32_slots_strided", {
+        res[key] = config_line(nbytes, ms, ok, "subspace_crc32_slots_strided", name=key, extra={
             "workload": "S_meta: 65,536 slots (prefix 128 B with 16 B metadata + 4 KiB payload, stride 4,224), "
                         "3-span checksum, " + ("publish" if mode == gpu.SLOT_CALCULATE else "verify"),
             "check": check})

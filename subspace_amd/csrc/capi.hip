@@ -490,7 +490,7 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
   const u64 tiles = (count + 1) / 2;
   const unsigned blocks =
       (unsigned)std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSmallRingTiles));
-  const size_t lds = small_lds_bytes() + 16;
+  const size_t lds = small_lds_bytes() + 32;  // + the mismatch word and the 4 pair counters
   if (slot) {
     a.prefixes = slot->prefixes;
     a.pstride = slot->pstride;
@@ -629,6 +629,13 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
       for (int n = 0; n < 16; n++)
         for (int cp = 0; cp < 4; cp++) laneops[128 * kUniSlotOpZ64 + k * 64 + n * 4 + cp] = nt[k * 16 + n];
   }
+  {  // Z_32, replicated 4x the same way (crc_device.h kUniSlotOpZ32)
+    u32 nt[128];
+    nibble_tables(z_bytes(c->host_tab, 32), nt);
+    for (int k = 0; k < 8; k++)
+      for (int n = 0; n < 16; n++)
+        for (int cp = 0; cp < 4; cp++) laneops[128 * kUniSlotOpZ32 + k * 64 + n * 4 + cp] = nt[k * 16 + n];
+  }
   nibble_tables(z_bytes(c->host_tab, 4096), &rops[kLaneOpWords]);
   for (int k = 0; k < 31; k++)
     nibble_tables(z_bytes(c->host_tab, 8192ull << k),
@@ -684,13 +691,13 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
                             (int)ragged_lds_bytes());
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)small_lds_bytes() + 16);
+                            (int)small_lds_bytes() + 32);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)small_lds_bytes() + 16);
+                            (int)small_lds_bytes() + 32);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)small_lds_bytes() + 16);
+                            (int)small_lds_bytes() + 32);
   if (e != hipSuccess) {
     subspace_crc_ctx_destroy(c);
     return hip_fail(e, "context setup");

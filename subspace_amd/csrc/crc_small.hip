@@ -55,10 +55,13 @@
 #include "crc_device.h"
 
 // Timing-only investigation builds (tools/ab_lib.sh -DSUBSPACE_SMALL_VARIANT=n; the product is
-// 0, the others compute nothing valid): 1 no prologue span loads / hash; 2 no flush; 3 tile 0's
-// loads in the FAST form when the wave is FAST.
+// 0, the others compute nothing valid): 1 no prologue span loads / hash; 2 no flush.
 #ifndef SUBSPACE_SMALL_VARIANT
 #define SUBSPACE_SMALL_VARIANT 0
+#endif
+// FAST tiles shared by a SIMD's two waves (A/B builds; 0: each wave its own 16 tiles, r05f).
+#ifndef SUBSPACE_SMALL_PAIR
+#define SUBSPACE_SMALL_PAIR 1
 #endif
 
 namespace subspace_amd {
@@ -93,6 +96,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   const u32 nk = t0 < ntiles ? (u32)((ntiles - t0 + nw - 1) / nw) : 0u;  // tiles tau = t0 + k*nw
   const uint8_t* safe = reinterpret_cast<const uint8_t*>(gtab);  // 16 readable bytes
   const bool calc = a.mode == 0u;
+  constexpr bool kPair = SUBSPACE_SMALL_PAIR != 0 && NPW == 8;
 
   // this lane's message in tile k (present: k < nk and m < count)
   auto msg_of = [&](u32 k) __attribute__((always_inline)) { return 2 * (t0 + (u64)k * nw) + (u64)h; };
@@ -125,6 +129,39 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u64 L0 = readlane64(wL, i0), L1 = readlane64(wL, i0 + 1);
     s = h ? s1 : s0;
     L = h ? L1 : L0;
+  };
+  // FAST, paired: the two waves of a SIMD (wid and wid ^ 4: wave slots 0 and 1 of every SIMD,
+  // r05e) share their tiles. In a streaming launch the SIMD's older wave runs ~25 % faster than
+  // its partner (config S's list: loop ends 43.5 against 53.0 us, the uniform kernel's 1.5 us
+  // apart; issue priority does not change it, r05g), and the older then sits idle for ~10 us.
+  // The pair's tiles j = 0 .. T-1 (T = both waves' tile counts; tile j is tile j >> 1 of wave
+  // (j & 1 ? second : first)) are drawn from a per-pair LDS counter, two per ticket, a tile
+  // ahead; each wave starts with its own tiles 0 and 1 (tile 0 the prologue's load) and writes
+  // every result into the owning wave's ring, which the owner flushes after a workgroup barrier.
+  const u32 pfirst = wid & (u32)(NPW / 2 - 1), psecond = pfirst + (u32)(NPW / 2);
+  const bool second = wid >= (u32)(NPW / 2);
+  const u32 pwid = second ? pfirst : psecond;  // the partner
+  const u64 pt0 = front_slot(blockIdx.x, gridDim.x, pwid);
+  const u32 pnk = pt0 < ntiles ? (u32)((ntiles - pt0 + nw - 1) / nw) : 0u;
+  const u64 pfm = 2 * (pt0 + (u64)((u32)lane >> 1) * nw) + ((u32)lane & 1u);
+  const bool pflive = ((u32)lane >> 1) < pnk && pfm < count;
+  const u64 pfmc = pfm < count ? pfm : count - 1;
+  u64 pS = 0, pL = 0;  // the partner's window records (lane i: its message i)
+  const u32 T = nk + pnk;
+  const u32 nk0 = second ? pnk : nk, nk1 = second ? nk : pnk;  // tile counts of first, second
+  const u64 t00 = second ? pt0 : t0, t01 = second ? t0 : pt0;
+  // pair tile j's line offset for this lane (j clamped into the pair's tiles), pinned
+  auto pair_off = [&](u32 j) __attribute__((always_inline)) {
+    const u32 jj = j < T ? j : (T ? T - 1u : 0u);
+    const bool o = (jj & 1u) != 0u;  // owner: second
+    u32 kk = jj >> 1;
+    kk = kk < kSmallRingTiles ? kk : kSmallRingTiles - 1u;
+    const u64 w = (o == second) ? wS : pS;
+    const int i0 = (int)(2u * kk);
+    const u64 s0 = readlane64(w, i0), s1 = readlane64(w, i0 + 1);
+    u64 off = (h ? s1 : s0) + 128u * l;
+    asm volatile("" : "+v"(off));
+    return off;
   };
   // Extended bytes this kernel reads for tile k's half as a half-tile (0: nothing -- no
   // message, an empty one, or one longer than a half-tile, computed apart: long_crc).
@@ -355,6 +392,36 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32 code = (k < nk && msg_of(k) < count) ? 0u : kCodeSkip;
     if (l == 31u) lds_st64(sring + 8u * (2u * (k & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
   };
+  // FAST, paired: pair tile j into its owner's ring
+  auto process_pair = [&](const u32x4 (&cur)[8], u32 j) __attribute__((always_inline)) {
+    const u32 crc = line_crc32_2chain(cur, l == 0u ? a.init : 0u, lc0, lc1, z64);
+    u32 v = lane_shift(lop, crc);
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    const bool o = (j & 1u) != 0u;
+    const u32 kk = j >> 1;
+    const u64 m = 2 * ((o ? t01 : t00) + (u64)kk * nw) + (u64)h;
+    const u32 code = (kk < (o ? nk1 : nk0) && m < count) ? 0u : kCodeSkip;
+    const u32 ring = sbase + kSmallRing + (o ? psecond : pfirst) * kSmallRingBytesPerWave;
+    if (l == 31u && j < T) lds_st64(ring + 8u * (2u * (kk & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
+  };
+  // the pair's next tile: lane 0's LDS atomic, issued a tile ahead; the ticket reaches the
+  // wave (ticket()) only where it is used, after the tile's lookups
+  const u32 pctr = sbase + (u32)small_lds_bytes() + 16u + 4u * pfirst;
+  // (inline asm: hipcc's atomic optimizer would broadcast the result inside the lane-0 branch,
+  // waiting for the LDS round trip right there)
+  auto draw = [&]() __attribute__((always_inline)) {
+    u32 t = 0;
+    if (lane == 0) asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(t) : "v"(pctr), "v"(2u) : "memory");
+    return t;
+  };
+  auto ticket = [&](u32 t) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t)::"memory");  // (the asm atomic is invisible to hipcc)
+    return (u32)__builtin_amdgcn_readfirstlane((int)t);
+  };
   // SLOT: lane i's message of the first window (fm): its record's prefix offset, and (after
   // the barrier) the prefix terms, from words loaded in the prologue
   u64 fpre = 0;
@@ -414,8 +481,13 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   wS = a.offsets[fmc * a.ostride];
   wL = a.lengths[fmc * a.lstride];
   if constexpr (SLOT) fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
+  if constexpr (kPair) {
+    pS = a.offsets[pfmc * a.ostride];
+    pL = a.lengths[pfmc * a.lstride];
+  }
   fill.store(sbase);
   if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
+  if (kPair && threadIdx.x < (u32)(NPW / 2)) lds_st(sbase + (u32)small_lds_bytes() + 16u + 4u * threadIdx.x, 4u);
   // FAST (wave-uniform): the window is every tile of the wave (at most 32: small_run's grid) and
   // each of its messages is a whole 4 KiB payload on a 16-B boundary (SLOT: within max_len) --
   // the fixed-size channel drain. Its loop is the uniform kernel's: the next tile's address from
@@ -425,8 +497,10 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // immediate offsets -- 67.5 against 44.1 us per 65,536 slots in the read probe, testutil.hip
   // slot_list_read_kernel modes 2 and 3 -- and its address and code arithmetic made the kernel
   // compute-bound, 6,759 VALU instructions per wave against the uniform kernel's 4,508.)
+  // (paired: over both windows, so the two waves of a pair decide alike)
   const bool conf = !flive || (wL == (u64)kSmallMaxExt && (wS & 15u) == 0 && (!SLOT || wL <= a.max_len));
-  const bool fast = nk <= kSmallRingTiles && __ballot(!conf) == 0;
+  const bool pconf = !kPair || !pflive || (pL == (u64)kSmallMaxExt && (pS & 15u) == 0 && (!SLOT || pL <= a.max_len));
+  const bool fast = nk <= kSmallRingTiles && (!kPair || pnk <= kSmallRingTiles) && __ballot(!conf || !pconf) == 0;
   if constexpr (probe) pt[1] = __builtin_amdgcn_s_memrealtime();
   u64 sA, LA, sB, LB;
   win_rec(0, sA, LA);
@@ -438,16 +512,44 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   }
   u32x4 A[8], B[8];
   u64 sc = sA, Lc = LA;
-  if (SUBSPACE_SMALL_VARIANT == 3 && fast)
-    load_at(A, fast_off(0));
-  else
-    load_lines(A, sc, ext(0, sc, Lc));  // (FAST: the same addresses as load_at's)
+  load_lines(A, sc, ext(0, sc, Lc));  // (FAST: the same addresses as load_at's)
   __syncthreads();
   if constexpr (probe) pt[2] = __builtin_amdgcn_s_memrealtime();
   if constexpr (SLOT && SUBSPACE_SMALL_VARIANT != 1) eH = span_hash(pwords, pmeta, eF, eS, ehas);
 
   u32 k = 0;
-  if (fast) {
+  if (fast && kPair) {
+    // ping-pong, one tile in flight (crc_uniform.hip's loop) over the pair's tiles, two per
+    // iteration: A holds tile x0 (a wave's first: its own tile 0, the prologue's load), B gets
+    // x1, the next two come from one ticket (the pair's counter starts at 4: tiles 0-3 are the
+    // two waves' first two). One exit, at the top: a break between the halves gave the loop head
+    // a predecessor with B's loads pending, and hipcc then waited for the tile in flight at every
+    // iteration's head. A tile past the pair's last is a re-read of that tile, not stored.
+    // (the drain as a builtin s_waitcnt vmcnt(0), which hipcc's waitcnt pass sees)
+    auto drain = [&]() __attribute__((always_inline)) { __builtin_amdgcn_s_waitcnt(0x0F70); };
+    u32 x0 = second ? 1u : 0u, x1 = x0 + 2u;
+    u32 t = draw();
+    drain();  // tile 0 and the prologue's loads, before the loop (a clean loop-head state)
+    for (;;) {
+      if (x0 >= T) break;
+      const u64 qB = pair_off(x1);
+      issue_prio_hi();
+      drain();  // tile x0's lines
+      load_at(B, qB);
+      issue_prio_lo();
+      process_pair(A, x0);
+      const u32 y = ticket(t);
+      const u64 qA = pair_off(y);
+      issue_prio_hi();
+      drain();
+      load_at(A, qA);
+      issue_prio_lo();
+      t = draw();
+      process_pair(B, x1);
+      x0 = y;
+      x1 = y + 1u;
+    }
+  } else if (fast) {
     // ping-pong, unrolled by two, one tile in flight (crc_uniform.hip's loop)
     for (; k + 1 < nk; k += 2) {
       const u64 qB = fast_off(k + 1);
@@ -467,9 +569,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       drain_before_issue();
       process_fast(A, k);
     }
-    if constexpr (probe) pt[4] = __builtin_amdgcn_s_memrealtime();
-    if (nk && SUBSPACE_SMALL_VARIANT != 2) flush(0, nk);
-    if constexpr (probe) pt[5] = __builtin_amdgcn_s_memrealtime();
   } else {
     // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines; the
     // ring is finished whenever it holds 32 tiles, right after the next tile's loads are issued
@@ -500,13 +599,15 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
       process(A, sc, Lc, k);
     }
-    if constexpr (probe) pt[4] = __builtin_amdgcn_s_memrealtime();
-    if (nk) {
-      const u32 kf = (nk - 1u) & ~kWinMask;  // the last window, not flushed yet
-      flush(kf, nk - kf);
-    }
-    if constexpr (probe) pt[5] = __builtin_amdgcn_s_memrealtime();
   }
+  if constexpr (probe) pt[4] = __builtin_amdgcn_s_memrealtime();
+  // every wave of the workgroup: a pair's waves wrote into each other's rings
+  if constexpr (kPair) __syncthreads();
+  if (nk && SUBSPACE_SMALL_VARIANT != 2) {
+    const u32 kf = (nk - 1u) & ~kWinMask;  // the last window, not flushed yet (FAST: 0)
+    flush(kf, nk - kf);
+  }
+  if constexpr (probe) pt[5] = __builtin_amdgcn_s_memrealtime();
   if constexpr (SLOT) {
     if (a.error_count && lane == 0) {
       if (calc) {

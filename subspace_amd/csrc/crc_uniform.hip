@@ -49,6 +49,11 @@
 #ifndef SUBSPACE_SLOT_VARIANT
 #define SUBSPACE_SLOT_VARIANT 0
 #endif
+// A wave's last tile -- computed with nothing in flight -- as four 8-step chains per line
+// (crc_device.h line_crc32_4chain) instead of two 16-step ones (A/B builds).
+#ifndef SUBSPACE_LAST4
+#define SUBSPACE_LAST4 0
+#endif
 
 namespace subspace_amd {
 
@@ -73,7 +78,8 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   // four pairs); bit-exact.
   constexpr bool kTwoChain = true;  // (false: the one-chain line CRC, for A/B builds)
   // step tables, per-lane operators, Z_4096 and Z_64 (the two-chain line CRC's join)
-  LdsFill<WG, kTwoChain ? kUniOpSlots : kUniOpSlotsOneChain> fill;
+  // (the Z_32 slots only for LAST4 builds)
+  LdsFill<WG, kTwoChain ? (SUBSPACE_LAST4 != 0 ? kUniOpSlots : kUniSlotOpZ32) : kUniOpSlotsOneChain> fill;
   fill.load(gtab, gops);
 
   const int lane = threadIdx.x & 63;
@@ -169,6 +175,11 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
     if constexpr (kTwoChain) return line_crc32_2chain(d, s_init, lc0, lc1, z64);
     else return line_crc32(d, s_init, lc0, lc1);
   };
+  const u32 z32 = sbase + kLdsOps + 512u * (u32)kUniSlotOpZ32 + 4u * (u32)(lane & 3);
+  auto line_crc_last = [&](const u32x4 (&d)[8]) {
+    if constexpr (SUBSPACE_LAST4 != 0) return line_crc32_4chain(d, s_init, lc0, lc1, z32, z64);
+    else return line_crc(d);
+  };
   // Message CRCs of tile k: into ring slots 2*(k - kf) + h (kf = first tile of the window);
   // SLOT: into the tagged ring entry 2*k + h (k < kSlotRingRounds), as CRC | k << 32.
   auto tile_result = [&](u32 crc, u32 k, u32 kf) {
@@ -232,7 +243,8 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   constexpr u32 kWin = SLOT ? ~0u : (u32)(kRing / 2);
   u32 k = 0, kf = 0;
   u64 pt_finish = 0;  // PROBE, SLOT: when a finishing wave began
-  for (; k + 1 < nk; k += 2) {
+  // (LAST4: the loop leaves the last one or two tiles to the tail below)
+  for (; k + 1 + (SUBSPACE_LAST4 != 0) < nk; k += 2) {
     const u64 qB = addr_before_wait(k + 1);
     issue_prio_hi();
     drain_before_issue();
@@ -252,13 +264,27 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
     tile_result(line_crc(B), k + 1, kf);
   }
   if constexpr (PROBE) pt[2] = __builtin_amdgcn_s_memrealtime();
-  if (k < nk) {  // odd last tile, already loaded
+  if (SUBSPACE_LAST4 != 0 && k + 1 < nk) {  // LAST4: the last two tiles, the last one four-chain
+    const u64 qB = addr_before_wait(k + 1);
+    issue_prio_hi();
+    drain_before_issue();
+    load_at(B, qB);
+    issue_prio_lo();
     if (!SLOT && k - kf == kWin) {
       wave_lds_sync();
       flush(kf, kRing / 2);
       kf = k;
     }
     tile_result(line_crc(A), k, kf);
+    drain_before_issue();
+    tile_result(line_crc_last(B), k + 1, kf);
+  } else if (k < nk) {  // odd last tile, already loaded
+    if (!SLOT && k - kf == kWin) {
+      wave_lds_sync();
+      flush(kf, kRing / 2);
+      kf = k;
+    }
+    tile_result(line_crc_last(A), k, kf);
   }
   wave_lds_sync();
   if constexpr (SLOT) {

@@ -224,7 +224,7 @@ int subspace_crc_testutil_slot_list_read(const void* dev_records, uint64_t count
   if (grid < 1) grid = 1;
   if (out_words < grid * 512) return -1;
   const auto* r = static_cast<const uint64_t*>(dev_records);
-  const size_t ldsb = lds ? subspace_amd::small_lds_bytes() + 16 : 0;
+  const size_t ldsb = lds ? subspace_amd::small_lds_bytes() + 32 : 0;
   const void* fns[5] = {(const void*)slot_list_read_kernel<0>, (const void*)slot_list_read_kernel<1>,
                         (const void*)slot_list_read_kernel<2>, (const void*)slot_list_read_kernel<3>,
                         (const void*)slot_list_read_kernel<4>};

@@ -35,7 +35,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--settle", type=int, default=600)
-    ap.add_argument("--order", default="shuffled", choices=["shuffled", "ordered"])
+    ap.add_argument("--order", default="shuffled", choices=["shuffled", "ordered", "alias"],
+                    help="alias: every record points at slot 0 of copy 0 (the compute-only run)")
     ap.add_argument("--mode", default="verify", choices=["verify", "publish"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -54,9 +55,10 @@ def main():
     for b in bufs:
         ctx.crc32_slots_strided(b, stride, N, message_size=SIZE, checksum_size=4, metadata_size=0,
                                 mode=gpu.SLOT_CALCULATE)
-    order = rng.permutation(N).astype(np.uint64) if a.order == "shuffled" else np.arange(N, dtype=np.uint64)
+    order = {"shuffled": rng.permutation(N).astype(np.uint64), "ordered": np.arange(N, dtype=np.uint64),
+             "alias": np.zeros(N, dtype=np.uint64)}[a.order]
     recs = []
-    for b in bufs:
+    for b in (bufs if a.order != "alias" else bufs[:1] * NB):
         b0 = np.uint64(b.data_ptr())
         r = np.stack([b0 + order * np.uint64(stride), b0 + order * np.uint64(stride) + np.uint64(ps),
                       np.full(N, SIZE, dtype=np.uint64)], axis=1)
