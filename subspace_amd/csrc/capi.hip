@@ -490,7 +490,7 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
   const u64 tiles = (count + 1) / 2;
   const unsigned blocks =
       (unsigned)std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSmallRingTiles));
-  const size_t lds = small_lds_bytes() + 32;  // + the mismatch word and the 4 pair counters
+  const size_t lds = small_lds_bytes() + 16;  // + the mismatch word
   if (slot) {
     a.prefixes = slot->prefixes;
     a.pstride = slot->pstride;
@@ -691,13 +691,13 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
                             (int)ragged_lds_bytes());
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)small_lds_bytes() + 32);
+                            (int)small_lds_bytes() + 16);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)small_lds_bytes() + 32);
+                            (int)small_lds_bytes() + 16);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)small_lds_bytes() + 32);
+                            (int)small_lds_bytes() + 16);
   if (e != hipSuccess) {
     subspace_crc_ctx_destroy(c);
     return hip_fail(e, "context setup");

@@ -156,7 +156,7 @@ constexpr u32 kSmallRing = kLdsOps + (u32)kSmallOpSlots * 512u;  // per-wave res
 constexpr u32 kSmallRingTiles = 32;                               // tiles per ring window
 constexpr u32 kSmallRingBytesPerWave = kSmallRingTiles * 2u * 8u;  // (value | code << 32) per message
 constexpr size_t small_lds_bytes() { return kSmallRing + 8u * kSmallRingBytesPerWave; }
-static_assert(small_lds_bytes() + 32u <= 160u * 1024u, "small-message kernel LDS (+ mismatch word and pair counters) exceeds 160 KiB");
+static_assert(small_lds_bytes() + 16u <= 160u * 1024u, "small-message kernel LDS (+ mismatch word) exceeds 160 KiB");
 
 // Small-message kernel arguments (crc_small.hip; one struct: read with scalar loads).
 struct SmallArgs {

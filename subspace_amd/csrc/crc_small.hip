@@ -59,10 +59,6 @@
 #ifndef SUBSPACE_SMALL_VARIANT
 #define SUBSPACE_SMALL_VARIANT 0
 #endif
-// FAST tiles shared by a SIMD's two waves (A/B builds; 0: each wave its own 16 tiles, r05f).
-#ifndef SUBSPACE_SMALL_PAIR
-#define SUBSPACE_SMALL_PAIR 1
-#endif
 
 namespace subspace_amd {
 
@@ -96,7 +92,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   const u32 nk = t0 < ntiles ? (u32)((ntiles - t0 + nw - 1) / nw) : 0u;  // tiles tau = t0 + k*nw
   const uint8_t* safe = reinterpret_cast<const uint8_t*>(gtab);  // 16 readable bytes
   const bool calc = a.mode == 0u;
-  constexpr bool kPair = SUBSPACE_SMALL_PAIR != 0 && NPW == 8;
 
   // this lane's message in tile k (present: k < nk and m < count)
   auto msg_of = [&](u32 k) __attribute__((always_inline)) { return 2 * (t0 + (u64)k * nw) + (u64)h; };
@@ -130,39 +125,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     s = h ? s1 : s0;
     L = h ? L1 : L0;
   };
-  // FAST, paired: the two waves of a SIMD (wid and wid ^ 4: wave slots 0 and 1 of every SIMD,
-  // r05e) share their tiles. In a streaming launch the SIMD's older wave runs ~25 % faster than
-  // its partner (config S's list: loop ends 43.5 against 53.0 us, the uniform kernel's 1.5 us
-  // apart; issue priority does not change it, r05g), and the older then sits idle for ~10 us.
-  // The pair's tiles j = 0 .. T-1 (T = both waves' tile counts; tile j is tile j >> 1 of wave
-  // (j & 1 ? second : first)) are drawn from a per-pair LDS counter, two per ticket, a tile
-  // ahead; each wave starts with its own tiles 0 and 1 (tile 0 the prologue's load) and writes
-  // every result into the owning wave's ring, which the owner flushes after a workgroup barrier.
-  const u32 pfirst = wid & (u32)(NPW / 2 - 1), psecond = pfirst + (u32)(NPW / 2);
-  const bool second = wid >= (u32)(NPW / 2);
-  const u32 pwid = second ? pfirst : psecond;  // the partner
-  const u64 pt0 = front_slot(blockIdx.x, gridDim.x, pwid);
-  const u32 pnk = pt0 < ntiles ? (u32)((ntiles - pt0 + nw - 1) / nw) : 0u;
-  const u64 pfm = 2 * (pt0 + (u64)((u32)lane >> 1) * nw) + ((u32)lane & 1u);
-  const bool pflive = ((u32)lane >> 1) < pnk && pfm < count;
-  const u64 pfmc = pfm < count ? pfm : count - 1;
-  u64 pS = 0, pL = 0;  // the partner's window records (lane i: its message i)
-  const u32 T = nk + pnk;
-  const u32 nk0 = second ? pnk : nk, nk1 = second ? nk : pnk;  // tile counts of first, second
-  const u64 t00 = second ? pt0 : t0, t01 = second ? t0 : pt0;
-  // pair tile j's line offset for this lane (j clamped into the pair's tiles), pinned
-  auto pair_off = [&](u32 j) __attribute__((always_inline)) {
-    const u32 jj = j < T ? j : (T ? T - 1u : 0u);
-    const bool o = (jj & 1u) != 0u;  // owner: second
-    u32 kk = jj >> 1;
-    kk = kk < kSmallRingTiles ? kk : kSmallRingTiles - 1u;
-    const u64 w = (o == second) ? wS : pS;
-    const int i0 = (int)(2u * kk);
-    const u64 s0 = readlane64(w, i0), s1 = readlane64(w, i0 + 1);
-    u64 off = (h ? s1 : s0) + 128u * l;
-    asm volatile("" : "+v"(off));
-    return off;
-  };
   // Extended bytes this kernel reads for tile k's half as a half-tile (0: nothing -- no
   // message, an empty one, or one longer than a half-tile, computed apart: long_crc).
   auto ext = [&](u32 k, u64 s, u64 L) __attribute__((always_inline)) -> u32 {
@@ -173,11 +135,17 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   auto load_lines = [&](u32x4 (&D)[8], u64 s, u32 E) __attribute__((always_inline)) {
     const uint8_t* p0 = E ? base + (s & ~(u64)15) : safe;
     const u32 lastb = E ? (E - 1u) & ~15u : 0u;  // the block holding the message's last byte
+    const u32x4* q[8];
 #pragma unroll
     for (int b = 0; b < 8; b++) {
       const u32 off = 128u * l + 16u * (u32)b;
-      D[b] = *reinterpret_cast<const u32x4*>(p0 + (off < lastb ? off : lastb));
+      q[b] = reinterpret_cast<const u32x4*>(p0 + (off < lastb ? off : lastb));
+      D[b] = *q[b];
     }
+    // (the addresses live past the loads: none of their VGPRs becomes a load's destination,
+    // load_at)
+#pragma unroll
+    for (int b = 0; b < 8; b++) asm volatile("" ::"v"(q[b]));
     // keep the loads at this point, in order (hipcc otherwise sinks them into the compute)
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -194,6 +162,10 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32x4* q = reinterpret_cast<const u32x4*>(base + off);
 #pragma unroll
     for (int b = 0; b < 8; b++) D[b] = q[b];
+    // the address stays live past the last load: hipcc otherwise hands its (dead) VGPRs to that
+    // load as its destination, and the loop ran ~8 us slower per 65,536-slot call (r05,
+    // tools/load_overlap.py)
+    asm volatile("" ::"v"(q));
     __builtin_amdgcn_sched_barrier(0);
   };
   // Z_{2^b}^{-1} applied for the set bits of `bits` (b < nb <= 12; wave-uniform loop over the
@@ -392,36 +364,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32 code = (k < nk && msg_of(k) < count) ? 0u : kCodeSkip;
     if (l == 31u) lds_st64(sring + 8u * (2u * (k & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
   };
-  // FAST, paired: pair tile j into its owner's ring
-  auto process_pair = [&](const u32x4 (&cur)[8], u32 j) __attribute__((always_inline)) {
-    const u32 crc = line_crc32_2chain(cur, l == 0u ? a.init : 0u, lc0, lc1, z64);
-    u32 v = lane_shift(lop, crc);
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-    const bool o = (j & 1u) != 0u;
-    const u32 kk = j >> 1;
-    const u64 m = 2 * ((o ? t01 : t00) + (u64)kk * nw) + (u64)h;
-    const u32 code = (kk < (o ? nk1 : nk0) && m < count) ? 0u : kCodeSkip;
-    const u32 ring = sbase + kSmallRing + (o ? psecond : pfirst) * kSmallRingBytesPerWave;
-    if (l == 31u && j < T) lds_st64(ring + 8u * (2u * (kk & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
-  };
-  // the pair's next tile: lane 0's LDS atomic, issued a tile ahead; the ticket reaches the
-  // wave (ticket()) only where it is used, after the tile's lookups
-  const u32 pctr = sbase + (u32)small_lds_bytes() + 16u + 4u * pfirst;
-  // (inline asm: hipcc's atomic optimizer would broadcast the result inside the lane-0 branch,
-  // waiting for the LDS round trip right there)
-  auto draw = [&]() __attribute__((always_inline)) {
-    u32 t = 0;
-    if (lane == 0) asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(t) : "v"(pctr), "v"(2u) : "memory");
-    return t;
-  };
-  auto ticket = [&](u32 t) __attribute__((always_inline)) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t)::"memory");  // (the asm atomic is invisible to hipcc)
-    return (u32)__builtin_amdgcn_readfirstlane((int)t);
-  };
   // SLOT: lane i's message of the first window (fm): its record's prefix offset, and (after
   // the barrier) the prefix terms, from words loaded in the prologue
   u64 fpre = 0;
@@ -473,6 +415,25 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
     wave_lds_sync();
   };
+  // FAST waves' flush: one window (kf = 0), every code 0 (a whole aligned 4 KiB message: no
+  // padding, no mis) or none -- no long messages, no inverses, no prefix reload (r05y: 0.5-0.7 us
+  // per 65,536-slot list against the general flush).
+  auto flush_fast = [&](u32 nt) __attribute__((always_inline)) {
+    wave_lds_sync();
+    const u32 hh = (u32)lane & 1u, ti = (u32)lane >> 1;
+    const u64 e = lds_ld64(sring + 8u * (u32)lane);
+    const u32 v = (u32)e;
+    const bool live = ti < nt && (u32)(e >> 32) == 0u;
+    const u64 m = 2 * (t0 + (u64)ti * nw) + hh;
+    if constexpr (SLOT) {
+      const uint8_t* pfx = flive ? base + fpre - a.pdelta : safe;
+      // Z_0(crc_raw(H, payload)) = Z_4096(H) ^ V (mis = 0, p = 0)
+      const u32 R = opmul(sbase, kUniSlotOpZ4096, eH) ^ v;
+      slot_store(live, false, m, pfx, eF, eS, ehas, R);
+    } else {
+      if (live) a.out[m] = v ^ a.final_xor;
+    }
+  };
   constexpr u32 kWinMask = kSmallRingTiles - 1u;
 
   // Prologue: table loads, the window's records (and SLOT its prefix offsets); the LDS fill while
@@ -481,13 +442,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   wS = a.offsets[fmc * a.ostride];
   wL = a.lengths[fmc * a.lstride];
   if constexpr (SLOT) fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
-  if constexpr (kPair) {
-    pS = a.offsets[pfmc * a.ostride];
-    pL = a.lengths[pfmc * a.lstride];
-  }
   fill.store(sbase);
   if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
-  if (kPair && threadIdx.x < (u32)(NPW / 2)) lds_st(sbase + (u32)small_lds_bytes() + 16u + 4u * threadIdx.x, 4u);
   // FAST (wave-uniform): the window is every tile of the wave (at most 32: small_run's grid) and
   // each of its messages is a whole 4 KiB payload on a 16-B boundary (SLOT: within max_len) --
   // the fixed-size channel drain. Its loop is the uniform kernel's: the next tile's address from
@@ -497,10 +453,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // immediate offsets -- 67.5 against 44.1 us per 65,536 slots in the read probe, testutil.hip
   // slot_list_read_kernel modes 2 and 3 -- and its address and code arithmetic made the kernel
   // compute-bound, 6,759 VALU instructions per wave against the uniform kernel's 4,508.)
-  // (paired: over both windows, so the two waves of a pair decide alike)
   const bool conf = !flive || (wL == (u64)kSmallMaxExt && (wS & 15u) == 0 && (!SLOT || wL <= a.max_len));
-  const bool pconf = !kPair || !pflive || (pL == (u64)kSmallMaxExt && (pS & 15u) == 0 && (!SLOT || pL <= a.max_len));
-  const bool fast = nk <= kSmallRingTiles && (!kPair || pnk <= kSmallRingTiles) && __ballot(!conf || !pconf) == 0;
+  const bool fast = nk <= kSmallRingTiles && __ballot(!conf) == 0;
   if constexpr (probe) pt[1] = __builtin_amdgcn_s_memrealtime();
   u64 sA, LA, sB, LB;
   win_rec(0, sA, LA);
@@ -518,38 +472,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   if constexpr (SLOT && SUBSPACE_SMALL_VARIANT != 1) eH = span_hash(pwords, pmeta, eF, eS, ehas);
 
   u32 k = 0;
-  if (fast && kPair) {
-    // ping-pong, one tile in flight (crc_uniform.hip's loop) over the pair's tiles, two per
-    // iteration: A holds tile x0 (a wave's first: its own tile 0, the prologue's load), B gets
-    // x1, the next two come from one ticket (the pair's counter starts at 4: tiles 0-3 are the
-    // two waves' first two). One exit, at the top: a break between the halves gave the loop head
-    // a predecessor with B's loads pending, and hipcc then waited for the tile in flight at every
-    // iteration's head. A tile past the pair's last is a re-read of that tile, not stored.
-    // (the drain as a builtin s_waitcnt vmcnt(0), which hipcc's waitcnt pass sees)
-    auto drain = [&]() __attribute__((always_inline)) { __builtin_amdgcn_s_waitcnt(0x0F70); };
-    u32 x0 = second ? 1u : 0u, x1 = x0 + 2u;
-    u32 t = draw();
-    drain();  // tile 0 and the prologue's loads, before the loop (a clean loop-head state)
-    for (;;) {
-      if (x0 >= T) break;
-      const u64 qB = pair_off(x1);
-      issue_prio_hi();
-      drain();  // tile x0's lines
-      load_at(B, qB);
-      issue_prio_lo();
-      process_pair(A, x0);
-      const u32 y = ticket(t);
-      const u64 qA = pair_off(y);
-      issue_prio_hi();
-      drain();
-      load_at(A, qA);
-      issue_prio_lo();
-      t = draw();
-      process_pair(B, x1);
-      x0 = y;
-      x1 = y + 1u;
-    }
-  } else if (fast) {
+  if (fast) {
     // ping-pong, unrolled by two, one tile in flight (crc_uniform.hip's loop)
     for (; k + 1 < nk; k += 2) {
       const u64 qB = fast_off(k + 1);
@@ -601,11 +524,13 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
   }
   if constexpr (probe) pt[4] = __builtin_amdgcn_s_memrealtime();
-  // every wave of the workgroup: a pair's waves wrote into each other's rings
-  if constexpr (kPair) __syncthreads();
   if (nk && SUBSPACE_SMALL_VARIANT != 2) {
-    const u32 kf = (nk - 1u) & ~kWinMask;  // the last window, not flushed yet (FAST: 0)
-    flush(kf, nk - kf);
+    if (fast) {
+      flush_fast(nk);
+    } else {
+      const u32 kf = (nk - 1u) & ~kWinMask;  // the last window, not flushed yet
+      flush(kf, nk - kf);
+    }
   }
   if constexpr (probe) pt[5] = __builtin_amdgcn_s_memrealtime();
   if constexpr (SLOT) {

@@ -152,16 +152,21 @@ __global__ __launch_bounds__(512) void slot_list_read_kernel(const uint64_t* __r
       const gptr q = (gptr)(s + 128u * l);
 #pragma unroll
       for (int b = 0; b < 8; b++) D[b] = q[b];
+      asm volatile("" ::"v"(q));  // (no load's destination in its address VGPRs: crc_small.hip load_at)
     } else {
       u64 E = L + (s & 15u);
       E = E < 16 ? 16 : (E > 4096 ? 4096 : E);
       const u64 p0 = s & ~(u64)15;
       const u32 lastb = ((u32)E - 1u) & ~15u;
+      gptr q[8];
 #pragma unroll
       for (int b = 0; b < 8; b++) {
         const u32 off = 128u * l + 16u * (u32)b;
-        D[b] = *(gptr)(p0 + (off < lastb ? off : lastb));
+        q[b] = (gptr)(p0 + (off < lastb ? off : lastb));
+        D[b] = *q[b];
       }
+#pragma unroll
+      for (int b = 0; b < 8; b++) asm volatile("" ::"v"(q[b]));
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -224,7 +229,7 @@ int subspace_crc_testutil_slot_list_read(const void* dev_records, uint64_t count
   if (grid < 1) grid = 1;
   if (out_words < grid * 512) return -1;
   const auto* r = static_cast<const uint64_t*>(dev_records);
-  const size_t ldsb = lds ? subspace_amd::small_lds_bytes() + 32 : 0;
+  const size_t ldsb = lds ? subspace_amd::small_lds_bytes() + 16 : 0;
   const void* fns[5] = {(const void*)slot_list_read_kernel<0>, (const void*)slot_list_read_kernel<1>,
                         (const void*)slot_list_read_kernel<2>, (const void*)slot_list_read_kernel<3>,
                         (const void*)slot_list_read_kernel<4>};

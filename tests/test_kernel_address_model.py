@@ -432,62 +432,6 @@ def test_small_kernel_loads_stay_in_messages(seed, count, G):
                 assert covered.get(m) == set(range(s, s + L)), m
 
 
-
-def pair_fast_schedule(nk0, nk1, rng):
-    """Replays the paired FAST loop of crc32_small_kernel (crc_small.hip): the two waves of a
-    SIMD (first: nk0 tiles, second: nk1 = nk0 or nk0 - 1) share T = nk0 + nk1 tiles, tile j being
-    tile j >> 1 of wave j & 1; each wave starts with its tiles j = own and own + 2, then takes two
-    per ticket from the pair's LDS counter (starting at 4), in an arbitrary interleaving of the
-    waves. Returns [(computing wave, j, owner, k, stored)] for every tile processed, the loads'
-    tiles per wave (past the pair's last tile: the last tile's re-read)."""
-    T = nk0 + nk1
-    counter = [4]
-    state = {}
-    for w in (0, 1):
-        state[w] = {"x0": w, "x1": w + 2, "t": None, "done": False, "phase": "draw"}
-    out, loads = [], {0: [], 1: []}
-
-    def clamp(j):
-        return j if j < T else max(T - 1, 0)
-    while not all(st["done"] for st in state.values()):
-        w = int(rng.integers(0, 2))
-        st = state[w]
-        if st["done"]:
-            continue
-        if st["phase"] == "draw":  # the ticket for the next two (issued a tile ahead)
-            st["t"] = counter[0]
-            counter[0] += 2
-            st["phase"] = "run"
-            continue
-        if st["x0"] >= T:
-            st["done"] = True
-            continue
-        for j in (st["x0"], st["x1"]):
-            loads[w].append(clamp(j))
-            stored = j < T
-            out.append((w, j, j & 1, j >> 1, stored))
-        y = st["t"]
-        st["x0"], st["x1"] = y, y + 1
-        st["phase"] = "draw"
-    return out, loads
-
-
-@pytest.mark.parametrize("nk0,nk1", [(16, 16), (16, 15), (1, 0), (1, 1), (2, 1), (3, 3), (32, 32), (32, 31), (0, 0)])
-def test_pair_fast_tiles_stored_exactly_once(nk0, nk1):
-    """The paired FAST loop stores every tile of both waves exactly once -- into its owner's
-    ring entry -- whichever wave computes it and in whatever order the tickets are drawn, and
-    stores nothing for tickets past the pair's tiles; every load is one of the pair's tiles."""
-    for seed in range(20):
-        out, loads = pair_fast_schedule(nk0, nk1, np.random.default_rng(seed))
-        stored = [(o, k) for _, _, o, k, st in out if st]
-        assert sorted(stored) == sorted([(0, k) for k in range(nk0)] + [(1, k) for k in range(nk1)])
-        T = nk0 + nk1
-        for w in (0, 1):
-            assert all(0 <= j < max(T, 1) for j in loads[w])
-        # an owner's k stays inside its 32-tile ring window
-        assert all(k < 32 for _, _, _, k, st in out if st)
-
-
 def fast_line_blocks(s, l):
     """The FAST loop's 8 loads of lane l (one address, immediate offsets 0..112)."""
     return [s + 128 * l + 16 * b for b in range(8)]

@@ -23,6 +23,8 @@ counters() {
     p1) echo "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT" ;;
     p2) echo "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VMEM" ;;
     p3) echo "SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_IFETCH SQ_WAIT_INST_ANY SQ_INSTS_VMEM_WR" ;;
+    ic1) echo "SQC_ICACHE_HITS SQC_ICACHE_MISSES" ;;
+    ic2) echo "SQC_ICACHE_MISSES_DUPLICATE SQC_TC_INST_REQ" ;;
     f) echo "FETCH_SIZE" ;;
     w) echo "WRITE_SIZE" ;;
   esac
