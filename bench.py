@@ -801,6 +801,18 @@ def slot_configs(ctx, dev, iters) -> dict:
     torch.cuda.synchronize()
     list_kernel = "subspace_crc32_slots: subspace_amd::crc32_small_kernel<512, true> (one launch, slots finished in it; " \
                   "crc_small.hip)"
+    # the slot-list access shape's own read ceiling: the kernel's FAST-loop loads over the same
+    # rotated shuffled lists, no CRC (gpu.slot_list_read mode 4)
+    sink = torch.empty(256 * 512, dtype=torch.int32, device=dev)
+    j = [0]
+
+    def probe():
+        gpu.slot_list_read(d_recs[j[0] % nbuf], n, sink, mode=4)
+        j[0] += 1
+    pms = time_calls(probe, 400)
+    ceiling = {"GBps": round(nbytes / (pms * 1e-3) / 1e9, 1), "us_per_launch": round(pms * 1e3, 2),
+               "kernel": "slot_list_read_kernel<4> (testutil.hip): the small kernel's FAST-loop loads and first-window "
+                         "prefix words over the same rotated shuffled lists, no CRC"}
     for mode, key in ((gpu.SLOT_CALCULATE, "S_list_publish"), (gpu.SLOT_VERIFY, "S_list_verify")):
         i = [0]
         errs.zero_()
@@ -830,7 +842,9 @@ def slot_configs(ctx, dev, iters) -> dict:
                         "order, one per channel copy, 4 copies rotated, " +
                         ("publish" if mode == gpu.SLOT_CALCULATE else "verify"),
             "check": check})
-    del bufs, d_recs
+        res[key]["roofline"]["read_ceiling"] = ceiling
+        res[key]["roofline"]["frac_of_read_ceiling"] = round(pms / ms, 4)
+    del bufs, d_recs, sink
     # S_meta: 16 B of user metadata per slot (SetMetadataSize, client/options.h:375-391):
     # ComputePrefixSize(4, 16) = 128, stride 4,224; spans 44 + 16 + 4,096 B
     cs, ms_ = 4, 16

@@ -209,6 +209,17 @@ def fill_ragged(buf, offsets, lengths, *, seed: int, first_id: int = 0, id_strid
         _stream_ptr(stream)), "fill_ragged")
 
 
+def slot_list_read(records, count: int, out, mode: int = 4, stride: int = 0, lds: bool = True, stream=None) -> None:
+    """Slot-list read ceiling probe (testutil.hip slot_list_read_kernel): the small-message
+    kernel's loads over `count` device subspace_crc_slot records -- mode 4 = its FAST loop's (the
+    window's records in registers, one address and 8 immediate offsets per tile, the first
+    window's prefix words) -- with an XOR fold instead of the CRC; out: int32 device tensor of at
+    least the kernel's grid x 512 words (256 * 512 covers every count up to 2^22 slots)."""
+    _check(_lib.load().subspace_crc_testutil_slot_list_read(
+        _ptr(records), int(count), int(mode), int(stride), 1 if lds else 0, _ptr(out), int(out.numel()),
+        _stream_ptr(stream)), "slot_list_read")
+
+
 def stream_read(buf, out, stream=None) -> None:
     """Streaming-read ceiling probe over buf (the CRC kernels' load shape, no CRC);
     out: int32 device tensor of 256 * 512 words."""

@@ -12,6 +12,7 @@
 Each mode runs `settle` untimed launches then `launches` more, and prints one JSON line with
 the event-timed mean of the latter (the PMC passes read the per-dispatch counters)."""
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -28,6 +29,9 @@ def main():
     count, nb = 65536, 5
     ctx = gpu.CrcContext(0)
     lib = _lib.load()
+    wg = int(os.environ.get("UNIFORM_WG", "512"))  # the tuning hook's workgroup size (512: the product's)
+    if wg != 512 and lib.subspace_crc_testutil_tune(ctx._h, wg, 0, 0) != 0:
+        raise SystemExit(f"tune failed: {_lib.last_error()}")
     dev = torch.device("cuda", 0)
     bufs = [torch.empty(count * 4096, dtype=torch.uint8, device=dev) for _ in range(nb)]
     for k, b in enumerate(bufs):
@@ -57,7 +61,7 @@ def main():
     b.record()
     torch.cuda.synchronize()
     us = a.elapsed_time(b) * 1e3 / launches
-    line = {"mode": mode, "launches": launches, "settle": settle, "us_per_launch": round(us, 3),
+    line = {"mode": mode, "wg": wg, "launches": launches, "settle": settle, "us_per_launch": round(us, 3),
             "GBps": round(count * 4096 / us / 1e3, 1)}
     if mode == "l2":  # every message is message 0 of batch 0
         line["alias_crc_equal"] = bool((out == out[0]).all().item())
