@@ -629,13 +629,6 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
       for (int n = 0; n < 16; n++)
         for (int cp = 0; cp < 4; cp++) laneops[128 * kUniSlotOpZ64 + k * 64 + n * 4 + cp] = nt[k * 16 + n];
   }
-  {  // Z_32, replicated 4x the same way (crc_device.h kUniSlotOpZ32)
-    u32 nt[128];
-    nibble_tables(z_bytes(c->host_tab, 32), nt);
-    for (int k = 0; k < 8; k++)
-      for (int n = 0; n < 16; n++)
-        for (int cp = 0; cp < 4; cp++) laneops[128 * kUniSlotOpZ32 + k * 64 + n * 4 + cp] = nt[k * 16 + n];
-  }
   nibble_tables(z_bytes(c->host_tab, 4096), &rops[kLaneOpWords]);
   for (int k = 0; k < 31; k++)
     nibble_tables(z_bytes(c->host_tab, 8192ull << k),

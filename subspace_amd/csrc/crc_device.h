@@ -39,10 +39,7 @@ constexpr int kUniSlotOpZ4096 = kLaneOpWords * 4 / 512;  // opmul slot 32
 // reading copy l & 3 (conflict-free): the join of a line's two 64-B chains (two-chain line
 // CRC)
 constexpr int kUniSlotOpZ64 = kUniSlotOpZ4096 + 1;
-// slots 37..40: Z_32 replicated 4x the same way: the four-chain line CRC of a wave's last tile
-// (crc_uniform.hip SUBSPACE_LAST4)
-constexpr int kUniSlotOpZ32 = kUniSlotOpZ64 + 4;
-constexpr int kUniOpSlots = kUniSlotOpZ32 + 4;
+constexpr int kUniOpSlots = kUniSlotOpZ64 + 4;
 constexpr int kUniOpSlotsOneChain = kUniSlotOpZ4096 + 1;
 constexpr u32 kUniRing = kLdsOps + kUniOpSlots * 512u;
 // results per wave ring: 256 (128 tiles), or 128 where 16 waves' rings would not fit
@@ -352,25 +349,6 @@ __device__ __forceinline__ u32 line_crc32_2chain(const u32x4 (&d)[8], u32 init, 
     y = step4n(y, lc0, lc1, w < 15 ? d[(w + 17) >> 2][(w + 17) & 3] : 0u);
   }
   return opmul_z64(z64, x) ^ y;
-}
-
-// The same CRC as four independent 8-step chains (bytes 0..31 from `init`, the other three
-// quarters from 0) joined by linearity: Z_96(c0) ^ Z_64(c1) ^ Z_32(c2) ^ c3 =
-// Z_64(Z_32(c0) ^ c1) ^ Z_32(c2) ^ c3 -- half the two-chain form's dependent steps for 16 more
-// conflict-free lookups (z32, z64: the 4x replicated tables' bases + 4 * (lane & 3)).
-__device__ __forceinline__ u32 line_crc32_4chain(const u32x4 (&d)[8], u32 init, u32 lc0, u32 lc1, u32 z32, u32 z64) {
-  u32 c[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) c[j] = d[2 * j][0] ^ (j == 0 ? init : 0u);
-#pragma unroll
-  for (int w = 0; w < 8; w++) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int i = 8 * j + w + 1;  // the next data word of chain j
-      c[j] = step4n(c[j], lc0, lc1, w < 7 ? d[i >> 2][i & 3] : 0u);
-    }
-  }
-  return opmul_z64(z64, opmul_z64(z32, c[0]) ^ c[1]) ^ opmul_z64(z32, c[2]) ^ c[3];
 }
 
 // CRC of one 128-B line (8 x 16 B), from state `init`: 32 steps of step4n.

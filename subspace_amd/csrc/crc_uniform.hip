@@ -49,18 +49,6 @@
 #ifndef SUBSPACE_SLOT_VARIANT
 #define SUBSPACE_SLOT_VARIANT 0
 #endif
-// A wave's last tile -- computed with nothing in flight -- as four 8-step chains per line
-// (crc_device.h line_crc32_4chain) instead of two 16-step ones (A/B builds).
-#ifndef SUBSPACE_LAST4
-#define SUBSPACE_LAST4 0
-#endif
-// The two waves of a SIMD share their tiles through an LDS ticket counter (crc_small.hip's
-// paired FAST loop) when every wave's tiles fit one ring window (A/B builds; the counters use
-// the unfilled Z_32 slots, so not with LAST4).
-#ifndef SUBSPACE_UNI_PAIR
-#define SUBSPACE_UNI_PAIR 0
-#endif
-static_assert(!(SUBSPACE_UNI_PAIR && SUBSPACE_LAST4), "UNI_PAIR keeps its counters in the Z_32 slots");
 
 namespace subspace_amd {
 
@@ -85,8 +73,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   // four pairs); bit-exact.
   constexpr bool kTwoChain = true;  // (false: the one-chain line CRC, for A/B builds)
   // step tables, per-lane operators, Z_4096 and Z_64 (the two-chain line CRC's join)
-  // (the Z_32 slots only for LAST4 builds)
-  LdsFill<WG, kTwoChain ? (SUBSPACE_LAST4 != 0 ? kUniOpSlots : kUniSlotOpZ32) : kUniOpSlotsOneChain> fill;
+  LdsFill<WG, kTwoChain ? kUniOpSlots : kUniOpSlotsOneChain> fill;
   fill.load(gtab, gops);
 
   const int lane = threadIdx.x & 63;
@@ -163,7 +150,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
 #pragma unroll
     for (int i = 0; i < 8; i++) d[i] = q[i];
     // the address live past the last load, so that its VGPRs are never that load's destination
-    // (crc_small.hip load_at: ~8 us per 65,536-slot call there)
+    // (the 768- and 1,024-thread instantiations had such a load)
     asm volatile("" ::"v"(q));
     // keep the loads at this point, in order (hipcc otherwise sinks them into the compute)
     __builtin_amdgcn_sched_barrier(0);
@@ -184,11 +171,6 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   auto line_crc = [&](const u32x4 (&d)[8]) {
     if constexpr (kTwoChain) return line_crc32_2chain(d, s_init, lc0, lc1, z64);
     else return line_crc32(d, s_init, lc0, lc1);
-  };
-  const u32 z32 = sbase + kLdsOps + 512u * (u32)kUniSlotOpZ32 + 4u * (u32)(lane & 3);
-  auto line_crc_last = [&](const u32x4 (&d)[8]) {
-    if constexpr (SUBSPACE_LAST4 != 0) return line_crc32_4chain(d, s_init, lc0, lc1, z32, z64);
-    else return line_crc(d);
   };
   // Message CRCs of tile k: into ring slots 2*(k - kf) + h (kf = first tile of the window);
   // SLOT: into the tagged ring entry 2*k + h (k < kSlotRingRounds), as CRC | k << 32.
@@ -231,9 +213,6 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
     for (u32 i = threadIdx.x; i < kEntries; i += WG) lds_st64(sbase + kUniSlotRing + 8u * i, ~0ull);
     if (threadIdx.x == 0) lds_st(smism, 0u);
   }
-#if SUBSPACE_UNI_PAIR
-  if (threadIdx.x < 4) lds_st(sbase + kLdsOps + 512u * (u32)kUniSlotOpZ32 + 4u * threadIdx.x, 4u);
-#endif
   __syncthreads();
   // Wait for tile 0 right here (the loop's first drain is then a no-op). Waves without tiles
   // run through the loop without iterations rather than returning early: the early return
@@ -256,80 +235,7 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
   constexpr u32 kWin = SLOT ? ~0u : (u32)(kRing / 2);
   u32 k = 0, kf = 0;
   u64 pt_finish = 0;  // PROBE, SLOT: when a finishing wave began
-#if SUBSPACE_UNI_PAIR
-  // paired: grid-uniform (every wave's tiles within one ring window, order 0, no slots)
-  const u32 nkmax = (u32)((ntiles + nw - 1) / nw);
-  const bool paired = !SLOT && !PROBE && NPW == 8 && order == 0 && nkmax <= kWin;
-  if (paired) {
-    const u32 pfirst = (u32)wid & 3u, psecond = pfirst + 4u;
-    const bool second = (u32)wid >= 4u;
-    const u32 pwid = second ? pfirst : psecond;
-    const u64 pt0 = front_slot(blockIdx.x, gridDim.x, pwid);
-    const u32 pnk = pt0 < ntiles ? ((u32)(ntiles - pt0) + (u32)nw - 1u) / (u32)nw : 0u;
-    const u32 T = nk + pnk;
-    const u64 t00 = second ? pt0 : t0, t01 = second ? t0 : pt0;
-    const u32 ctr = sbase + kLdsOps + 512u * (u32)kUniSlotOpZ32 + 4u * pfirst;
-    auto pair_off = [&](u32 j) {
-      const u32 jj = j < T ? j : (T ? T - 1u : 0u);
-      const u64 tt = ((jj & 1u) ? t01 : t00) + (u64)(jj >> 1) * nw;
-      u64 msg = 2 * tt + (u64)h;
-      msg = msg < count ? msg : msg - 1;
-      u64 off = msg * stride + (u64)l * 128;
-      asm volatile("" : "+v"(off));
-      return off;
-    };
-    auto pair_result = [&](u32 crc, u32 j) {
-      u32 v = lane_shift(lop, crc);
-      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
-      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
-      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
-      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
-      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-      const u32 oring = sbase + kUniRing + ((j & 1u) ? psecond : pfirst) * (4u * kRing);
-      if (l == 31 && j < T) lds_st(oring + 4u * (2u * (j >> 1) + (u32)h), v ^ final_xor);
-    };
-    auto draw = [&]() {
-      u32 t = 0;
-      if (lane == 0) asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(t) : "v"(ctr), "v"(2u) : "memory");
-      return t;
-    };
-    auto ticket = [&](u32 t) {
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t)::"memory");
-      return (u32)__builtin_amdgcn_readfirstlane((int)t);
-    };
-    auto drain = [&]() { __builtin_amdgcn_s_waitcnt(0x0F70); };
-    // the counters were set to 4 before the prologue's barrier; A holds tile 0 (landed)
-    u32 x0 = second ? 1u : 0u, x1 = x0 + 2u;
-    u32 t = draw();
-    drain();
-    for (;;) {
-      if (x0 >= T) break;
-      const u64 qB = pair_off(x1);
-      issue_prio_hi();
-      drain();
-      load_at(B, qB);
-      issue_prio_lo();
-      pair_result(line_crc(A), x0);
-      const u32 y = ticket(t);
-      const u64 qA = pair_off(y);
-      issue_prio_hi();
-      drain();
-      load_at(A, qA);
-      issue_prio_lo();
-      t = draw();
-      if (x1 < T) pair_result(line_crc(B), x1);  // (a ticket's second tile past the last: nothing)
-      x0 = y;
-      x1 = y + 1u;
-    }
-    __syncthreads();  // the partners wrote into each other's rings
-    k = nk;           // every tile of this wave is in its ring (kf = 0): the final flush below
-  }
-  // (LAST4: the loop leaves the last one or two tiles to the tail below)
-  for (; !paired && k + 1 + (SUBSPACE_LAST4 != 0) < nk; k += 2) {
-#else
-  // (LAST4: the loop leaves the last one or two tiles to the tail below)
-  for (; k + 1 + (SUBSPACE_LAST4 != 0) < nk; k += 2) {
-#endif
+  for (; k + 1 < nk; k += 2) {
     const u64 qB = addr_before_wait(k + 1);
     issue_prio_hi();
     drain_before_issue();
@@ -349,27 +255,13 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
     tile_result(line_crc(B), k + 1, kf);
   }
   if constexpr (PROBE) pt[2] = __builtin_amdgcn_s_memrealtime();
-  if (SUBSPACE_LAST4 != 0 && k + 1 < nk) {  // LAST4: the last two tiles, the last one four-chain
-    const u64 qB = addr_before_wait(k + 1);
-    issue_prio_hi();
-    drain_before_issue();
-    load_at(B, qB);
-    issue_prio_lo();
+  if (k < nk) {  // odd last tile, already loaded
     if (!SLOT && k - kf == kWin) {
       wave_lds_sync();
       flush(kf, kRing / 2);
       kf = k;
     }
     tile_result(line_crc(A), k, kf);
-    drain_before_issue();
-    tile_result(line_crc_last(B), k + 1, kf);
-  } else if (k < nk) {  // odd last tile, already loaded
-    if (!SLOT && k - kf == kWin) {
-      wave_lds_sync();
-      flush(kf, kRing / 2);
-      kf = k;
-    }
-    tile_result(line_crc_last(A), k, kf);
   }
   wave_lds_sync();
   if constexpr (SLOT) {

@@ -5,6 +5,8 @@ quad-cycle split (ACTIVE_INST_ANY + WAIT_ANY + WAIT_INST_ANY = WAVE_CYCLES), LDS
 CU and per tile, and the event-timed launch time of each mode.
 
   python tools/summarize_ledger.py gpurun_out/<tag> > profiles/r04/<name>.json
+  python tools/summarize_ledger.py gpurun_out/<tag> list,ordered,alias,probe4,probe4o \
+      crc32_small_kernel,slot_list_read          (LEDGER=small: the slot-list drain, r05)
 """
 import collections
 import csv
@@ -15,6 +17,9 @@ from pathlib import Path
 CUS, TILES = 256, 32768  # config B: 65,536 messages = 32,768 tiles of 8 KiB per launch
 
 
+KERNELS = ("uniform4k", "stream_read")
+
+
 def mode_counters(root: Path, mode: str) -> dict:
     tot, n = collections.defaultdict(float), collections.Counter()
     for d in sorted(root.glob(f"{mode}_p*")):
@@ -22,16 +27,20 @@ def mode_counters(root: Path, mode: str) -> dict:
         if not f.exists():
             continue
         for r in csv.DictReader(open(f)):
-            if "uniform4k" in r["Kernel_Name"] or "stream_read" in r["Kernel_Name"]:
+            if any(k in r["Kernel_Name"] for k in KERNELS):
                 tot[r["Counter_Name"]] += float(r["Counter_Value"])
                 n[r["Counter_Name"]] += 1
     return {c: tot[c] / n[c] for c in sorted(tot)}
 
 
 def main():
+    global KERNELS
     root = Path(sys.argv[1])
-    out = {"source": str(root), "modes": {}}
-    for mode in ("hbm", "l2", "read"):
+    modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["hbm", "l2", "read"]
+    if len(sys.argv) > 3:
+        KERNELS = tuple(sys.argv[3].split(","))
+    out = {"source": str(root), "kernels": list(KERNELS), "modes": {}}
+    for mode in modes:
         c = mode_counters(root, mode)
         t = root / f"{mode}_t.json"
         entry = {"timing": json.loads(t.read_text()) if t.exists() else None, "counters": c}
