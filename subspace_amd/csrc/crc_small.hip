@@ -252,11 +252,15 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       const u32 lastb = (len - 1u) & ~15u;
       const uint8_t* pj = p0 + (j << 13);
       u32x4 d[8];
+      const u32x4* q[8];
 #pragma unroll
       for (int b = 0; b < 8; b++) {
         const u32 off = 128u * (u32)lane + 16u * (u32)b;
-        d[b] = *reinterpret_cast<const u32x4*>(pj + (off < lastb ? off : lastb));
+        q[b] = reinterpret_cast<const u32x4*>(pj + (off < lastb ? off : lastb));
+        d[b] = *q[b];
       }
+#pragma unroll
+      for (int b = 0; b < 8; b++) asm volatile("" ::"v"(q[b]));  // (load_lines)
       const bool hd = j == 0 && mis != 0u && lane == 0;
       if (__any(hd || len < 8192u)) {
         const int v0 = (int)len - 128 * lane;
@@ -448,11 +452,10 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // each of its messages is a whole 4 KiB payload on a 16-B boundary (SLOT: within max_len) --
   // the fixed-size channel drain. Its loop is the uniform kernel's: the next tile's address from
   // the window's records before the wait, one address and 8 loads at immediate offsets, no
-  // clamps, codes or records in the loop. (Measured on config S's channel, r05c: the general
-  // loop's 8 clamped per-block addresses read the same bytes ~50 % slower than one address with
-  // immediate offsets -- 67.5 against 44.1 us per 65,536 slots in the read probe, testutil.hip
-  // slot_list_read_kernel modes 2 and 3 -- and its address and code arithmetic made the kernel
-  // compute-bound, 6,759 VALU instructions per wave against the uniform kernel's 4,508.)
+  // clamps, codes or records in the loop. (Config S's channel as a shuffled slot list: 53.0 against
+  // the general loop's 60.8 us per 65,536 slots, compute only 36.5 against 45.7 us -- its address
+  // and code arithmetic, 6,759 VALU instructions per wave against the uniform kernel's 4,508;
+  // r05z)
   const bool conf = !flive || (wL == (u64)kSmallMaxExt && (wS & 15u) == 0 && (!SLOT || wL <= a.max_len));
   const bool fast = nk <= kSmallRingTiles && __ballot(!conf) == 0;
   if constexpr (probe) pt[1] = __builtin_amdgcn_s_memrealtime();

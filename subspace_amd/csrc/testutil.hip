@@ -98,6 +98,8 @@ __global__ __launch_bounds__(512) void stream_read_lds_kernel(const u32x4* __res
 //   3  as 2, one address and 8 immediate offsets (crc_uniform.hip's load issue)
 //   4  the window's records in registers, one address and 8 immediate offsets (crc_small.hip's
 //      FAST loop)
+//   5  as 4 with two tiles in flight per wave (three line buffers)
+//   6  as 3 with two tiles in flight per wave
 template <int MODE>
 __global__ __launch_bounds__(512) void slot_list_read_kernel(const uint64_t* __restrict__ recs, uint64_t count,
                                                              uint64_t stride, unsigned* __restrict__ out) {
@@ -114,7 +116,8 @@ __global__ __launch_bounds__(512) void slot_list_read_kernel(const uint64_t* __r
   const u64 fm = 2 * (t0 + (u64)((u32)lane >> 1) * nw) + ((u32)lane & 1u);
   const u64 fmc = fm < count ? fm : count - 1;
   u64 wS = 0, wL = 0;
-  if (MODE == 1 || MODE == 4) {
+  constexpr bool kRegs = MODE == 1 || MODE == 4 || MODE == 5;
+  if (kRegs) {
     wS = recs[3 * fmc + 1];
     wL = recs[3 * fmc + 2];
   }
@@ -122,7 +125,7 @@ __global__ __launch_bounds__(512) void slot_list_read_kernel(const uint64_t* __r
   const u64 fpre = recs[3 * fmc];
   auto fetch = [&](u32 k, u64& s, u64& L) {
     const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
-    if (MODE == 1 || MODE == 4) {
+    if (kRegs) {
       const int i0 = (int)(2u * kk);
       const u64 s0 = ((u64)(u32)__builtin_amdgcn_readlane((int)(wS >> 32), i0) << 32) |
                      (u64)(u32)__builtin_amdgcn_readlane((int)(u32)wS, i0);
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(512) void slot_list_read_kernel(const uint64_t* __r
       if (MODE == 0) {
         s = recs[3 * m + 1];
         L = recs[3 * m + 2];
-      } else {
+      } else {  // modes 2, 3, 6
         s = s00 + m * stride;
         L = 4096;
       }
@@ -175,6 +178,44 @@ __global__ __launch_bounds__(512) void slot_list_read_kernel(const uint64_t* __r
 #pragma unroll
     for (int b = 0; b < 8; b++) acc ^= D[b].x ^ D[b].y ^ D[b].z ^ D[b].w;
   };
+  if constexpr (MODE >= 5) {
+    // two tiles in flight: wait until at most one tile's 8 loads are outstanding
+    auto wait_one = []() { __builtin_amdgcn_s_waitcnt(0x0F78); };  // vmcnt(8)
+    u32x4 A[8], B[8], C[8];
+    u64 s, L;
+    fetch(0, s, L);
+    load_lines(A, s, L);
+    fetch(1, s, L);
+    load_lines(B, s, L);
+    {
+      const __attribute__((address_space(1))) uint64_t* q = (const __attribute__((address_space(1))) uint64_t*)fpre;
+      uint64_t x = 0;
+#pragma unroll
+      for (int i = 0; i < 7; i++) x ^= q[i];
+      acc ^= (unsigned)x ^ (unsigned)(x >> 32);
+    }
+    u32 k = 0;
+    for (; k + 2 < nk; k += 3) {
+      wait_one();
+      fetch(k + 2, s, L);
+      load_lines(C, s, L);
+      fold(A);
+      wait_one();
+      fetch(k + 3, s, L);
+      load_lines(A, s, L);
+      fold(B);
+      wait_one();
+      fetch(k + 4, s, L);
+      load_lines(B, s, L);
+      fold(C);
+    }
+    subspace_amd::drain_before_issue();
+    if (k < nk) fold(A);
+    if (k + 1 < nk) fold(B);
+    if (acc == 0x12345678u && count == 1) lds_unused2[threadIdx.x] = acc;  // (keeps the allocation)
+    out[blockIdx.x * 512 + threadIdx.x] = acc;
+    return;
+  }
   u64 sA, LA, sB, LB;
   fetch(0, sA, LA);
   fetch(1, sB, LB);
@@ -217,7 +258,7 @@ extern "C" {
 // out_words >= grid * 512 words, grid = the small-message kernel's for this count on this device.
 int subspace_crc_testutil_slot_list_read(const void* dev_records, uint64_t count, uint32_t mode, uint64_t stride,
                                          uint32_t lds, unsigned* dev_out, uint64_t out_words, void* stream) {
-  if (!dev_records || !dev_out || count == 0 || mode > 4) return -1;
+  if (!dev_records || !dev_out || count == 0 || mode > 6) return -1;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return -2;
@@ -230,9 +271,10 @@ int subspace_crc_testutil_slot_list_read(const void* dev_records, uint64_t count
   if (out_words < grid * 512) return -1;
   const auto* r = static_cast<const uint64_t*>(dev_records);
   const size_t ldsb = lds ? subspace_amd::small_lds_bytes() + 16 : 0;
-  const void* fns[5] = {(const void*)slot_list_read_kernel<0>, (const void*)slot_list_read_kernel<1>,
+  const void* fns[7] = {(const void*)slot_list_read_kernel<0>, (const void*)slot_list_read_kernel<1>,
                         (const void*)slot_list_read_kernel<2>, (const void*)slot_list_read_kernel<3>,
-                        (const void*)slot_list_read_kernel<4>};
+                        (const void*)slot_list_read_kernel<4>, (const void*)slot_list_read_kernel<5>,
+                        (const void*)slot_list_read_kernel<6>};
   if (hipFuncSetAttribute(fns[mode], hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsb) != hipSuccess) return -2;
   const hipStream_t st = (hipStream_t)stream;
   switch (mode) {
@@ -240,7 +282,9 @@ int subspace_crc_testutil_slot_list_read(const void* dev_records, uint64_t count
     case 1: slot_list_read_kernel<1><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
     case 2: slot_list_read_kernel<2><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
     case 3: slot_list_read_kernel<3><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
-    default: slot_list_read_kernel<4><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
+    case 4: slot_list_read_kernel<4><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
+    case 5: slot_list_read_kernel<5><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
+    default: slot_list_read_kernel<6><<<(unsigned)grid, 512, ldsb, st>>>(r, count, stride, dev_out); break;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -20,6 +20,7 @@ subspace_crc32_slots (the small-message kernel, crc_small.hip) or read by the pr
               probe3n without the kernel's LDS allocation
   probe4   -- the window's records in registers, one address and immediate offsets (the
               small kernel's FAST loop), shuffled; probe4o ordered, probe4n ordered without LDS
+  probe5   -- probe4 with two tiles in flight per wave (probe5o ordered); probe6: probe3 so
   list_ns, ordered_ns, strided_ns -- the same without the per-slot status array (the
               mismatch count only)
   strided  -- the fused uniform slot kernel (subspace_crc32_slots_strided), verify, rotated:
@@ -107,6 +108,9 @@ def main():
         "probe4": lambda i: probe(shuffled[i % NB], 4),
         "probe4o": lambda i: probe(ordered[i % NB], 4),
         "probe4n": lambda i: probe(ordered[i % NB], 4, 0),
+        "probe5": lambda i: probe(shuffled[i % NB], 5),
+        "probe5o": lambda i: probe(ordered[i % NB], 5),
+        "probe6": lambda i: probe(ordered[i % NB], 6),
         "strided": lambda i: ctx.crc32_slots_strided(bufs[i % NB], stride, N, message_size=SIZE, checksum_size=CS,
                                                      metadata_size=MS, mode=gpu.SLOT_VERIFY, status=status,
                                                      error_count=errs),

@@ -18,13 +18,13 @@ from pathlib import Path
 LOAD = re.compile(r"(global|buffer|flat)_load_dword\w*\s+v\[(\d+):(\d+)\],\s*(?:v\[(\d+):(\d+)\]|v(\d+))")
 
 
-def main():
-    every = "--all" in sys.argv  # also single-dword and 64-bit loads (records, prefix words)
-    src, flags = sys.argv[1], [f for f in sys.argv[2:] if f != "--all"]
+def overlaps(src, flags=(), every=False):
+    """{kernel: (overlapping loads, loads)} for the gfx950 device code of `src` (16-B loads only
+    unless every)."""
     with tempfile.TemporaryDirectory() as d:
         co = Path(d) / "k.co"
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only",
-                        "--no-gpu-bundle-output", *flags, "-c", src, "-o", str(co)], check=True)
+                        "--no-gpu-bundle-output", *flags, "-c", str(src), "-o", str(co)], check=True)
         dis = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "-d", str(co)], check=True,
                              capture_output=True, text=True).stdout
     kernel, loads, over = None, Counter(), Counter()
@@ -39,9 +39,16 @@ def main():
             loads[kernel] += 1
             if not (a1 < d0 or a0 > d1):
                 over[kernel] += 1
-    for k in loads:
-        print(f"{over[k]:4d} of {loads[k]:4d} loads overlap  {k}")
-    return 1 if sum(over.values()) else 0
+    return {k: (over[k], loads[k]) for k in loads}
+
+
+def main():
+    every = "--all" in sys.argv  # also single-dword and 64-bit loads (records, prefix words)
+    src, flags = sys.argv[1], [f for f in sys.argv[2:] if f != "--all"]
+    res = overlaps(src, flags, every)
+    for k, (o, n) in res.items():
+        print(f"{o:4d} of {n:4d} loads overlap  {k}")
+    return 1 if any(o for o, _ in res.values()) else 0
 
 
 if __name__ == "__main__":
