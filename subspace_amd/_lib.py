@@ -108,6 +108,10 @@ def load() -> ctypes.CDLL:
     lib.subspace_crc_testutil_stream_read_lds.argtypes = [vp, u64, vp, ctypes.c_uint32, vp]
     lib.subspace_crc_testutil_uniform_alias.restype = i32
     lib.subspace_crc_testutil_uniform_alias.argtypes = [vp, vp, u64, vp, vp]
+    lib.subspace_crc_testutil_probe.restype = i32
+    lib.subspace_crc_testutil_probe.argtypes = [vp, vp]
+    lib.subspace_crc_testutil_probe_waves.restype = u64
+    lib.subspace_crc_testutil_probe_waves.argtypes = [vp, u64]
     if hasattr(lib, "subspace_crc_testutil_slot_list_read"):  # (absent from older A/B builds)
         lib.subspace_crc_testutil_slot_list_read.restype = i32
         lib.subspace_crc_testutil_slot_list_read.argtypes = [vp, u64, u32, u64, u32, vp, u64, vp]
