@@ -43,7 +43,7 @@ __global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* o
 template <int WG>
 __global__ void crc32_long_kernel(const uint8_t*, u64, u32, u32, const u32*, const u32*, u32, u32, u32*, u32);
 __global__ void crc32_long_final_kernel(const u32*, const u32*, u32, u32, u32, u32, u32*, u64*, u64, u32*);
-template <int WG, bool SLOT, bool PROBE>
+template <int WG, bool SLOT, bool PROBE, int G>
 __global__ void crc32_small_kernel(const u32*, const u32*, SmallArgs);
 
 }  // namespace subspace_amd
@@ -456,10 +456,21 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
 // they start on 16-B boundaries, else 4,081 (the extended length adds offset & 15).
 bool small_fits(u64 max_len, bool aligned16) { return max_len <= (aligned16 ? kSmallMaxExt : kSmallMaxExt - 15); }
 
-// Small-message path (crc_small.hip): messages of at most 4 KiB two to a tile in one kernel
-// (the last workgroup computes any message longer than a half-tile). Same arguments and
-// results as ragged_run; with `slot` the kernel also finishes the slots (span terms, flag +
-// checksum or status, mismatch count) and `out` is unused.
+// Lanes per message for the small-message kernel (crc_small.hip G): the smallest power of two
+// whose 128-B lines hold `max_ext` extended bytes (a message's length + its start & 15), at
+// most 32 (a half-tile). A longer message than the bound is still computed whole (long path).
+u32 small_lanes(u64 max_ext) {
+  u32 g = 1;
+  while (g < 32 && 128ull * g < max_ext) g <<= 1;
+  return g;
+}
+
+// Small-message path (crc_small.hip): messages of at most 4 KiB in one kernel, g lanes (128-B
+// lines) per message, 64 / g messages per tile (a message longer than its g lines is computed
+// whole by its wave's flush). Same arguments and results as ragged_run (offsets == null: a
+// uniform batch, message m at base + m * ustride, ulen bytes); with `slot` the kernel also
+// finishes the slots (span terms, flag + checksum or status, mismatch count) and `out` is
+// unused.
 struct SmallSlot {
   const u64* prefixes;
   u32 pstride;
@@ -471,8 +482,10 @@ struct SmallSlot {
 };
 int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 ostride, const u64* lengths,
               u32 lstride, u64 count, u32 init, u32 final_xor, u32* out, hipStream_t st,
-              const SmallSlot* slot = nullptr) {
+              const SmallSlot* slot = nullptr, u32 g = 32, u64 ustride = 0, u64 ulen = 0) {
   SmallArgs a{};
+  a.ustride = ustride;  // (offsets == null: a uniform batch)
+  a.ulen = ulen;
   a.base = base;
   a.offsets = offsets;
   a.ostride = ostride;
@@ -485,9 +498,10 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
   a.rops = c->d_rops;
   a.pow2 = c->d_pow2;
   a.probe = c->probe;
-  // one workgroup per CU, or more, so that no wave gets more than one ring window of tiles
-  // (the kernel's in-loop flush then never runs: crc_small.hip)
-  const u64 tiles = (count + 1) / 2;
+  // one workgroup per CU, or more, so that no wave gets more than 32 tiles (G = 32: one ring
+  // window, the kernel's in-loop flush then never runs: crc_small.hip); g lanes per message
+  if (c->probe) g = 32;  // (the timestamp-recording instantiation is G = 32's)
+  const u64 tiles = ceil_div(count, 64ull / g);
   const unsigned blocks =
       (unsigned)std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSmallRingTiles));
   const size_t lds = small_lds_bytes() + 16;  // + the mismatch word
@@ -503,14 +517,27 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
     a.crc_out = slot->crc_out;
     a.error_count = slot->error_count;
     a.counter = c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters);
-    if (c->probe)  // experiment hook: the timestamp-recording instantiation (tools/small_timeline.py)
-      crc32_small_kernel<512, true, true><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
-    else
-      crc32_small_kernel<512, true, false><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
+    if (c->probe) {  // experiment hook: the timestamp-recording instantiation (tools/small_timeline.py)
+      crc32_small_kernel<512, true, true, 32><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
+    } else {
+      switch (g) {
+#define SMALL_SLOT_CASE(G) \
+  case G: crc32_small_kernel<512, true, false, G><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a); break;
+        SMALL_SLOT_CASE(1) SMALL_SLOT_CASE(2) SMALL_SLOT_CASE(4) SMALL_SLOT_CASE(8) SMALL_SLOT_CASE(16)
+        default: crc32_small_kernel<512, true, false, 32><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
+#undef SMALL_SLOT_CASE
+      }
+    }
   } else {
     a.zero_word = c->zero_word;
     c->zero_word = nullptr;
-    crc32_small_kernel<512, false, false><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
+    switch (g) {
+#define SMALL_CASE(G) \
+  case G: crc32_small_kernel<512, false, false, G><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a); break;
+      SMALL_CASE(1) SMALL_CASE(2) SMALL_CASE(4) SMALL_CASE(8) SMALL_CASE(16)
+      default: crc32_small_kernel<512, false, false, 32><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
+#undef SMALL_CASE
+    }
   }
   HIP_TRY(hipGetLastError());
   return SUBSPACE_CRC_OK;
@@ -682,15 +709,19 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_long_kernel<kRaggedWG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)ragged_lds_bytes());
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)small_lds_bytes() + 16);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)small_lds_bytes() + 16);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_small_kernel<512, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)small_lds_bytes() + 16);
+  {
+    const void* small_fns[] = {
+        (const void*)crc32_small_kernel<512, false, false, 1>,  (const void*)crc32_small_kernel<512, true, false, 1>,
+        (const void*)crc32_small_kernel<512, false, false, 2>,  (const void*)crc32_small_kernel<512, true, false, 2>,
+        (const void*)crc32_small_kernel<512, false, false, 4>,  (const void*)crc32_small_kernel<512, true, false, 4>,
+        (const void*)crc32_small_kernel<512, false, false, 8>,  (const void*)crc32_small_kernel<512, true, false, 8>,
+        (const void*)crc32_small_kernel<512, false, false, 16>, (const void*)crc32_small_kernel<512, true, false, 16>,
+        (const void*)crc32_small_kernel<512, false, false, 32>, (const void*)crc32_small_kernel<512, true, false, 32>,
+        (const void*)crc32_small_kernel<512, true, true, 32>};
+    for (const void* f : small_fns)
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)small_lds_bytes() + 16);
+  }
   if (e != hipSuccess) {
     subspace_crc_ctx_destroy(c);
     return hip_fail(e, "context setup");
@@ -856,8 +887,14 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
     c->scan_dirty = false;
     return SUBSPACE_CRC_OK;
   }
+  // Messages of at most 4 KiB: the small-message kernel straight from stride and length (no
+  // record arrays, no workspace).
+  const bool aligned = (stride % 16) == 0 && ((uintptr_t)dev_base % 16) == 0;
+  if (small_fits(length, aligned) && c->small_path && count > 1)
+    return small_run(c, static_cast<const uint8_t*>(dev_base), nullptr, 0, nullptr, 0, count, init, final_xor,
+                     dev_out, st, nullptr, small_lanes(length + (aligned ? 0 : 15)), stride, length);
   // Any other shape: materialise offsets/lengths (context workspace: ordered after the last
-  // workspace call first) and take the small-message or the ragged path.
+  // workspace call first) and take the ragged path.
   int rc = use_workspace(c, st);
   if (rc) return rc;
   if (count > c->u_capacity) {
@@ -872,9 +909,6 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
   uniform_offsets_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(stride, length, count, c->d_uoff,
                                                                            c->d_ulen);
   HIP_TRY(hipGetLastError());
-  if (small_fits(length, (stride % 16) == 0 && ((uintptr_t)dev_base % 16) == 0) && c->small_path && count > 1)
-    return small_run(c, static_cast<const uint8_t*>(dev_base), c->d_uoff, 1, c->d_ulen, 1, count, init, final_xor,
-                     dev_out, st);
   const u64 arena = stride * (count - 1) + length;
   return subspace_crc32_batch(c, dev_base, arena, c->d_uoff, c->d_ulen, count, init, flags, dev_out, stream);
 }
@@ -902,8 +936,10 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
   if (small && small_slot_fused(checksum_size, metadata_size)) {
     // one kernel, the slots finished in it; no context workspace (the counter ring, as the
     // fused uniform slot kernel)
+    // (lanes per slot from the bound: payloads of a channel's slots start on 16-B boundaries; one
+    // that does not and overruns its lines is still computed whole)
     const SmallSlot ss{rec, 3, 0, ~0ull, mode, checksum_size, metadata_size, dev_status, nullptr, dev_error_count};
-    return small_run(c, nullptr, rec + 1, 3, rec + 2, 3, count, 0u, 0u, nullptr, st, &ss);
+    return small_run(c, nullptr, rec + 1, 3, rec + 2, 3, count, 0u, 0u, nullptr, st, &ss, small_lanes(max_message_size));
   }
   rc = use_workspace(c, st);
   if (rc) return rc;
@@ -911,7 +947,8 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
   if (rc) return rc;
   want_zeroed(c, dev_error_count);
   if (small) {
-    rc = small_run(c, nullptr, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st);
+    rc = small_run(c, nullptr, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st, nullptr,
+                   small_lanes(max_message_size));
   } else {
     const u64 cap = count * ((max_message_size + 15 + 8191) / 8192) + 1;
     rc = ragged_run(c, nullptr, cap, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st, 0);  // absolute addresses
@@ -995,9 +1032,11 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
         was_zeroed(c, dev_error_count);  // the fused kernel writes the count itself
         const SmallSlot ss{c->d_soff, 1, prefix_size, slot_stride - prefix_size, mode, checksum_size, metadata_size,
                            dev_status, dev_crc_out, dev_error_count};
-        return small_run(c, buf, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, nullptr, st, &ss);
+        return small_run(c, buf, c->d_soff, 1, dev_message_sizes, 1, count, 0u, 0u, nullptr, st, &ss,
+                         small_lanes(slot_stride - prefix_size + (aligned ? 0 : 15)));
       }
-      rc = small_run(c, buf, c->d_soff, 1, c->d_slen, 1, count, 0u, 0u, c->d_crc0, st);
+      rc = small_run(c, buf, c->d_soff, 1, c->d_slen, 1, count, 0u, 0u, c->d_crc0, st, nullptr,
+                     small_lanes(slot_stride - prefix_size + (aligned ? 0 : 15)));
     } else {
       const u64 cap = (slot_stride * count + 15 * count) / 8192 + count + 1;
       rc = ragged_run(c, buf, cap, c->d_soff, 1, c->d_slen, 1, count, 0u, 0u, c->d_crc0, st,

@@ -180,6 +180,7 @@ struct SmallArgs {
                      // the slot's payload area); ~0 for slot lists
   u64* probe;        // experiment hook (subspace_crc_testutil_probe), else null: kProbeWords realtime
                      // stamps per wave, stored at exit (tools/small_timeline.py)
+  u64 ustride, ulen;  // offsets == null (a uniform batch): message m at base + m * ustride, ulen bytes
 };
 
 // Segments per workgroup of the segment-prefix look-back scan (crc_combine.hip, 256 threads)

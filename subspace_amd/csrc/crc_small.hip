@@ -62,11 +62,16 @@
 
 namespace subspace_amd {
 
-template <int WG, bool SLOT, bool PROBE>
+template <int WG, bool SLOT, bool PROBE, int G>
 __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__ gtab, const u32* __restrict__ gops,
                                                          SmallArgs a) {
   extern __shared__ __attribute__((aligned(16))) u32 smem[];
   constexpr int NPW = WG / 64;
+  // G lanes per message (one 128-B line each): M = 64 / G messages per tile, each of at most
+  // C = 128 G extended bytes; a ring window (64 messages) is W = G tiles. G = 32 is the
+  // half-tile form (two messages per tile); smaller G packs short messages.
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16 || G == 32, "lanes per message");
+  constexpr u32 M = 64u / (u32)G, C = 128u * (u32)G, W = (u32)G;
   const u32 sbase = (u32)(uintptr_t)smem;
   const u32 smism = sbase + (u32)small_lds_bytes();  // SLOT: the workgroup's mismatch word
   // experiment hook: realtime stamps (entry, window records landed, barrier, tile 0 landed,
@@ -80,13 +85,16 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   const int lane = threadIdx.x & 63;
   const u32 wid = rfl(threadIdx.x >> 6);
   const u32 l = (u32)lane & 31u, h = (u32)lane >> 5;
+  const u32 li = (u32)lane % (u32)G, mj = (u32)lane / (u32)G;  // line in its message, message in its tile
   const u32 sring = sbase + kSmallRing + wid * kSmallRingBytesPerWave;  // this wave's result ring
   const u32 lc0 = sbase + (l << 2), lc1 = lc0 + 0x10000u;
-  const u32 lop = sbase + kLdsOps + 4u * (31u - l);  // this lane's line-shift operator
+  const u32 lop = sbase + kLdsOps + 4u * (31u - l);  // this lane's line-shift operator (G = 32)
+  // Z_{128 (G-1-li)}: the lines after this one in its message (slot s of the table is Z_{128 s})
+  const u32 lopg = sbase + kLdsOps + 4u * ((u32)G - 1u - li);
   const u32 z64 = sbase + kLdsOps + 512u * (u32)kUniSlotOpZ64 + 4u * (u32)(lane & 3);
   const u64 count = a.count;
   const uint8_t* const base = a.base;
-  const u64 ntiles = (count + 1) >> 1;
+  const u64 ntiles = (count + M - 1) / M;
   const u64 nw = (u64)gridDim.x * NPW;
   const u64 t0 = front_slot(blockIdx.x, gridDim.x, wid);
   const u32 nk = t0 < ntiles ? (u32)((ntiles - t0 + nw - 1) / nw) : 0u;  // tiles tau = t0 + k*nw
@@ -94,20 +102,30 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   const bool calc = a.mode == 0u;
 
   // this lane's message in tile k (present: k < nk and m < count)
-  auto msg_of = [&](u32 k) __attribute__((always_inline)) { return 2 * (t0 + (u64)k * nw) + (u64)h; };
-  // Lane i's message of the first window (tile i / 2, half i & 1): the flush's message, and the
-  // record lane i holds for the tile loop (clamped into the batch like every record load)
-  const u64 fm = 2 * (t0 + (u64)((u32)lane >> 1) * nw) + ((u32)lane & 1u);
-  const bool flive = ((u32)lane >> 1) < nk && fm < count;
+  auto msg_of = [&](u32 k) __attribute__((always_inline)) { return M * (t0 + (u64)k * nw) + (u64)mj; };
+  // Lane i's message of the first window (tile i / M, message i % M): the flush's message, and
+  // the record lane i holds for the tile loop (clamped into the batch like every record load)
+  const u64 fm = M * (t0 + (u64)((u32)lane / M) * nw) + ((u32)lane % M);
+  const bool flive = ((u32)lane / M) < nk && fm < count;
   const u64 fmc = fm < count ? fm : count - 1;
-  // The record of this lane's half in tile k, clamped into the batch (every record load reads
-  // a real record; whether the half holds a message is decided from k and m when used).
+  // Message m's record: offset and length from the arrays, or (a uniform batch: no offsets)
+  // m * ustride and ulen (a kernel-argument branch)
+  auto record = [&](u64 m, u64& s, u64& L) __attribute__((always_inline)) {
+    if (a.offsets) {
+      s = a.offsets[m * a.ostride];
+      L = a.lengths[m * a.lstride];
+    } else {
+      s = m * a.ustride;
+      L = a.ulen;
+    }
+  };
+  // The record of this lane's message in tile k, clamped into the batch (every record load reads
+  // a real record; whether the lane's slot holds a message is decided from k and m when used).
   auto fetch = [&](u32 k, u64& s, u64& L) __attribute__((always_inline)) {
     const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
     u64 m = nk ? msg_of(kk) : 0;
     m = m < count ? m : count - 1;
-    s = a.offsets[m * a.ostride];
-    L = a.lengths[m * a.lstride];
+    record(m, s, L);
   };
   // The window's records, loaded once in the prologue (lane i: message i of the first window),
   // and tile k's record for this lane's half broadcast from them (k < 32; clamped as fetch's)
@@ -129,8 +147,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // message, an empty one, or one longer than a half-tile, computed apart: long_crc).
   auto ext = [&](u32 k, u64 s, u64 L) __attribute__((always_inline)) -> u32 {
     const u64 E = L + (s & 15u);
-    return (k < nk && msg_of(k) < count && L != 0 && E <= kSmallMaxExt && (!SLOT || L <= a.max_len)) ? (u32)E
-                                                                                                    : 0u;
+    return (k < nk && msg_of(k) < count && L != 0 && E <= C && (!SLOT || L <= a.max_len)) ? (u32)E : 0u;
   };
   auto load_lines = [&](u32x4 (&D)[8], u64 s, u32 E) __attribute__((always_inline)) {
     const uint8_t* p0 = E ? base + (s & ~(u64)15) : safe;
@@ -138,7 +155,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32x4* q[8];
 #pragma unroll
     for (int b = 0; b < 8; b++) {
-      const u32 off = 128u * l + 16u * (u32)b;
+      const u32 off = 128u * li + 16u * (u32)b;
       q[b] = reinterpret_cast<const u32x4*>(p0 + (off < lastb ? off : lastb));
       D[b] = *q[b];
     }
@@ -320,6 +337,28 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // SLOT: kCodeOversize for a size beyond the slot's payload area (nothing read or stored).
   constexpr u32 kCodeOversize = 0x10000000u, kCodeLong = 0x20000000u, kCodeEmpty = 0x40000000u,
                 kCodeSkip = 0x80000000u;
+  // A message's value from its lines' CRCs: line li -> Z_{128 (G-1-li)}(line), XOR over the
+  // message's G lanes (DPP). G = 32: row_shr 1/2/4/8 + row_bcast:15 leave each half's total in
+  // its last lane (31, 63); G <= 16: a butterfly (quad_perm xor 1, xor 2, row_half_mirror,
+  // row_mirror) leaves the group's total in every lane of the group.
+  auto msg_value = [&](u32 crc) __attribute__((always_inline)) -> u32 {
+    if constexpr (G == 32) {
+      u32 v = lane_shift(lop, crc);
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+      v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+      return v;
+    } else {
+      u32 v = G == 1 ? crc : lane_shift(lopg, crc);
+      if constexpr (G >= 2) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+      if constexpr (G >= 4) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+      if constexpr (G >= 8) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+      if constexpr (G >= 16) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false); // row_mirror
+      return v;
+    }
+  };
   auto process = [&](const u32x4 (&cur)[8], u64 s, u64 L, u32 k) __attribute__((always_inline)) {
     const u32 mis = (u32)s & 15u;
     const u32 E = ext(k, s, L);
@@ -328,32 +367,26 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     for (int b = 0; b < 8; b++) d[b] = cur[b];
     // Head: line 0's first mis bytes precede the message. Tail: bytes from E on (the
     // re-read last block included). Each lane keeps only its line's message bytes.
-    const bool head = E != 0u && mis != 0u && l == 0u;
-    if (__any(head || E < kSmallMaxExt)) {
-      const int v0 = (int)E - 128 * (int)l;
+    const bool head = E != 0u && mis != 0u && li == 0u;
+    if (__any(head || E < C)) {
+      const int v0 = (int)E - 128 * (int)li;
       const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
       keep_bytes(d, head ? mis : 0u, hi);
     }
     u32 seed = a.init;  // Z_mis^{-1}(init): after the mis masked bytes the state is init
     if (seed != 0u && __any(head)) seed = inv_bits(seed, mis, 4);
-    const u32 crc = line_crc32_2chain(d, l == 0u ? seed : 0u, lc0, lc1, z64);
-    // line l of half h -> Z_{128*(31-l)}(line), XOR over each half (DPP): lanes 31, 63
-    u32 v = lane_shift(lop, crc);
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    const u32 crc = line_crc32_2chain(d, li == 0u ? seed : 0u, lc0, lc1, z64);
+    const u32 v = msg_value(crc);
     const u64 m = msg_of(k);
     const bool present = k < nk && m < count;
-    const bool over = present && L + mis > kSmallMaxExt;
+    const bool over = present && L + mis > C;
     const u32 code = !present              ? kCodeSkip
                    : SLOT && L > a.max_len ? kCodeOversize
                    : over                  ? kCodeLong
                    : L == 0                ? kCodeEmpty
-                                           : (kSmallMaxExt - E) | (mis << 12);
-    // lane 31 of each half: its message's value and code, one 8-B LDS store
-    if (l == 31u) lds_st64(sring + 8u * (2u * (k & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
+                                           : (C - E) | (mis << 12);
+    // the message's last lane: its value and code, one 8-B LDS store
+    if (li == (u32)G - 1u) lds_st64(sring + 8u * ((k & (W - 1u)) * M + mj), (u64)v | ((u64)code << 32));
   };
   // FAST: a whole 16-B-aligned 4 KiB message per half (mis = 0, no padding: code 0); line 0 from
   // init itself
@@ -378,20 +411,21 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // offset from its record again).
   auto flush = [&](u32 kf, u32 nt) __attribute__((always_inline)) {
     wave_lds_sync();
-    const u32 hh = (u32)lane & 1u, ti = (u32)lane >> 1;
+    const u32 hh = (u32)lane % M, ti = (u32)lane / M;
     const bool valid = ti < nt;
     const u64 e = lds_ld64(sring + 8u * (u32)lane);
     u32 v = (u32)e;
     const u32 code = valid ? (u32)(e >> 32) : kCodeSkip;
-    const u64 m = 2 * (t0 + (u64)(kf + ti) * nw) + hh;
+    const u64 m = M * (t0 + (u64)(kf + ti) * nw) + hh;
     const u64 mc = code != kCodeSkip ? m : 0;  // (a real record for every lane)
     // rare: messages longer than a half-tile, one at a time by the whole wave
     u64 msk = __ballot(code == kCodeLong);
     while (msk) {
       const u32 src = (u32)__builtin_ctzll(msk);
       msk &= msk - 1;
-      const u64 ms = 2 * (t0 + (u64)(kf + (src >> 1)) * nw) + (src & 1u);
-      const u64 s = a.offsets[ms * a.ostride], L = a.lengths[ms * a.lstride];
+      const u64 ms = M * (t0 + (u64)(kf + src / M) * nw) + src % M;
+      u64 s, L;
+      record(ms, s, L);
       const u64 P = SLOT ? a.prefixes[ms * a.pstride] : 0;
       const u32 r = long_crc(s, L, P);
       v = lane == (int)src ? r : v;
@@ -407,9 +441,13 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       u32 F = eF, S = eS, H = eH;
       bool has = ehas;
       if (kf != 0) H = span_crc(pfx, F, S, has);
-      // Z_p(crc_raw(H, payload)) = Z_4096(Z_mis^{-1}(H)) ^ V, then Z_p undone
+      // Z_p(crc_raw(H, payload)) = Z_C(Z_mis^{-1}(H)) ^ V, then Z_p undone (Z_C: LDS for C = 4096,
+      // else Z_{2^k} from global memory)
       const u32 Hm = inv_bits(H, half ? (code >> 12) & 15u : 0u, 4);
-      const u32 X = opmul(sbase, kUniSlotOpZ4096, Hm) ^ v;
+      u32 zc;
+      if constexpr (G == 32) zc = opmul(sbase, kUniSlotOpZ4096, Hm);
+      else zc = opmul_global(a.pow2 + 128 * (7 + __builtin_ctz((u32)G)), Hm);
+      const u32 X = zc ^ v;
       const u32 R = half ? inv_bits(X, code & 0xFFFu, kSmallInvOps) : (code == kCodeLong ? v : H);
       slot_store(live, oversize, m, pfx, F, S, has, R);
     } else {
@@ -438,13 +476,14 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       if (live) a.out[m] = v ^ a.final_xor;
     }
   };
-  constexpr u32 kWinMask = kSmallRingTiles - 1u;
+  constexpr u32 kWinMask = W - 1u;
 
   // Prologue: table loads, the window's records (and SLOT its prefix offsets); the LDS fill while
   // the records are in flight; then the first window's prefix words and tile 0's lines, the
   // barrier (tile 0's latency hides behind it), and the span terms hashed under tile 0's flight.
-  wS = a.offsets[fmc * a.ostride];
-  wL = a.lengths[fmc * a.lstride];
+  if constexpr (G == 32) {
+    record(fmc, wS, wL);
+  }
   if constexpr (SLOT) fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
   fill.store(sbase);
   if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
@@ -457,11 +496,16 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // and code arithmetic, 6,759 VALU instructions per wave against the uniform kernel's 4,508;
   // r05z)
   const bool conf = !flive || (wL == (u64)kSmallMaxExt && (wS & 15u) == 0 && (!SLOT || wL <= a.max_len));
-  const bool fast = nk <= kSmallRingTiles && __ballot(!conf) == 0;
+  const bool fast = G == 32 && nk <= kSmallRingTiles && __ballot(!conf) == 0;
   if constexpr (probe) pt[1] = __builtin_amdgcn_s_memrealtime();
   u64 sA, LA, sB, LB;
-  win_rec(0, sA, LA);
-  win_rec(1, sB, LB);
+  if constexpr (G == 32) {
+    win_rec(0, sA, LA);
+    win_rec(1, sB, LB);
+  } else {
+    fetch(0, sA, LA);
+    fetch(1, sB, LB);
+  }
   u32 pwords[14], pmeta[kW];
   if constexpr (SLOT) {
     if (SUBSPACE_SMALL_VARIANT != 1) span_load(flive ? base + fpre - a.pdelta : safe, pwords, pmeta);
@@ -497,7 +541,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
   } else {
     // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines; the
-    // ring is finished whenever it holds 32 tiles, right after the next tile's loads are issued
+    // ring is finished whenever it holds W tiles (64 messages), right after the next tile's loads are issued
     // (so the stores retire during that tile's compute), and at the end (crc_ragged.hip's loop,
     // without descriptors). Nothing else lives across the loop (register-parked
     // values, 64-tile windows and a flush only after the loop each measured slower).
@@ -516,6 +560,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       fetch(k + 3, sB, LB);
       load_lines(A, s2, ext(k + 2, s2, L2));
       issue_prio_lo();
+      if constexpr (W == 1) flush(k, 1u);  // (one-tile windows: tile k before tile k + 1)
       process(B, s1, L1, k + 1);
       sc = s2;
       Lc = L2;
@@ -572,8 +617,16 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   }
 }
 
-template __global__ void crc32_small_kernel<512, false, false>(const u32*, const u32*, SmallArgs);
-template __global__ void crc32_small_kernel<512, true, false>(const u32*, const u32*, SmallArgs);
-template __global__ void crc32_small_kernel<512, true, true>(const u32*, const u32*, SmallArgs);
+#define SUBSPACE_SMALL_INST(G)                                                                          \
+  template __global__ void crc32_small_kernel<512, false, false, G>(const u32*, const u32*, SmallArgs); \
+  template __global__ void crc32_small_kernel<512, true, false, G>(const u32*, const u32*, SmallArgs);
+SUBSPACE_SMALL_INST(1)
+SUBSPACE_SMALL_INST(2)
+SUBSPACE_SMALL_INST(4)
+SUBSPACE_SMALL_INST(8)
+SUBSPACE_SMALL_INST(16)
+SUBSPACE_SMALL_INST(32)
+#undef SUBSPACE_SMALL_INST
+template __global__ void crc32_small_kernel<512, true, true, 32>(const u32*, const u32*, SmallArgs);
 
 }  // namespace subspace_amd

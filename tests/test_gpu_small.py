@@ -5,8 +5,9 @@ messages up to 4 KiB, and messages longer than a half-tile (extended length > 40
 broken max_message_size bound, a 4 KiB payload off a 16-B boundary), which a wave computes
 whole in its flush.
 Covers the half-tile edges (lengths 0, 1, 15-17, 127-129, 4080, 4081, 4096, every start
-offset & 15), odd counts, init / finalize, several 64-tile flush windows per wave, and
-agreement with the ragged path on the same records (testutil "small_path" 0).
+offset & 15), odd counts, init / finalize, several flush windows per wave, the packed forms
+(G = 1 ... 16 lanes per message for short messages and short slots), and agreement with the
+ragged path on the same records (testutil "small_path" 0).
 """
 import numpy as np
 import pytest
@@ -124,6 +125,39 @@ def test_slot_list_small_publish_verify(gpu_ctx, oracle, count, cs, ms, misalign
         if sizes[i]:
             pay2[int(pay_off[i]) + int(rng.integers(0, int(sizes[i])))] ^= np.uint8(1 << int(rng.integers(0, 8)))
     _, st, err = run_slot_list(gpu_ctx, got_pre, pay2, pay_off, sizes, order, ps, cs, ms, 4096, gpu.SLOT_VERIFY)
+    arena2, po, yo = oracle_arena(got_pre, pay2, pay_off, count, ps)
+    want = oracle.verify_slots(arena2, po, yo, sizes, cs, ms)
+    assert np.array_equal(st, want)
+    assert err == int((want == 1).sum())
+
+
+@pytest.mark.parametrize("count,max_size,cs,ms,misaligned,oversize", [
+    (20_001, 64, 4, 0, 0.0, 0.0),     # one lane per slot (G = 1)
+    (20_001, 100, 4, 16, 0.2, 0.02),  # G = 1, payloads off 16-B boundaries past their line: long path
+    (50_001, 256, 4, 0, 0.1, 0.0),    # G = 2
+    (9_999, 700, 8, 5, 0.3, 0.01),    # G = 8
+    (9_999, 2000, 4, 0, 0.2, 0.0),    # G = 16
+    (300_001, 200, 4, 0, 0.0, 0.0),   # G = 2, several ring windows (2 tiles each) per wave
+])
+def test_slot_list_packed(gpu_ctx, oracle, count, max_size, cs, ms, misaligned, oversize):
+    """Slot lists of short slots: max_message_size picks G = the lanes per slot (crc_small.hip:
+    64 / G slots per tile), bit-exact publish and verify against the oracle for every slot,
+    including ones longer than the bound or off a 16-B boundary past their G lines (computed
+    whole by the flush)."""
+    pre, pay, pay_off, sizes, order, ps = build_slot_list(count, count + max_size, cs, ms, max_size, misaligned,
+                                                          oversize, over_max=max_size * 3 + 50)
+    got_pre, st, _ = run_slot_list(gpu_ctx, pre, pay, pay_off, sizes, order, ps, cs, ms, max_size, gpu.SLOT_CALCULATE)
+    arena, po, yo = oracle_arena(pre, pay, pay_off, count, ps)
+    oracle.publish_slots(arena, po, yo, sizes, cs, ms)
+    assert (st == 0).all()
+    bad = np.nonzero(got_pre != arena[:len(pre)])[0]
+    assert len(bad) == 0, f"{len(bad)} prefix bytes differ, first slots {np.unique(bad // ps)[:8]}"
+    rng = np.random.default_rng(count + 1)
+    pay2 = pay.copy()
+    for i in np.nonzero(rng.random(count) < 0.1)[0]:
+        if sizes[i]:
+            pay2[int(pay_off[i]) + int(rng.integers(0, int(sizes[i])))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    _, st, err = run_slot_list(gpu_ctx, got_pre, pay2, pay_off, sizes, order, ps, cs, ms, max_size, gpu.SLOT_VERIFY)
     arena2, po, yo = oracle_arena(got_pre, pay2, pay_off, count, ps)
     want = oracle.verify_slots(arena2, po, yo, sizes, cs, ms)
     assert np.array_equal(st, want)
