@@ -630,7 +630,7 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   c->host_tab = make_tables(poly);
   c->zinv1 = inverse(z_one(c->host_tab));
 
-  std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kSmallOpSlots * 128, 0u), rops(kRagOpWords, 0u);
+  std::vector<u32> tab(1024), pow2(64 * 128, 0u), laneops(kSmallLaneOpSlots * 128, 0u), rops(kRagOpWords, 0u);
   for (int k = 0; k < 4; k++)
     for (int b = 0; b < 256; b++) tab[k * 256 + b] = c->host_tab.t[k][b];
 
@@ -669,6 +669,8 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
     nibble_tables(inverse(z_bytes(c->host_tab, 1ull << b)), &rops[kRagInvOps + 128 * b]);
   std::copy(rops.begin() + kRagInvOps, rops.begin() + kRagInvOps + 128 * kSmallInvOps,
             laneops.begin() + 128 * kSmallOpInv);
+  for (int j = 0; j < 5; j++)  // Z_{128 * 2^j}: the packed small-message forms' Z_C
+    nibble_tables(z_bytes(c->host_tab, 128ull << j), &laneops[128 * (kSmallOpZC + j)]);
   for (int k = 0; k < 3; k++)
     for (u64 d = 1; d < 16; d++)
       nibble_tables(inverse(z_bytes(c->host_tab, d << (4 * k))), &rops[kRagNibInvOps + 128 * (15 * k + (int)d - 1)]);

@@ -148,8 +148,12 @@ static_assert(ragged_lds_bytes() <= 160u * 1024u, "ragged kernel LDS exceeds 160
 constexpr int kSmallOpInv = kUniOpSlots;
 constexpr int kSmallInvOps = 12;
 constexpr int kSmallOpSlots = kSmallOpInv + kSmallInvOps;
+// one more LDS slot: Z_C for the packed forms' capacity C = 128 G < 4096 (the slot finish's
+// Z_C(H)), copied per launch from d_laneops slot kSmallOpZC + log2(G) (G = 1..16)
+constexpr int kSmallOpZC = kSmallOpSlots;
+constexpr int kSmallLaneOpSlots = kSmallOpZC + 5;  // d_laneops slots
 constexpr u32 kSmallMaxExt = 4096;  // extended bytes (length + offset & 15) of one half-tile
-constexpr u32 kSmallRing = kLdsOps + (u32)kSmallOpSlots * 512u;  // per-wave result rings
+constexpr u32 kSmallRing = kLdsOps + (u32)(kSmallOpSlots + 1) * 512u;  // per-wave result rings
 constexpr u32 kSmallRingTiles = 32;                               // tiles per ring window
 constexpr u32 kSmallRingBytesPerWave = kSmallRingTiles * 2u * 8u;  // (value | code << 32) per message
 constexpr size_t small_lds_bytes() { return kSmallRing + 8u * kSmallRingBytesPerWave; }

@@ -187,10 +187,14 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   };
   // Z_{2^b}^{-1} applied for the set bits of `bits` (b < nb <= 12; wave-uniform loop over the
   // bits any lane has): Z_mis^{-1} and the padding inverses Z_p^{-1}
+  // (an operator only where some lane has the bit: a batch of one size has one padding, and
+  // its bits cost one opmul each instead of every bit below the highest)
   auto inv_bits = [&](u32 x, u32 bits, int nb) __attribute__((always_inline)) {
     for (int b = 0; b < nb && __any(bits != 0u); b++) {
-      const u32 xm = opmul(sbase, kSmallOpInv + b, x);
-      x = (bits & 1u) ? xm : x;
+      if (__any((bits & 1u) != 0u)) {
+        const u32 xm = opmul(sbase, kSmallOpInv + b, x);
+        x = (bits & 1u) ? xm : x;
+      }
       bits >>= 1;
     }
     return x;
@@ -441,13 +445,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       u32 F = eF, S = eS, H = eH;
       bool has = ehas;
       if (kf != 0) H = span_crc(pfx, F, S, has);
-      // Z_p(crc_raw(H, payload)) = Z_C(Z_mis^{-1}(H)) ^ V, then Z_p undone (Z_C: LDS for C = 4096,
-      // else Z_{2^k} from global memory)
+      // Z_p(crc_raw(H, payload)) = Z_C(Z_mis^{-1}(H)) ^ V, then Z_p undone
       const u32 Hm = inv_bits(H, half ? (code >> 12) & 15u : 0u, 4);
-      u32 zc;
-      if constexpr (G == 32) zc = opmul(sbase, kUniSlotOpZ4096, Hm);
-      else zc = opmul_global(a.pow2 + 128 * (7 + __builtin_ctz((u32)G)), Hm);
-      const u32 X = zc ^ v;
+      const u32 X = opmul(sbase, G == 32 ? kUniSlotOpZ4096 : kSmallOpZC, Hm) ^ v;
       const u32 R = half ? inv_bits(X, code & 0xFFFu, kSmallInvOps) : (code == kCodeLong ? v : H);
       slot_store(live, oversize, m, pfx, F, S, has, R);
     } else {
@@ -486,6 +486,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   }
   if constexpr (SLOT) fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
   fill.store(sbase);
+  if constexpr (SLOT && G < 32) {  // Z_C into its LDS slot
+    if (threadIdx.x < 128u)
+      lds_st(sbase + kLdsOps + 512u * (u32)kSmallOpZC + 4u * threadIdx.x,
+             gops[128 * (kSmallOpZC + __builtin_ctz((u32)G)) + threadIdx.x]);
+  }
   if (SLOT && threadIdx.x == 0) lds_st64(smism, 0ull);
   // FAST (wave-uniform): the window is every tile of the wave (at most 32: small_run's grid) and
   // each of its messages is a whole 4 KiB payload on a 16-B boundary (SLOT: within max_len) --

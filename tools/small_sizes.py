@@ -4,7 +4,11 @@ of n messages of L bytes (stride = L rounded up to 16 B) through subspace_crc32_
 event-timed over `launches` back-to-back calls after `settle` untimed ones, rotated over buffers
 large enough to leave the 256 MB MALL behind.
 
-  python tools/small_sizes.py [L,L,...] [launches] [settle]
+  python tools/small_sizes.py [L,L,...] [launches] [settle] [uniform|slots]
+
+slots: a channel of L-byte slots (MessagePrefix 64 B + payload, the reference's stride) per
+256 MiB, published once, then verified as shuffled device slot lists (subspace_crc32_slots,
+max_message_size = L) over four rotated copies; GB/s counts span 0 (44 B) + payload.
 """
 import json
 import sys
@@ -13,15 +17,20 @@ from pathlib import Path
 import torch
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
-from subspace_amd import gpu  # noqa: E402
+import numpy as np  # noqa: E402
+
+from subspace_amd import gpu, slots  # noqa: E402
 
 
 def main():
     sizes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "64,256,1024,2048,4000").split(",")]
     launches = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     settle = int(sys.argv[3]) if len(sys.argv) > 3 else 200
+    mode = sys.argv[4] if len(sys.argv) > 4 else "uniform"
     ctx = gpu.CrcContext(0)
     dev = torch.device("cuda", 0)
+    if mode == "slots":
+        return slot_lists(ctx, dev, sizes, launches, settle)
     for L in sizes:
         stride = (L + 15) & ~15
         n = (256 << 20) // stride  # 256 MiB of messages per batch
@@ -42,8 +51,51 @@ def main():
         print(json.dumps({"length": L, "stride": stride, "messages": n, "us_per_call": round(us, 2),
                           "GBps": round(n * L / us / 1e3, 1), "Gmsg_per_s": round(n / us / 1e3, 3),
                           "pct_of_hbm_peak": round(100 * n * L / us / 1e3 / 8000, 2)}), flush=True)
-        del bufs, out
-        torch.cuda.empty_cache()
+        del bufs, out  # (no empty_cache: VRAM handed back is wiped in the background)
+    ctx.close()
+
+
+def slot_lists(ctx, dev, sizes, launches, settle):
+    rng = np.random.default_rng(0x5153)
+    for L in sizes:
+        cs, ms = 4, 0
+        ps, stride = slots.compute_prefix_size(cs, ms), slots.slot_stride(L, cs, ms)
+        n = (256 << 20) // stride
+        host = rng.integers(0, 256, stride * n, dtype=np.uint8)
+        host.reshape(n, stride)[:, :ps] = slots.make_prefixes(n, np.full(n, L, dtype=np.uint64), checksum_size=cs,
+                                                              metadata_size=ms, seed=5)
+        bufs = [torch.from_numpy(host).to(dev) for _ in range(4)]
+        for b in bufs:
+            ctx.crc32_slots_strided(b, stride, n, message_size=L, checksum_size=cs, metadata_size=ms,
+                                    mode=gpu.SLOT_CALCULATE)
+        order = rng.permutation(n).astype(np.uint64)
+        recs = []
+        for b in bufs:
+            b0 = np.uint64(b.data_ptr())
+            r = np.stack([b0 + order * np.uint64(stride), b0 + order * np.uint64(stride) + np.uint64(ps),
+                          np.full(n, L, dtype=np.uint64)], axis=1)
+            recs.append(torch.from_numpy(np.ascontiguousarray(r).view(np.int64)).to(dev))
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+        errs = torch.zeros(1, dtype=torch.int32, device=dev)
+
+        def one(i):
+            ctx.crc32_slots(recs[i % 4], max_message_size=L, checksum_size=cs, metadata_size=ms,
+                            mode=gpu.SLOT_VERIFY, status=status, error_count=errs)
+        for i in range(settle):
+            one(i)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for i in range(launches):
+            one(i)
+        b.record()
+        torch.cuda.synchronize()
+        us = a.elapsed_time(b) * 1e3 / launches
+        ok = int(errs.item()) == 0 and bool((status == 0).all().item())
+        nbytes = n * (L + 44)
+        print(json.dumps({"slot_payload": L, "stride": stride, "slots": n, "us_per_call": round(us, 2),
+                          "GBps": round(nbytes / us / 1e3, 1), "Gslots_per_s": round(n / us / 1e3, 3),
+                          "pct_of_hbm_peak": round(100 * nbytes / us / 1e3 / 8000, 2), "all_pass": ok}), flush=True)
+        del bufs, recs, status
     ctx.close()
 
 
