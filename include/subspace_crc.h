@@ -145,8 +145,9 @@ typedef struct subspace_crc_slot {
 
 /* Slot list (any placement, e.g. split buffers). max_message_size bounds every
  * message_size (pass the channel's slot size): with max_message_size <= 4096 the call is
- * one kernel launch (two messages per 8 KiB tile, the slot checksums finished in the same
- * kernel); larger bounds take the ragged pipeline. Either way a message larger than the
+ * one kernel launch (up to 64 messages per 8 KiB tile -- as many 128-B lines per message as
+ * the bound needs -- the slot checksums finished in the same kernel); larger bounds take the
+ * ragged pipeline. Either way a message larger than the
  * bound is still handled correctly, only more slowly.
  * dev_status: optional uint32[count]. dev_error_count: optional uint32, set to the number
  * of SUBSPACE_CRC_SLOT_MISMATCH slots of this call. */

@@ -1,5 +1,8 @@
-// Small-message kernel: one CRC32 per message of at most 4 KiB, two messages per 8 KiB tile
-// -- the slot-list and per-slot-size paths (subspace_crc32_slots with max_message_size <=
+// Small-message kernel: one CRC32 per message of at most 4 KiB, 64 / G messages per 8 KiB tile
+// (G = 1 .. 32 lanes per message, the host's choice from the call's length bound; the text
+// below describes G = 32, two messages per tile, and the packed forms differ only in the
+// counts: message slot mj = lane / G, line li = lane % G, capacity C = 128 G, ring window G
+// tiles) -- the slot-list and per-slot-size paths (subspace_crc32_slots with max_message_size <=
 // 4096, subspace_crc32_slots_strided with per-slot sizes in slots of <= 4 KiB) and uniform
 // batches of messages shorter than 4 KiB. It replaces the ragged pipeline (tile-count scan,
 // descriptors, ragged kernel, segment scans, final kernel, slot finish: seven launches,
