@@ -799,8 +799,8 @@ def slot_configs(ctx, dev, iters) -> dict:
         pre[:, 48:52].zero_()                # the stored checksum
         pre[:, 32].bitwise_and_(0xFB)        # kMessageHasChecksum (flags, offset 32)
     torch.cuda.synchronize()
-    list_kernel = "subspace_crc32_slots: subspace_amd::crc32_small_kernel<512, true> (one launch, slots finished in it; " \
-                  "crc_small.hip)"
+    list_kernel = "subspace_crc32_slots: subspace_amd::crc32_small_kernel<512, true, false, 32> (one launch, " \
+                  "slots finished in it; crc_small.hip)"
     # the slot-list access shape's own read ceiling: the kernel's FAST-loop loads over the same
     # rotated shuffled lists, no CRC (gpu.slot_list_read mode 4)
     sink = torch.empty(256 * 512, dtype=torch.int32, device=dev)
