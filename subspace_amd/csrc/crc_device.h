@@ -356,6 +356,15 @@ __device__ __forceinline__ u32 line_crc32_2chain(const u32x4 (&d)[8], u32 init, 
   return opmul_z64(z64, x) ^ y;
 }
 
+// The same for a line whose bytes 64..127 are zero (their chain from 0 stays 0): one 16-step
+// chain, Z_64 of it.
+__device__ __forceinline__ u32 line_crc32_lo(const u32x4 (&d)[8], u32 init, u32 lc0, u32 lc1, u32 z64) {
+  u32 x = init ^ d[0][0];
+#pragma unroll
+  for (int w = 0; w < 16; w++) x = step4n(x, lc0, lc1, w < 15 ? d[(w + 1) >> 2][(w + 1) & 3] : 0u);
+  return opmul_z64(z64, x);
+}
+
 // CRC of one 128-B line (8 x 16 B), from state `init`: 32 steps of step4n.
 __device__ __forceinline__ u32 line_crc32(const u32x4 (&d)[8], u32 init, u32 lc0, u32 lc1) {
   u32 x = init ^ d[0][0];

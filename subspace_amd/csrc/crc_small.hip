@@ -382,7 +382,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
     u32 seed = a.init;  // Z_mis^{-1}(init): after the mis masked bytes the state is init
     if (seed != 0u && __any(head)) seed = inv_bits(seed, mis, 4);
-    const u32 crc = line_crc32_2chain(d, li == 0u ? seed : 0u, lc0, lc1, z64);
+    // (G = 1, every message of the tile within 64 bytes: the line's second half is zeros)
+    const u32 crc = G == 1 && __all(E <= 64u) ? line_crc32_lo(d, seed, lc0, lc1, z64)
+                                              : line_crc32_2chain(d, li == 0u ? seed : 0u, lc0, lc1, z64);
     const u32 v = msg_value(crc);
     const u64 m = msg_of(k);
     const bool present = k < nk && m < count;
