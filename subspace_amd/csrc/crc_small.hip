@@ -410,6 +410,30 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32 code = (k < nk && msg_of(k) < count) ? 0u : kCodeSkip;
     if (l == 31u) lds_st64(sring + 8u * (2u * (k & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
   };
+  // UNIFORM FAST (G < 32, no slots): a uniform batch of messages of exactly C bytes on 16-B
+  // boundaries -- no masks, codes or padding; the tile's address from m * stride
+  auto u_off = [&](u32 k) __attribute__((always_inline)) {
+    const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
+    u64 m = msg_of(kk);
+    m = m < count ? m : count - 1;
+    u64 off = m * a.ustride + 128u * li;
+    asm volatile("" : "+v"(off));
+    return off;
+  };
+  auto process_u = [&](const u32x4 (&cur)[8], u32 k) __attribute__((always_inline)) {
+    const u32 crc = line_crc32_2chain(cur, li == 0u ? a.init : 0u, lc0, lc1, z64);
+    const u32 v = msg_value(crc);
+    const u32 code = (k < nk && msg_of(k) < count) ? 0u : kCodeSkip;
+    if (li == (u32)G - 1u) lds_st64(sring + 8u * ((k & (W - 1u)) * M + mj), (u64)v | ((u64)code << 32));
+  };
+  auto flush_u = [&](u32 kf, u32 nt) __attribute__((always_inline)) {
+    wave_lds_sync();
+    const u32 hh = (u32)lane % M, ti = (u32)lane / M;
+    const u64 e = lds_ld64(sring + 8u * (u32)lane);
+    const u64 m = M * (t0 + (u64)(kf + ti) * nw) + hh;
+    if (ti < nt && (u32)(e >> 32) == 0u) a.out[m] = (u32)e ^ a.final_xor;
+    wave_lds_sync();
+  };
   // SLOT: lane i's message of the first window (fm): its record's prefix offset, and (after
   // the barrier) the prefix terms, from words loaded in the prologue
   u64 fpre = 0;
@@ -507,6 +531,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // r05z)
   const bool conf = !flive || (wL == (u64)kSmallMaxExt && (wS & 15u) == 0 && (!SLOT || wL <= a.max_len));
   const bool fast = G == 32 && nk <= kSmallRingTiles && __ballot(!conf) == 0;
+  const bool fastu = !SLOT && G < 32 && a.offsets == nullptr && a.ulen == (u64)C && (a.ustride & 15u) == 0 &&
+                     ((uintptr_t)base & 15u) == 0;
   if constexpr (probe) pt[1] = __builtin_amdgcn_s_memrealtime();
   u64 sA, LA, sB, LB;
   if constexpr (G == 32) {
@@ -549,6 +575,29 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       drain_before_issue();
       process_fast(A, k);
     }
+  } else if (fastu) {
+    // the general loop's schedule (windows of W tiles) with the FAST loop's loads and compute
+    for (; k + 1 < nk; k += 2) {
+      const u64 qB = u_off(k + 1);
+      issue_prio_hi();
+      drain_before_issue();  // tile k's lines
+      load_at(B, qB);
+      issue_prio_lo();
+      if (k && (k & kWinMask) == 0u) flush_u(k - W, W);
+      process_u(A, k);
+      const u64 qA = u_off(k + 2);
+      issue_prio_hi();
+      drain_before_issue();
+      load_at(A, qA);
+      issue_prio_lo();
+      if constexpr (W == 1) flush_u(k, 1u);
+      process_u(B, k + 1);
+    }
+    if (k < nk) {
+      drain_before_issue();
+      if (k && (k & kWinMask) == 0u) flush_u(k - W, W);
+      process_u(A, k);
+    }
   } else {
     // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines; the
     // ring is finished whenever it holds W tiles (64 messages), right after the next tile's loads are issued
@@ -585,6 +634,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   if (nk && SUBSPACE_SMALL_VARIANT != 2) {
     if (fast) {
       flush_fast(nk);
+    } else if (fastu) {
+      const u32 kf = (nk - 1u) & ~kWinMask;
+      flush_u(kf, nk - kf);
     } else {
       const u32 kf = (nk - 1u) & ~kWinMask;  // the last window, not flushed yet
       flush(kf, nk - kf);

@@ -32,6 +32,19 @@ def test_uniform_small_lengths(gpu_ctx, oracle, length, extra):
     assert np.array_equal(got, expected_uniform(oracle, count, length, 0x5A11 + length))
 
 
+@pytest.mark.parametrize("length,count", [(128, 300_001), (256, 200_001), (512, 150_001), (1024, 100_001),
+                                          (2048, 100_001), (64, 9_999)])
+def test_uniform_small_exact_sizes(gpu_ctx, oracle, length, count):
+    """Messages of exactly G lines on 16-B boundaries (the packed FAST loop: no masks, codes or
+    padding), over several ring windows per wave, with a nonzero init and the final XOR; 64 B:
+    the one-lane form's 16-step chain."""
+    got = run_uniform(gpu_ctx, count, length=length, stride=length, seed=0x5A15 + length, init=0x9E3779B9,
+                      finalize=True)
+    want = expected_uniform(oracle, count, length, 0x5A15 + length, init=0x9E3779B9, finalize=True)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} mismatches, first {bad[:5]}"
+
+
 @pytest.mark.parametrize("init,finalize", [(0, False), (0x12345678, False), (0xDEADBEEF, True)])
 def test_uniform_small_init_finalize(gpu_ctx, oracle, init, finalize):
     got = run_uniform(gpu_ctx, 999, length=777, stride=781, seed=0x5A12, init=init, finalize=finalize)
