@@ -19,8 +19,9 @@
 //  * Waves sweep the tiles like the uniform kernel (order-0 front). A tile's two records
 //    are loaded one tile ahead of its lines (vector loads, retired in order with the line
 //    loads, as the ragged kernel's descriptors), so line addresses never wait on a record.
-//    The host gives no wave more than one 32-tile ring window (more workgroups for longer
-//    batches), so the in-loop flush below never runs; it stays for any grid. (Round 4: the same
+//    The host gives no wave more than 32 tiles (more workgroups for longer batches): for G =
+//    32 one ring window, so the in-loop flush below never runs; the packed forms flush every G
+//    tiles (64 messages) right after the next tile's loads are issued. (Round 4: the same
 //    kernel with the flush moved out of the loop -- 0 SGPR spills, no full drain in the loop
 //    -- measured 2.3-3.4 us slower per 65,536-slot list, with or without loop padding:
 //    profiles/r04/README.md.)
