@@ -59,7 +59,8 @@
 #include "crc_device.h"
 
 // Timing-only investigation builds (tools/ab_lib.sh -DSUBSPACE_SMALL_VARIANT=n; the product is
-// 0, the others compute nothing valid): 1 no prologue span loads / hash; 2 no flush.
+// 0, the others compute nothing valid): 1 no prologue span loads / hash; 2 no flush; 3 no
+// prefix reload in later windows.
 #ifndef SUBSPACE_SMALL_VARIANT
 #define SUBSPACE_SMALL_VARIANT 0
 #endif
@@ -474,7 +475,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
                                                      : safe;  // (a read-only block)
       u32 F = eF, S = eS, H = eH;
       bool has = ehas;
-      if (kf != 0) H = span_crc(pfx, F, S, has);
+      if (kf != 0 && SUBSPACE_SMALL_VARIANT != 3) H = span_crc(pfx, F, S, has);
       // Z_p(crc_raw(H, payload)) = Z_C(Z_mis^{-1}(H)) ^ V, then Z_p undone
       const u32 Hm = inv_bits(H, half ? (code >> 12) & 15u : 0u, 4);
       const u32 X = opmul(sbase, G == 32 ? kUniSlotOpZ4096 : kSmallOpZC, Hm) ^ v;

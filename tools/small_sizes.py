@@ -26,11 +26,11 @@ def main():
     sizes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "64,256,1024,2048,4000").split(",")]
     launches = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     settle = int(sys.argv[3]) if len(sys.argv) > 3 else 200
-    mode = sys.argv[4] if len(sys.argv) > 4 else "uniform"
+    mode = sys.argv[4] if len(sys.argv) > 4 else "uniform"  # uniform | slots | slots_ordered
     ctx = gpu.CrcContext(0)
     dev = torch.device("cuda", 0)
-    if mode == "slots":
-        return slot_lists(ctx, dev, sizes, launches, settle)
+    if mode.startswith("slots"):
+        return slot_lists(ctx, dev, sizes, launches, settle, ordered=mode == "slots_ordered")
     for L in sizes:
         stride = (L + 15) & ~15
         n = (256 << 20) // stride  # 256 MiB of messages per batch
@@ -55,7 +55,7 @@ def main():
     ctx.close()
 
 
-def slot_lists(ctx, dev, sizes, launches, settle):
+def slot_lists(ctx, dev, sizes, launches, settle, ordered=False):
     rng = np.random.default_rng(0x5153)
     for L in sizes:
         cs, ms = 4, 0
@@ -68,7 +68,7 @@ def slot_lists(ctx, dev, sizes, launches, settle):
         for b in bufs:
             ctx.crc32_slots_strided(b, stride, n, message_size=L, checksum_size=cs, metadata_size=ms,
                                     mode=gpu.SLOT_CALCULATE)
-        order = rng.permutation(n).astype(np.uint64)
+        order = np.arange(n, dtype=np.uint64) if ordered else rng.permutation(n).astype(np.uint64)
         recs = []
         for b in bufs:
             b0 = np.uint64(b.data_ptr())
@@ -92,7 +92,7 @@ def slot_lists(ctx, dev, sizes, launches, settle):
         us = a.elapsed_time(b) * 1e3 / launches
         ok = int(errs.item()) == 0 and bool((status == 0).all().item())
         nbytes = n * (L + 44)
-        print(json.dumps({"slot_payload": L, "stride": stride, "slots": n, "us_per_call": round(us, 2),
+        print(json.dumps({"order": "channel" if ordered else "shuffled", "slot_payload": L, "stride": stride, "slots": n, "us_per_call": round(us, 2),
                           "GBps": round(nbytes / us / 1e3, 1), "Gslots_per_s": round(n / us / 1e3, 3),
                           "pct_of_hbm_peak": round(100 * nbytes / us / 1e3 / 8000, 2), "all_pass": ok}), flush=True)
         del bufs, recs, status
