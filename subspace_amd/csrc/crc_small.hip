@@ -154,13 +154,13 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u64 E = L + (s & 15u);
     return (k < nk && msg_of(k) < count && L != 0 && E <= C && (!SLOT || L <= a.max_len)) ? (u32)E : 0u;
   };
-  auto load_lines = [&](u32x4 (&D)[8], u64 s, u32 E) __attribute__((always_inline)) {
+  auto load_lines_at = [&](u32x4 (&D)[8], u64 s, u32 E, u32 line) __attribute__((always_inline)) {
     const uint8_t* p0 = E ? base + (s & ~(u64)15) : safe;
     const u32 lastb = E ? (E - 1u) & ~15u : 0u;  // the block holding the message's last byte
     const u32x4* q[8];
 #pragma unroll
     for (int b = 0; b < 8; b++) {
-      const u32 off = 128u * li + 16u * (u32)b;
+      const u32 off = 128u * line + 16u * (u32)b;
       q[b] = reinterpret_cast<const u32x4*>(p0 + (off < lastb ? off : lastb));
       D[b] = *q[b];
     }
@@ -171,6 +171,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     // keep the loads at this point, in order (hipcc otherwise sinks them into the compute)
     __builtin_amdgcn_sched_barrier(0);
   };
+  auto load_lines = [&](u32x4 (&D)[8], u64 s, u32 E) __attribute__((always_inline)) { load_lines_at(D, s, E, li); };
   // FAST path: the tile's line offset from base, computed (and pinned) before the wait for
   // the previous tile, then 8 loads at immediate offsets (the uniform kernel's issue)
   auto fast_off = [&](u32 k) __attribute__((always_inline)) {
@@ -436,6 +437,53 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     if (ti < nt && (u32)(e >> 32) == 0u) a.out[m] = (u32)e ^ a.final_xor;
     wave_lds_sync();
   };
+  // REPACK (G = 32 kernels): a wave whose window (every tile of the wave) holds no message
+  // longer than 2 KiB (extended) -- a channel of large slots carrying shorter messages -- packs
+  // its window's 64 messages rg lanes each (rg = 1 .. 16, the wave's own choice), rg tiles for
+  // the 64 instead of 32; message e of the window (lane e's records, read by ds_bpermute) is
+  // slot e % rM of packed tile e / rM. Lane li' applies Z_{128 (31-li')} -- the value as if the
+  // message filled a half-tile (its lines past rg from 0 contribute 0) -- so the ring, codes
+  // (p = 4096 - E) and flush are the general loop's.
+  u32 rg = 32, rlg = 5;
+  auto bperm = [&](u32 e, u32 v) __attribute__((always_inline)) {
+    return (u32)__builtin_amdgcn_ds_bpermute((int)(e << 2), (int)v);
+  };
+  auto rp_rec = [&](u32 j, u64& s, u64& L, bool& pres) __attribute__((always_inline)) {
+    const u32 e = (j << (6u - rlg)) + ((u32)lane >> rlg);
+    const bool in = e < 2u * nk;
+    const u32 ec = in ? e : 0u;
+    s = ((u64)bperm(ec, (u32)(wS >> 32)) << 32) | (u64)bperm(ec, (u32)wS);
+    L = (u64)bperm(ec, (u32)wL);
+    pres = in && bperm(ec, flive ? 1u : 0u) != 0u;
+  };
+  auto rp_ext = [&](u64 s, u64 L, bool pres) __attribute__((always_inline)) -> u32 {
+    return pres && L != 0 ? (u32)(L + (s & 15u)) : 0u;
+  };
+  auto process_rp = [&](const u32x4 (&cur)[8], u64 s, u64 L, bool pres, u32 j) __attribute__((always_inline)) {
+    const u32 rli = (u32)lane & (rg - 1u);
+    const u32 mis = (u32)s & 15u;
+    const u32 E = rp_ext(s, L, pres);
+    u32x4 d[8];
+#pragma unroll
+    for (int b = 0; b < 8; b++) d[b] = cur[b];
+    const bool head = E != 0u && mis != 0u && rli == 0u;
+    if (__any(head || E < 128u * rg)) {
+      const int v0 = (int)E - 128 * (int)rli;
+      const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
+      keep_bytes(d, head ? mis : 0u, hi);
+    }
+    u32 seed = a.init;
+    if (seed != 0u && __any(head)) seed = inv_bits(seed, mis, 4);
+    const u32 crc = line_crc32_2chain(d, rli == 0u ? seed : 0u, lc0, lc1, z64);
+    u32 v = lane_shift(sbase + kLdsOps + 4u * (31u - rli), crc);
+    if (rg >= 2u) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    if (rg >= 4u) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    if (rg >= 8u) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    if (rg >= 16u) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false); // row_mirror
+    const u32 code = !pres ? kCodeSkip : L == 0 ? kCodeEmpty : (kSmallMaxExt - E) | (mis << 12);
+    const u32 e = (j << (6u - rlg)) + ((u32)lane >> rlg);
+    if (rli == rg - 1u) lds_st64(sring + 8u * e, (u64)v | ((u64)code << 32));
+  };
   // SLOT: lane i's message of the first window (fm): its record's prefix offset, and (after
   // the barrier) the prefix terms, from words loaded in the prologue
   u64 fpre = 0;
@@ -535,6 +583,22 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   const bool fast = G == 32 && nk <= kSmallRingTiles && __ballot(!conf) == 0;
   const bool fastu = !SLOT && G < 32 && a.offsets == nullptr && a.ulen == (u64)C && (a.ustride & 15u) == 0 &&
                      ((uintptr_t)base & 15u) == 0;
+  bool repack = false;
+  if constexpr (G == 32) {
+    if (!fast && nk <= kSmallRingTiles) {
+      const u64 Ew = wL + (wS & 15u);
+      const bool fits = !flive || (Ew <= 2048u && (!SLOT || wL <= a.max_len));
+      if (__ballot(!fits) == 0) {
+        repack = true;
+        rg = 1u;
+        rlg = 0u;
+        while (rg < 16u && __ballot(flive && Ew > 128u * rg) != 0) {
+          rg <<= 1;
+          rlg++;
+        }
+      }
+    }
+  }
   if constexpr (probe) pt[1] = __builtin_amdgcn_s_memrealtime();
   u64 sA, LA, sB, LB;
   if constexpr (G == 32) {
@@ -551,7 +615,13 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   }
   u32x4 A[8], B[8];
   u64 sc = sA, Lc = LA;
-  load_lines(A, sc, ext(0, sc, Lc));  // (FAST: the same addresses as load_at's)
+  bool pc = false;  // (REPACK: tile 0's slot holds a message)
+  if (repack) {
+    rp_rec(0u, sc, Lc, pc);
+    load_lines_at(A, sc, rp_ext(sc, Lc, pc), (u32)lane & (rg - 1u));
+  } else {
+    load_lines(A, sc, ext(0, sc, Lc));  // (FAST: the same addresses as load_at's)
+  }
   __syncthreads();
   if constexpr (probe) pt[2] = __builtin_amdgcn_s_memrealtime();
   if constexpr (SLOT && SUBSPACE_SMALL_VARIANT != 1) eH = span_hash(pwords, pmeta, eF, eS, ehas);
@@ -576,6 +646,36 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     if (k < nk) {
       drain_before_issue();
       process_fast(A, k);
+    }
+  } else if (repack) {
+    // the general loop's ping-pong over the wave's rg packed tiles (64 messages)
+    const u32 nt = (2u * nk + (64u >> rlg) - 1u) >> (6u - rlg);
+    const u32 rli = (u32)lane & (rg - 1u);
+    u32 j = 0;
+    for (; j + 1 < nt; j += 2) {
+      u64 s1, L1;
+      bool p1;
+      rp_rec(j + 1, s1, L1, p1);
+      issue_prio_hi();
+      drain_before_issue();  // tile j's lines
+      load_lines_at(B, s1, rp_ext(s1, L1, p1), rli);
+      issue_prio_lo();
+      process_rp(A, sc, Lc, pc, j);
+      u64 s2, L2;
+      bool p2;
+      rp_rec(j + 2, s2, L2, p2);
+      issue_prio_hi();
+      drain_before_issue();
+      load_lines_at(A, s2, rp_ext(s2, L2, p2), rli);
+      issue_prio_lo();
+      process_rp(B, s1, L1, p1, j + 1);
+      sc = s2;
+      Lc = L2;
+      pc = p2;
+    }
+    if (j < nt) {
+      drain_before_issue();
+      process_rp(A, sc, Lc, pc, j);
     }
   } else if (fastu) {
     // the general loop's schedule (windows of W tiles) with the FAST loop's loads and compute

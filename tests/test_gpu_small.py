@@ -177,6 +177,44 @@ def test_slot_list_packed(gpu_ctx, oracle, count, max_size, cs, ms, misaligned, 
     assert err == int((want == 1).sum())
 
 
+@pytest.mark.parametrize("gen_max,count,spoil", [(100, 20_001, 0), (300, 50_001, 0), (1500, 9_999, 0),
+                                                (2000, 30_001, 0), (700, 30_001, 3000)])
+def test_slot_list_repack(gpu_ctx, oracle, gen_max, count, spoil):
+    """A channel of 4 KiB slots (max_message_size 4096) carrying shorter messages: each wave
+    whose window holds nothing longer than 2 KiB repacks it (crc_small.hip REPACK, rg lanes per
+    message); `spoil` puts one 3,000-B message in every 50th window, so repacked and general
+    waves share the launch. Publish and verify bit-exact against the oracle (payload starts
+    off 16-B boundaries included)."""
+    pre, pay, pay_off, sizes, order, ps = build_slot_list(count, count + gen_max, 4, 0, gen_max, 0.2, 0.0)
+    if spoil:  # (payload room: build_slot_list sized it for gen_max, so give the slot a fresh area)
+        extra = []
+        for i in range(0, count, 64 * 50):
+            off = len(pay) + len(extra) * (spoil + 64)
+            extra.append(i)
+            pay_off[i] = off
+            sizes[i] = spoil
+        pay = np.concatenate([pay, np.random.default_rng(7).integers(0, 256, len(extra) * (spoil + 64) + 64,
+                                                                      dtype=np.uint8)])
+        pre = slots.make_prefixes(count, sizes, checksum_size=4, metadata_size=0, seed=count + gen_max + 1)
+        pre = pre.reshape(-1).copy()
+    got_pre, st, _ = run_slot_list(gpu_ctx, pre, pay, pay_off, sizes, order, ps, 4, 0, 4096, gpu.SLOT_CALCULATE)
+    arena, po, yo = oracle_arena(pre, pay, pay_off, count, ps)
+    oracle.publish_slots(arena, po, yo, sizes, 4, 0)
+    assert (st == 0).all()
+    bad = np.nonzero(got_pre != arena[:len(pre)])[0]
+    assert len(bad) == 0, f"{len(bad)} prefix bytes differ, first slots {np.unique(bad // ps)[:8]}"
+    rng = np.random.default_rng(count + 3)
+    pay2 = pay.copy()
+    for i in np.nonzero(rng.random(count) < 0.1)[0]:
+        if sizes[i]:
+            pay2[int(pay_off[i]) + int(rng.integers(0, int(sizes[i])))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    _, st, err = run_slot_list(gpu_ctx, got_pre, pay2, pay_off, sizes, order, ps, 4, 0, 4096, gpu.SLOT_VERIFY)
+    arena2, po, yo = oracle_arena(got_pre, pay2, pay_off, count, ps)
+    want = oracle.verify_slots(arena2, po, yo, sizes, 4, 0)
+    assert np.array_equal(st, want)
+    assert err == int((want == 1).sum())
+
+
 def test_slot_list_small_matches_ragged(gpu_ctx, lib):
     """The same records through the small-message kernel and through the ragged pipeline."""
     count, cs, ms = 4000, 8, 5

@@ -4,11 +4,12 @@ of n messages of L bytes (stride = L rounded up to 16 B) through subspace_crc32_
 event-timed over `launches` back-to-back calls after `settle` untimed ones, rotated over buffers
 large enough to leave the 256 MB MALL behind.
 
-  python tools/small_sizes.py [L,L,...] [launches] [settle] [uniform|slots]
+  python tools/small_sizes.py [L,L,...] [launches] [settle] [uniform|slots|slots_ordered|slots4k]
 
 slots: a channel of L-byte slots (MessagePrefix 64 B + payload, the reference's stride) per
 256 MiB, published once, then verified as shuffled device slot lists (subspace_crc32_slots,
-max_message_size = L) over four rotated copies; GB/s counts span 0 (44 B) + payload.
+max_message_size = L) over four rotated copies; GB/s counts span 0 (44 B) + payload. slots4k:
+L-byte messages in a channel of 4 KiB slots (max_message_size 4096).
 """
 import json
 import sys
@@ -26,11 +27,12 @@ def main():
     sizes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "64,256,1024,2048,4000").split(",")]
     launches = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     settle = int(sys.argv[3]) if len(sys.argv) > 3 else 200
-    mode = sys.argv[4] if len(sys.argv) > 4 else "uniform"  # uniform | slots | slots_ordered
+    mode = sys.argv[4] if len(sys.argv) > 4 else "uniform"  # uniform | slots | slots_ordered | slots4k
     ctx = gpu.CrcContext(0)
     dev = torch.device("cuda", 0)
     if mode.startswith("slots"):
-        return slot_lists(ctx, dev, sizes, launches, settle, ordered=mode == "slots_ordered")
+        return slot_lists(ctx, dev, sizes, launches, settle, ordered=mode == "slots_ordered",
+                          slot_size=4096 if mode == "slots4k" else 0)
     for L in sizes:
         stride = (L + 15) & ~15
         n = (256 << 20) // stride  # 256 MiB of messages per batch
@@ -55,19 +57,21 @@ def main():
     ctx.close()
 
 
-def slot_lists(ctx, dev, sizes, launches, settle, ordered=False):
+def slot_lists(ctx, dev, sizes, launches, settle, ordered=False, slot_size=0):
+    """slot_size: the channel's slot size (max_message_size); 0: each message fills its slot."""
     rng = np.random.default_rng(0x5153)
     for L in sizes:
         cs, ms = 4, 0
-        ps, stride = slots.compute_prefix_size(cs, ms), slots.slot_stride(L, cs, ms)
+        area = slot_size or L
+        ps, stride = slots.compute_prefix_size(cs, ms), slots.slot_stride(area, cs, ms)
         n = (256 << 20) // stride
         host = rng.integers(0, 256, stride * n, dtype=np.uint8)
         host.reshape(n, stride)[:, :ps] = slots.make_prefixes(n, np.full(n, L, dtype=np.uint64), checksum_size=cs,
                                                               metadata_size=ms, seed=5)
         bufs = [torch.from_numpy(host).to(dev) for _ in range(4)]
         for b in bufs:
-            ctx.crc32_slots_strided(b, stride, n, message_size=L, checksum_size=cs, metadata_size=ms,
-                                    mode=gpu.SLOT_CALCULATE)
+            ctx.crc32_slots_strided(b, stride, n, sizes=torch.full((n,), L, dtype=torch.int64, device=dev),
+                                    checksum_size=cs, metadata_size=ms, mode=gpu.SLOT_CALCULATE)
         order = np.arange(n, dtype=np.uint64) if ordered else rng.permutation(n).astype(np.uint64)
         recs = []
         for b in bufs:
@@ -79,7 +83,7 @@ def slot_lists(ctx, dev, sizes, launches, settle, ordered=False):
         errs = torch.zeros(1, dtype=torch.int32, device=dev)
 
         def one(i):
-            ctx.crc32_slots(recs[i % 4], max_message_size=L, checksum_size=cs, metadata_size=ms,
+            ctx.crc32_slots(recs[i % 4], max_message_size=area, checksum_size=cs, metadata_size=ms,
                             mode=gpu.SLOT_VERIFY, status=status, error_count=errs)
         for i in range(settle):
             one(i)
@@ -92,7 +96,7 @@ def slot_lists(ctx, dev, sizes, launches, settle, ordered=False):
         us = a.elapsed_time(b) * 1e3 / launches
         ok = int(errs.item()) == 0 and bool((status == 0).all().item())
         nbytes = n * (L + 44)
-        print(json.dumps({"order": "channel" if ordered else "shuffled", "slot_payload": L, "stride": stride, "slots": n, "us_per_call": round(us, 2),
+        print(json.dumps({"order": "channel" if ordered else "shuffled", "slot_area": area, "message": L, "stride": stride, "slots": n, "us_per_call": round(us, 2),
                           "GBps": round(nbytes / us / 1e3, 1), "Gslots_per_s": round(n / us / 1e3, 3),
                           "pct_of_hbm_peak": round(100 * nbytes / us / 1e3 / 8000, 2), "all_pass": ok}), flush=True)
         del bufs, recs, status
