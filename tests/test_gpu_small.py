@@ -177,15 +177,18 @@ def test_slot_list_packed(gpu_ctx, oracle, count, max_size, cs, ms, misaligned, 
     assert err == int((want == 1).sum())
 
 
-@pytest.mark.parametrize("gen_max,count,spoil", [(100, 20_001, 0), (300, 50_001, 0), (1500, 9_999, 0),
-                                                (2000, 30_001, 0), (700, 30_001, 3000)])
-def test_slot_list_repack(gpu_ctx, oracle, gen_max, count, spoil):
+@pytest.mark.parametrize("gen_max,count,spoil,cs,ms", [(100, 20_001, 0, 4, 0), (300, 50_001, 0, 4, 0),
+                                                      (1500, 9_999, 0, 4, 0), (2000, 30_001, 0, 4, 0),
+                                                      (700, 30_001, 3000, 4, 0), (500, 20_001, 0, 8, 16),
+                                                      (500, 20_001, 0, 4, 100)])
+def test_slot_list_repack(gpu_ctx, oracle, lib, gen_max, count, spoil, cs, ms):
     """A channel of 4 KiB slots (max_message_size 4096) carrying shorter messages: each wave
     whose window holds nothing longer than 2 KiB repacks it (crc_small.hip REPACK, rg lanes per
     message); `spoil` puts one 3,000-B message in every 50th window, so repacked and general
-    waves share the launch. Publish and verify bit-exact against the oracle (payload starts
-    off 16-B boundaries included)."""
-    pre, pay, pay_off, sizes, order, ps = build_slot_list(count, count + gen_max, 4, 0, gen_max, 0.2, 0.0)
+    waves share the launch; a metadata span (fused), and metadata over 64 B (the small kernel +
+    the slot-finish kernel). Publish and verify bit-exact against the oracle (payload starts off
+    16-B boundaries included)."""
+    pre, pay, pay_off, sizes, order, ps = build_slot_list(count, count + gen_max, cs, ms, gen_max, 0.2, 0.0)
     if spoil:  # (payload room: build_slot_list sized it for gen_max, so give the slot a fresh area)
         extra = []
         for i in range(0, count, 64 * 50):
@@ -195,11 +198,11 @@ def test_slot_list_repack(gpu_ctx, oracle, gen_max, count, spoil):
             sizes[i] = spoil
         pay = np.concatenate([pay, np.random.default_rng(7).integers(0, 256, len(extra) * (spoil + 64) + 64,
                                                                       dtype=np.uint8)])
-        pre = slots.make_prefixes(count, sizes, checksum_size=4, metadata_size=0, seed=count + gen_max + 1)
+        pre = slots.make_prefixes(count, sizes, checksum_size=cs, metadata_size=ms, seed=count + gen_max + 1)
         pre = pre.reshape(-1).copy()
-    got_pre, st, _ = run_slot_list(gpu_ctx, pre, pay, pay_off, sizes, order, ps, 4, 0, 4096, gpu.SLOT_CALCULATE)
+    got_pre, st, _ = run_slot_list(gpu_ctx, pre, pay, pay_off, sizes, order, ps, cs, ms, 4096, gpu.SLOT_CALCULATE)
     arena, po, yo = oracle_arena(pre, pay, pay_off, count, ps)
-    oracle.publish_slots(arena, po, yo, sizes, 4, 0)
+    oracle.publish_slots(arena, po, yo, sizes, cs, ms)
     assert (st == 0).all()
     bad = np.nonzero(got_pre != arena[:len(pre)])[0]
     assert len(bad) == 0, f"{len(bad)} prefix bytes differ, first slots {np.unique(bad // ps)[:8]}"
@@ -208,11 +211,31 @@ def test_slot_list_repack(gpu_ctx, oracle, gen_max, count, spoil):
     for i in np.nonzero(rng.random(count) < 0.1)[0]:
         if sizes[i]:
             pay2[int(pay_off[i]) + int(rng.integers(0, int(sizes[i])))] ^= np.uint8(1 << int(rng.integers(0, 8)))
-    _, st, err = run_slot_list(gpu_ctx, got_pre, pay2, pay_off, sizes, order, ps, 4, 0, 4096, gpu.SLOT_VERIFY)
+    _, st, err = run_slot_list(gpu_ctx, got_pre, pay2, pay_off, sizes, order, ps, cs, ms, 4096, gpu.SLOT_VERIFY)
     arena2, po, yo = oracle_arena(got_pre, pay2, pay_off, count, ps)
-    want = oracle.verify_slots(arena2, po, yo, sizes, 4, 0)
+    want = oracle.verify_slots(arena2, po, yo, sizes, cs, ms)
     assert np.array_equal(st, want)
     assert err == int((want == 1).sum())
+    if ms <= 64:  # the fused kernel: which waves repacked, from its per-wave records
+        r = wave_records(gpu_ctx, lib, lambda: run_slot_list(gpu_ctx, got_pre, pay2, pay_off, sizes, order, ps, cs,
+                                                              ms, 4096, gpu.SLOT_VERIFY))
+        live = (r[:, 0] > 0) & (((r[:, 7] >> np.uint64(32)) & np.uint64(0xFFFF)) > 0)
+        rp = ((r[:, 7] >> np.uint64(49)) & np.uint64(1)) == 1
+        windows_spoiled = len(range(0, count, 64 * 50)) if spoil else 0
+        assert int((live & ~rp).sum()) <= windows_spoiled and int((live & rp).sum()) > 0
+
+
+def wave_records(ctx, lib, run):
+    """The fused slot kernel's per-wave experiment records (crc_small.hip PROBE: lane 7 = nk << 32
+    | fast << 48 | repack << 49 | rg << 52) for one call `run()`."""
+    waves = int(lib.subspace_crc_testutil_probe_waves(ctx._h, 1 << 22))
+    rb = torch.zeros(waves * 8, dtype=torch.int64, device=DEV)
+    assert lib.subspace_crc_testutil_probe(ctx._h, rb.data_ptr()) == 0
+    try:
+        run()
+    finally:
+        lib.subspace_crc_testutil_probe(ctx._h, None)
+    return rb.cpu().numpy().view(np.uint64).reshape(waves, 8)
 
 
 def test_slot_list_small_matches_ragged(gpu_ctx, lib):
