@@ -460,6 +460,7 @@ bool small_fits(u64 max_len, bool aligned16) { return max_len <= (aligned16 ? kS
 // whose 128-B lines hold `max_ext` extended bytes (a message's length + its start & 15), at
 // most 32 (a half-tile). A longer message than the bound is still computed whole (long path).
 u32 small_lanes(u64 max_ext) {
+  if (max_ext == 0) return 32;  // (no bound given: the half-tile form; waves still repack)
   u32 g = 1;
   while (g < 32 && 128ull * g < max_ext) g <<= 1;
   return g;
