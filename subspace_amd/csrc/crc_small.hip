@@ -413,8 +413,17 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32 code = (k < nk && msg_of(k) < count) ? 0u : kCodeSkip;
     if (l == 31u) lds_st64(sring + 8u * (2u * (k & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
   };
-  // UNIFORM FAST (G < 32, no slots): a uniform batch of messages of exactly C bytes on 16-B
-  // boundaries -- no masks, codes or padding; the tile's address from m * stride
+  // UNIFORM FAST (G < 32, no slots): a uniform batch of messages of L <= C bytes on 16-B
+  // boundaries -- the tile's address from m * stride, one address and 8 immediate-offset loads
+  // (reading C bytes per message: past L they are the next messages' bytes, masked), one padding
+  // p = C - L for every message, no codes. A tile holding a message whose C bytes would reach
+  // past the batch (the last few) takes the clamped loads instead.
+  const u64 uL = a.ulen;
+  const u32 upad = C - (u32)(uL < C ? uL : C);
+  // the last message whose C-byte read stays inside the batch (none: -1)
+  const int64_t usafe = upad == 0u ? (int64_t)count - 1
+                        : a.ustride == 0 ? -1
+                                         : (int64_t)count - 1 - (int64_t)((upad + a.ustride - 1) / a.ustride);
   auto u_off = [&](u32 k) __attribute__((always_inline)) {
     const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
     u64 m = msg_of(kk);
@@ -423,8 +432,30 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     asm volatile("" : "+v"(off));
     return off;
   };
+  auto u_safe = [&](u32 k) __attribute__((always_inline)) {  // wave-uniform: the tile's last message
+    const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
+    return (int64_t)(M * (t0 + (u64)kk * nw) + M - 1) <= usafe;
+  };
+  auto u_load = [&](u32x4 (&D)[8], u32 k, u64 q) __attribute__((always_inline)) {
+    if (u_safe(k)) {
+      load_at(D, q);
+    } else {
+      const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
+      u64 m = msg_of(kk);
+      m = m < count ? m : count - 1;
+      load_lines(D, m * a.ustride, (u32)uL);
+    }
+  };
   auto process_u = [&](const u32x4 (&cur)[8], u32 k) __attribute__((always_inline)) {
-    const u32 crc = line_crc32_2chain(cur, li == 0u ? a.init : 0u, lc0, lc1, z64);
+    u32x4 d[8];
+#pragma unroll
+    for (int b = 0; b < 8; b++) d[b] = cur[b];
+    if (upad != 0u) {  // (uniform) the bytes from L on
+      const int v0 = (int)uL - 128 * (int)li;
+      keep_bytes(d, 0u, v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0));
+    }
+    const u32 crc = G == 1 && uL <= 64u ? line_crc32_lo(d, a.init, lc0, lc1, z64)
+                                        : line_crc32_2chain(d, li == 0u ? a.init : 0u, lc0, lc1, z64);
     const u32 v = msg_value(crc);
     const u32 code = (k < nk && msg_of(k) < count) ? 0u : kCodeSkip;
     if (li == (u32)G - 1u) lds_st64(sring + 8u * ((k & (W - 1u)) * M + mj), (u64)v | ((u64)code << 32));
@@ -434,7 +465,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32 hh = (u32)lane % M, ti = (u32)lane / M;
     const u64 e = lds_ld64(sring + 8u * (u32)lane);
     const u64 m = M * (t0 + (u64)(kf + ti) * nw) + hh;
-    if (ti < nt && (u32)(e >> 32) == 0u) a.out[m] = (u32)e ^ a.final_xor;
+    const u32 r = upad ? inv_bits((u32)e, upad, kSmallInvOps) : (u32)e;
+    if (ti < nt && (u32)(e >> 32) == 0u) a.out[m] = r ^ a.final_xor;
     wave_lds_sync();
   };
   // REPACK (G = 32 kernels): a wave whose window (every tile of the wave) holds no message
@@ -581,8 +613,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // r05z)
   const bool conf = !flive || (wL == (u64)kSmallMaxExt && (wS & 15u) == 0 && (!SLOT || wL <= a.max_len));
   const bool fast = G == 32 && nk <= kSmallRingTiles && __ballot(!conf) == 0;
-  const bool fastu = !SLOT && G < 32 && a.offsets == nullptr && a.ulen == (u64)C && (a.ustride & 15u) == 0 &&
-                     ((uintptr_t)base & 15u) == 0;
+  const bool fastu = !SLOT && G < 32 && a.offsets == nullptr && a.ulen != 0 && a.ulen <= (u64)C &&
+                     (a.ustride & 15u) == 0 && ((uintptr_t)base & 15u) == 0;
   bool repack = false;
   if constexpr (G == 32) {
     if (!fast && nk <= kSmallRingTiles) {
@@ -683,14 +715,14 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       const u64 qB = u_off(k + 1);
       issue_prio_hi();
       drain_before_issue();  // tile k's lines
-      load_at(B, qB);
+      u_load(B, k + 1, qB);
       issue_prio_lo();
       if (k && (k & kWinMask) == 0u) flush_u(k - W, W);
       process_u(A, k);
       const u64 qA = u_off(k + 2);
       issue_prio_hi();
       drain_before_issue();
-      load_at(A, qA);
+      u_load(A, k + 2, qA);
       issue_prio_lo();
       if constexpr (W == 1) flush_u(k, 1u);
       process_u(B, k + 1);
@@ -702,10 +734,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
   } else {
     // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines; the
-    // ring is finished whenever it holds W tiles (64 messages), right after the next tile's loads are issued
-    // (so the stores retire during that tile's compute), and at the end (crc_ragged.hip's loop,
-    // without descriptors). Nothing else lives across the loop (register-parked
-    // values, 64-tile windows and a flush only after the loop each measured slower).
+    // ring is finished whenever it holds W tiles (64 messages), right after the next tile's
+    // loads are issued (so the stores retire during that tile's compute), and at the end
+    // (crc_ragged.hip's loop, without descriptors). Nothing else lives across the loop
+    // (register-parked values, 64-tile windows and a flush only after the loop
+    // each measured slower).
     for (; k + 1 < nk; k += 2) {
       issue_prio_hi();       // (crc_device.h)
       drain_before_issue();  // tile k's lines and tile k+1's record
