@@ -29,7 +29,9 @@
 //    min(128 l + 16 b, last block), so the lanes past the end re-read the last block (one
 //    cache line) instead of branching around loads, and a half with nothing to read (no
 //    message, an empty one, or one too long for this kernel) reads a 16-B block of the step
-//    table. Loads never touch a 16-B block that holds no byte of the message.
+//    table. Loads never touch a 16-B block that holds no byte of the message (the uniform
+//    FAST form excepted: it reads a message's C bytes, the next messages' beyond L, never past
+//    the batch; tests/test_kernel_address_model.py).
 //  * Line 0 starts from seed = Z_mis^{-1}(init), every other line from 0, so each half gives
 //      V = crc_raw(seed, 0^mis || D || 0^p) = Z_p(crc_raw(init, D)),   p = 4096 - E;
 //    each message's value and code are parked in a per-wave LDS ring (32 tiles), and every 32

@@ -432,6 +432,51 @@ def test_small_kernel_loads_stay_in_messages(seed, count, G):
                 assert covered.get(m) == set(range(s, s + L)), m
 
 
+def uniform_fast_reads(count, L, stride, G, grid):
+    """Replays crc_small.hip's UNIFORM FAST loads (a uniform batch of L-byte messages, stride
+    16-B aligned, G lanes per message, C = 128 G >= L): for every tile the kernel loads, the byte
+    ranges its lanes read -- [m * stride, m * stride + C) for the tile's messages when the tile's
+    last message is at most usafe (u_safe), else the clamped blocks of [m * stride, + L)."""
+    M, C = 64 // G, 128 * G
+    upad = C - min(L, C)
+    usafe = count - 1 if upad == 0 else (-1 if stride == 0 else count - 1 - -(-upad // stride))
+    ntiles = -(-count // M)
+    nw = 8 * grid
+    for b in range(grid):
+        for wid in range(8):
+            t0 = front_slot(b, grid, wid)
+            nk = (ntiles - t0 + nw - 1) // nw if t0 < ntiles else 0
+            for k in range(nk + 2):  # (the loop loads up to two tiles past the last: clamped)
+                kk = k if k < nk else max(nk - 1, 0)
+                if not nk:
+                    continue
+                last = M * (t0 + kk * nw) + M - 1
+                for j in range(M):
+                    m = min(M * (t0 + kk * nw) + j, count - 1)
+                    if last <= usafe:
+                        yield m * stride, m * stride + C
+                    else:
+                        lastb = (L - 1) & ~15
+                        for li in range(G):
+                            for blk in range(8):
+                                o = m * stride + min(128 * li + 16 * blk, lastb)
+                                yield o, o + 16
+
+
+@pytest.mark.parametrize("count,L,stride,G,grid", [(1000, 1000, 1008, 8, 4), (5000, 16, 16, 1, 8), (301, 129, 144, 2, 3),
+                                                   (70, 100, 112, 1, 2), (4097, 2000, 2000, 16, 16),
+                                                   (63, 512, 512, 4, 1), (2, 17, 32, 1, 1)])
+def test_uniform_fast_reads_stay_in_the_batch(count, L, stride, G, grid):
+    """The packed uniform FAST loop reads past a message's L bytes (into the next messages) but
+    never past the batch: every range it reads lies in [0, end) with end the batch's last byte
+    rounded up to its 16-B block (the clamped loads' rule: whole 16-B blocks holding message
+    bytes), and the unclamped C-byte reads end within the batch itself."""
+    end = (count - 1) * stride + L
+    end16 = (end + 15) & ~15
+    for lo, hi in uniform_fast_reads(count, L, stride, G, grid):
+        assert 0 <= lo and hi <= (end if hi - lo == 128 * G else end16), (lo, hi, end)
+
+
 def fast_line_blocks(s, l):
     """The FAST loop's 8 loads of lane l (one address, immediate offsets 0..112)."""
     return [s + 128 * l + 16 * b for b in range(8)]
