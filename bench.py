@@ -99,8 +99,9 @@ def parse():
                          "bytes (strong scaling) + RCCL gather; "
                          "E: 8 Mi x 4 KiB sharded round-robin over the GPUs (strong scaling) + RCCL gather")
     ap.add_argument("--configs", default=None,
-                    help="secondary configs timed after the headline at N = 1 (comma list of C, Cu, D, Du, S; "
-                         "default C,D,Du,S with workload B, none otherwise; 'none' disables)")
+                    help="secondary configs timed after the headline at N = 1 (comma list of C, Cu, D, Du, S, "
+                         "Usmall, S_short; default C,D,Du,S,Usmall,S_short with workload B, none otherwise; "
+                         "'none' disables)")
     ap.add_argument("--config-iters", type=int, default=20)
     ap.add_argument("--no-solo", action="store_true", help="N > 1: skip rank 0's single-GPU reference leg")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
@@ -712,6 +713,10 @@ def secondary_configs(ctx, dev, names, iters) -> dict:
             del buf, out
         elif name == "S":
             res.update(slot_configs(ctx, dev, iters))
+        elif name == "Usmall":
+            res[name] = small_uniform_config(ctx, dev)
+        elif name == "S_short":
+            res[name] = short_slots_config(ctx, dev)
 
     # No torch.cuda.empty_cache() between configs: VRAM given back to the driver is wiped in the
     # background for seconds (every HBM-bound kernel ~2-4 % slower meanwhile: config S after
@@ -723,6 +728,87 @@ def secondary_configs(ctx, dev, names, iters) -> dict:
         except Exception as e:  # a secondary config must never cost the headline line
             res[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
     return res
+
+
+def small_uniform_config(ctx, dev) -> dict:
+    """Informational (no BASELINE config): 1 Mi messages of 256 B, stride 256, through
+    subspace_crc32_batch_uniform -- the small-message kernel packed two lanes per message
+    (crc_small.hip G = 2), 4 rotated batches; 256 sampled CRCs checked against the host
+    drop-in (SubspaceCRC32, include/subspace/checksum.h)."""
+    import torch
+    from subspace_amd import checksum, gpu
+    n, L, nb = 1 << 20, 256, 4
+    bufs = [torch.empty(n * L, dtype=torch.uint8, device=dev) for _ in range(nb)]
+    for k, b in enumerate(bufs):
+        gpu.fill_uniform(b, L, L, n, seed=0x5EED0256 + k)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    i = [0]
+
+    def call():
+        ctx.crc32_uniform(bufs[i[0] % nb], L, L, n, out)
+        i[0] += 1
+    ms = time_calls(call, 400)
+    ctx.crc32_uniform(bufs[0], L, L, n, out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    host = bufs[0].cpu().numpy()
+    idx = np.random.default_rng(1).choice(n, 256, replace=False)
+    ok = all(checksum.subspace_crc32(0xFFFFFFFF, host[j * L:(j + 1) * L]) == int(got[j]) for j in idx)
+    line = config_line(n * L, ms, ok, "subspace_crc32_batch_uniform: crc32_small_kernel<512, false, false, 2> "
+                       "(G = 2 lanes per message, the uniform FAST loop)", extra={
+                           "workload": "Usmall (informational): 1 Mi x 256 B messages, stride 256, 4 batches rotated",
+                           "messages_per_s": round(n / (ms * 1e-3), 1),
+                           "check": "256 sampled CRCs equal the host drop-in's SubspaceCRC32"})
+    del bufs, out
+    return line
+
+
+def short_slots_config(ctx, dev) -> dict:
+    """Informational (no BASELINE config): a channel of 65,536 4 KiB slots (stride 4,160)
+    carrying 256-B messages, published by the fused strided kernel, then drained as shuffled
+    device slot lists (max_message_size 4096) through subspace_crc32_slots -- the small kernel's
+    waves repack their windows two lanes per message (crc_small.hip REPACK); 4 rotated copies.
+    Bytes: span 0 + payload per slot. Check: every slot verifies (publish and verify are
+    different kernels)."""
+    import torch
+    from subspace_amd import gpu, slots
+    n, area, L, cs, ms_, nbuf = MSGS, MSG_BYTES, 256, 4, 0, 4
+    ps, stride = slots.compute_prefix_size(cs, ms_), slots.slot_stride(area, cs, ms_)
+    rng = np.random.default_rng(0x5EED0257)
+    host = rng.integers(0, 256, stride * n, dtype=np.uint8)
+    host.reshape(n, stride)[:, :ps] = slots.make_prefixes(n, np.full(n, L, dtype=np.uint64), checksum_size=cs,
+                                                          metadata_size=ms_, seed=7)
+    bufs = [torch.from_numpy(host).to(dev) for _ in range(nbuf)]
+    d_sizes = torch.full((n,), L, dtype=torch.int64, device=dev)
+    for b in bufs:
+        ctx.crc32_slots_strided(b, stride, n, sizes=d_sizes, checksum_size=cs, metadata_size=ms_,
+                                mode=gpu.SLOT_CALCULATE)
+    order = rng.permutation(n).astype(np.uint64)
+    recs = []
+    for b in bufs:
+        b0 = np.uint64(b.data_ptr())
+        r = np.stack([b0 + order * np.uint64(stride), b0 + order * np.uint64(stride) + np.uint64(ps),
+                      np.full(n, L, dtype=np.uint64)], axis=1)
+        recs.append(torch.from_numpy(np.ascontiguousarray(r).view(np.int64)).to(dev))
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    errs = torch.zeros(1, dtype=torch.int32, device=dev)
+    i = [0]
+
+    def call():
+        ctx.crc32_slots(recs[i[0] % nbuf], max_message_size=area, checksum_size=cs, metadata_size=ms_,
+                        mode=gpu.SLOT_VERIFY, status=status, error_count=errs)
+        i[0] += 1
+    ms = time_calls(call, 400)
+    torch.cuda.synchronize()
+    ok = int(errs.item()) == 0 and bool((status == 0).all().item())
+    line = config_line(n * (L + 44), ms, ok, "subspace_crc32_slots: crc32_small_kernel<512, true, false, 32> "
+                       "(REPACK: two lanes per message)", extra={
+                           "workload": "S_short (informational): 65,536 slots of 4 KiB (stride 4,160) carrying 256-B "
+                                       "messages, shuffled device slot lists, verify, 4 copies rotated",
+                           "slots_per_s": round(n / (ms * 1e-3), 1),
+                           "check": "every slot verifies (published by the fused strided kernel)"})
+    del bufs, recs, status
+    return line
 
 
 def slot_leg_check(mode, buf, n, stride, ps, size, cs, ms_, status, errs, rng):
@@ -1122,7 +1208,8 @@ def main():
             return {"error": f"{type(e).__name__}: {e}"[:300]}
 
     configs = None
-    cfg_names = args.configs if args.configs is not None else ("C,D,Du,S" if args.workload == "B" else "none")
+    cfg_names = args.configs if args.configs is not None else ("C,D,Du,S,Usmall,S_short" if args.workload == "B"
+                                                               else "none")
     if world == 1 and cfg_names != "none":
         configs = optional(lambda: secondary_configs(ctx, dev, [c for c in cfg_names.split(",") if c],
                                                      args.config_iters))

@@ -7,7 +7,8 @@ calls made and writes profiles/traffic_configs.json, which bench.py reads.
 
   python tools/pmc_configs.py <config> [calls]
   config: C, Cu, D, Du, S_publish, S_verify, S_meta_publish, S_meta_verify, S_list_publish,
-          S_list_verify (bench.py's secondary configs, the same shapes and synthetic data)
+          S_list_verify, Usmall, S_short (bench.py's secondary configs, the same shapes and
+          synthetic data)
 
 Prints one JSON line: the config, the calls made and the algorithmic bytes per call (bench.py's
 "bytes"). Verify legs run over unpublished slots (every slot a mismatch): the same reads."""
@@ -53,6 +54,42 @@ def main():
         else:
             fn = lambda: ctx.crc32_uniform(buf, L, L, n, out)  # noqa: E731
         nbytes = n * L
+    elif name == "Usmall":  # bench.py small_uniform_config: 1 Mi x 256 B, 4 rotated batches
+        n, L = 1 << 20, 256
+        bufs = [torch.empty(n * L, dtype=torch.uint8, device=dev) for _ in range(4)]
+        for k, b in enumerate(bufs):
+            gpu.fill_uniform(b, L, L, n, seed=0x5EED0256 + k)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        i = [0]
+
+        def fn():
+            ctx.crc32_uniform(bufs[i[0] % 4], L, L, n, out)
+            i[0] += 1
+        nbytes = n * L
+    elif name == "S_short":  # bench.py short_slots_config: 256-B messages in 4 KiB slots, shuffled list
+        n, area, L, cs = 65536, 4096, 256, 4
+        ps, stride = slots.compute_prefix_size(cs, 0), slots.slot_stride(area, cs, 0)
+        rng = np.random.default_rng(0x5EED0257)
+        host = rng.integers(0, 256, stride * n, dtype=np.uint8)
+        host.reshape(n, stride)[:, :ps] = slots.make_prefixes(n, np.full(n, L, dtype=np.uint64), checksum_size=cs,
+                                                              metadata_size=0, seed=7)
+        bufs = [torch.from_numpy(host).to(dev) for _ in range(4)]
+        order = rng.permutation(n).astype(np.uint64)
+        recs = []
+        for b in bufs:
+            b0 = np.uint64(b.data_ptr())
+            r = np.stack([b0 + order * np.uint64(stride), b0 + order * np.uint64(stride) + np.uint64(ps),
+                          np.full(n, L, dtype=np.uint64)], axis=1)
+            recs.append(torch.from_numpy(np.ascontiguousarray(r).view(np.int64)).to(dev))
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+        errs = torch.zeros(1, dtype=torch.int32, device=dev)
+        i = [0]
+
+        def fn():
+            ctx.crc32_slots(recs[i[0] % 4], max_message_size=area, checksum_size=cs, metadata_size=0,
+                            mode=gpu.SLOT_VERIFY, status=status, error_count=errs)
+            i[0] += 1
+        nbytes = n * (L + 44)
     else:  # config S's slots (bench.py slot_configs): 65,536 x 4 KiB payloads, 4 rotated copies
         n, size, cs = 65536, 4096, 4
         ms_ = 16 if name.startswith("S_meta") else 0
