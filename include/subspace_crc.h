@@ -91,7 +91,9 @@ int subspace_crc_ctx_check(subspace_crc_ctx* ctx, void* stream);
 int subspace_crc_ctx_reserve(subspace_crc_ctx* ctx, uint64_t max_messages, uint64_t max_tiles);
 
 /* Fixed-size batch: message i is the `length` bytes at dev_base + i*stride.
- * stride >= length. Any length (0 allowed); any stride. */
+ * stride >= length. Any length (0 allowed); any stride. The kernels read only inside
+ * [dev_base, dev_base + (count-1)*stride + length), the end rounded up to 16 bytes (gaps
+ * between messages included: they are read and ignored). */
 int subspace_crc32_batch_uniform(subspace_crc_ctx* ctx, const void* dev_base, uint64_t stride, uint64_t length,
                                  uint64_t count, uint32_t init, uint32_t flags, uint32_t* dev_out, void* stream);
 
