@@ -755,7 +755,7 @@ def small_uniform_config(ctx, dev) -> dict:
     idx = np.random.default_rng(1).choice(n, 256, replace=False)
     ok = all(checksum.subspace_crc32(0xFFFFFFFF, host[j * L:(j + 1) * L]) == int(got[j]) for j in idx)
     line = config_line(n * L, ms, ok, "subspace_crc32_batch_uniform: crc32_small_kernel<512, false, false, 2> "
-                       "(G = 2 lanes per message, the uniform FAST loop)", extra={
+                       "(G = 2 lanes per message, the uniform FAST loop)", name="Usmall", extra={
                            "workload": "Usmall (informational): 1 Mi x 256 B messages, stride 256, 4 batches rotated",
                            "messages_per_s": round(n / (ms * 1e-3), 1),
                            "check": "256 sampled CRCs equal the host drop-in's SubspaceCRC32"})
@@ -802,7 +802,7 @@ def short_slots_config(ctx, dev) -> dict:
     torch.cuda.synchronize()
     ok = int(errs.item()) == 0 and bool((status == 0).all().item())
     line = config_line(n * (L + 44), ms, ok, "subspace_crc32_slots: crc32_small_kernel<512, true, false, 32> "
-                       "(REPACK: two lanes per message)", extra={
+                       "(REPACK: two lanes per message)", name="S_short", extra={
                            "workload": "S_short (informational): 65,536 slots of 4 KiB (stride 4,160) carrying 256-B "
                                        "messages, shuffled device slot lists, verify, 4 copies rotated",
                            "slots_per_s": round(n / (ms * 1e-3), 1),
