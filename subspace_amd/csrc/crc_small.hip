@@ -526,7 +526,25 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // Finish and store the ring's tiles kf .. kf+nt-1 (nt <= 32): lane i takes message i of the
   // window, i.e. tile kf + i/2, half i & 1 (its value and code from the ring; a slot's prefix
   // offset from its record again).
-  auto flush = [&](u32 kf, u32 nt) __attribute__((always_inline)) {
+  // SLOT, G < 32 (windows of G tiles, an in-loop flush every window): a window's prefix offsets
+  // are loaded at the previous window's flush and its prefix words at its own flush before the
+  // next tile's loads are issued (flush_issue), so the flush's reads wait for neither a record
+  // round trip nor that tile (vmcnt retires in order); flush_any(..., true) hashes them.
+  u64 Pn = 0, Pc = 0;  // the next / current window's prefix offset of this lane's entry
+  u32 fw[14], fW1[kW];
+  auto win_pref = [&](u32 kf) __attribute__((always_inline)) -> u64 {
+    const u32 ti = (u32)lane / M, hh = (u32)lane % M;
+    const u64 m = M * (t0 + (u64)(kf + ti) * nw) + hh;
+    return a.prefixes[(kf + ti < nk && m < count ? m : 0) * a.pstride];
+  };
+  auto flush_issue = [&](u32 kf) __attribute__((always_inline)) {
+    if (kf != 0) {
+      Pc = Pn;
+      span_load(base + Pc - a.pdelta, fw, fW1);
+    }
+    Pn = win_pref(kf + W);
+  };
+  auto flush_any = [&](u32 kf, u32 nt, bool pre) __attribute__((always_inline)) {
     wave_lds_sync();
     const u32 hh = (u32)lane % M, ti = (u32)lane / M;
     const bool valid = ti < nt;
@@ -553,11 +571,12 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       const bool live = code != kCodeSkip && !oversize;
       // the first window's prefix terms come from the prologue (every window, under the host's
       // grid rule); a later window's are loaded here
-      const uint8_t* pfx = (kf == 0 ? flive : live) ? base + (kf == 0 ? fpre : a.prefixes[mc * a.pstride]) - a.pdelta
-                                                     : safe;  // (a read-only block)
+      const uint8_t* pfx =
+          (kf == 0 ? flive : live) ? base + (kf == 0 ? fpre : (pre ? Pc : a.prefixes[mc * a.pstride])) - a.pdelta
+                                   : safe;  // (a read-only block)
       u32 F = eF, S = eS, H = eH;
       bool has = ehas;
-      if (kf != 0 && SUBSPACE_SMALL_VARIANT != 3) H = span_crc(pfx, F, S, has);
+      if (kf != 0 && SUBSPACE_SMALL_VARIANT != 3) H = pre ? span_hash(fw, fW1, F, S, has) : span_crc(pfx, F, S, has);
       // Z_p(crc_raw(H, payload)) = Z_C(Z_mis^{-1}(H)) ^ V, then Z_p undone
       const u32 Hm = inv_bits(H, half ? (code >> 12) & 15u : 0u, 4);
       const u32 X = opmul(sbase, G == 32 ? kUniSlotOpZ4096 : kSmallOpZC, Hm) ^ v;
@@ -570,6 +589,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
     wave_lds_sync();
   };
+  auto flush = [&](u32 kf, u32 nt) __attribute__((always_inline)) { flush_any(kf, nt, false); };
+  constexpr bool kSplit = SLOT && G < 32;
   // FAST waves' flush: one window (kf = 0), every code 0 (a whole aligned 4 KiB message: no
   // padding, no mis) or none -- no long messages, no inverses, no prefix reload (r05y: 0.5-0.7 us
   // per 65,536-slot list against the general flush).
@@ -744,19 +765,24 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     for (; k + 1 < nk; k += 2) {
       issue_prio_hi();       // (crc_device.h)
       drain_before_issue();  // tile k's lines and tile k+1's record
+      const bool wb = k && (k & kWinMask) == 0u;
+      if constexpr (kSplit) {
+        if (wb) flush_issue(k - W);
+      }
       const u64 s1 = sB, L1 = LB;
       fetch(k + 2, sA, LA);
       load_lines(B, s1, ext(k + 1, s1, L1));
       issue_prio_lo();
-      if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
+      if (wb) flush_any(k - W, W, kSplit);
       process(A, sc, Lc, k);
       issue_prio_hi();
       drain_before_issue();
+      if constexpr (kSplit && W == 1) flush_issue(k);
       const u64 s2 = sA, L2 = LA;
       fetch(k + 3, sB, LB);
       load_lines(A, s2, ext(k + 2, s2, L2));
       issue_prio_lo();
-      if constexpr (W == 1) flush(k, 1u);  // (one-tile windows: tile k before tile k + 1)
+      if constexpr (W == 1) flush_any(k, 1u, kSplit);  // (one-tile windows: tile k before tile k + 1)
       process(B, s1, L1, k + 1);
       sc = s2;
       Lc = L2;
