@@ -369,15 +369,17 @@ def test_r02s3i_prefix_variant_was_in_bounds():
 
 
 # ------------------------------------------------------------------ small-message kernel
-def small_kernel_loads(starts, lengths, G):
-    """Replays crc32_small_kernel<512> (crc_small.hip): per wave (order-0 front, G workgroups x 8
-    waves) the tiles whose lines it loads -- the prologue's tile 0, then tiles k+1 and k+2 per
-    loop pair, clamped records past the wave's last tile -- and per half the 16-B blocks of
-    load_lines: s0 + min(128 l + 16 b, last block) for a half with E = L + (s & 15) in
-    [1, 4096] and L > 0, else the step table's block (None here). Yields (message or None,
-    block address or None); returns nothing else."""
+def small_kernel_loads(starts, lengths, G, lanes=32):
+    """Replays crc32_small_kernel<512, SLOT, false, lanes>'s general loop (crc_small.hip): per wave
+    (order-0 front, G workgroups x 8 waves) the tiles whose lines it loads -- the prologue's tile
+    0, then tiles k+1 and k+2 per loop pair, clamped records past the wave's last tile -- and per
+    message (M = 64 / lanes per tile, C = 128 lanes bytes) the 16-B blocks of load_lines: line li
+    of message mj loads s0 + min(128 li + 16 b, last block) for E = L + (s & 15) in [1, C] and
+    L > 0, else the step table's block (None here; longer messages take long_crc). Yields
+    (message or None, block address or None); returns nothing else."""
     count = len(starts)
-    ntiles = (count + 1) // 2
+    M, C = 64 // lanes, 128 * lanes
+    ntiles = (count + M - 1) // M
     nw = 8 * G
     for b in range(G):
         for wid in range(8):
@@ -389,36 +391,40 @@ def small_kernel_loads(starts, lengths, G):
                 ks += [k + 1, k + 2]
                 k += 2
             for k in ks:
-                for h in (0, 1):
-                    m = 2 * (t0 + k * nw) + h
+                for mj in range(M):
+                    m = M * (t0 + k * nw) + mj
                     present = k < nk and m < count
                     kk = k if k < nk else max(nk - 1, 0)
-                    mr = min(2 * (t0 + kk * nw) + h if nk else 0, count - 1)  # the record read
+                    mr = min(M * (t0 + kk * nw) + mj if nk else 0, count - 1)  # the record read
                     s, L = int(starts[mr]), int(lengths[mr])
                     E = L + (s & 15)
-                    if not (present and L and E <= 4096):
+                    if not (present and L and E <= C):
                         yield None, None
                         continue
                     assert mr == m
                     lastb = (E - 1) & ~15
-                    for l in range(32):
+                    for li in range(lanes):
                         for blk in range(8):
-                            yield m, (s & ~15) + min(128 * l + 16 * blk, lastb)
+                            yield m, (s & ~15) + min(128 * li + 16 * blk, lastb)
 
 
-@pytest.mark.parametrize("seed,count,G", [(0, 1, 1), (1, 2, 1), (2, 3, 1), (3, 999, 63), (4, 5001, 256),
-                                          (5, 30001, 256)])
-def test_small_kernel_loads_stay_in_messages(seed, count, G):
-    """Every line load of the small-message kernel is a 16-B-aligned block holding at least one
-    byte of its own message (no load outside the caller's messages; messages at any offset &
-    15, empty ones, and ones over a half-tile, which read only the step table), and every byte
-    of every message it computes is loaded."""
+@pytest.mark.parametrize("seed,count,G,lanes", [(0, 1, 1, 32), (1, 2, 1, 32), (2, 3, 1, 32), (3, 999, 63, 32),
+                                                (4, 5001, 256, 32), (5, 30001, 256, 32), (6, 1, 1, 1),
+                                                (7, 67, 1, 1), (8, 999, 3, 2), (9, 4097, 256, 4),
+                                                (10, 3001, 7, 8), (11, 2049, 256, 16)])
+def test_small_kernel_loads_stay_in_messages(seed, count, G, lanes):
+    """Every line load of the small-message kernel's tile loop is a 16-B-aligned block holding at
+    least one byte of its own message (no load outside the caller's messages; messages at any
+    offset & 15, empty ones, and ones over C, which read only the step table), and every byte of
+    every message it computes is loaded -- for G = 32 lanes per message and the packed forms
+    (lanes = 1 .. 16: M = 64 / lanes messages per tile, each over lanes 128-B lines)."""
     rng = np.random.default_rng(seed)
-    lengths = rng.integers(0, 4097, count)
-    lengths[rng.random(count) < 0.05] = rng.integers(4097, 9000)
+    C = 128 * lanes
+    lengths = rng.integers(0, C + 1, count)
+    lengths[rng.random(count) < 0.05] = rng.integers(C + 1, 2 * C + 900)
     starts = np.cumsum(np.concatenate([[0], lengths[:-1] + rng.integers(0, 40, count - 1)])) + 7
     covered = {}
-    for m, addr in small_kernel_loads(starts, lengths, G):
+    for m, addr in small_kernel_loads(starts, lengths, G, lanes):
         if m is None:
             continue
         s, e = int(starts[m]), int(starts[m] + lengths[m])
@@ -428,7 +434,7 @@ def test_small_kernel_loads_stay_in_messages(seed, count, G):
     if count <= 5001:
         for m in range(count):
             s, L = int(starts[m]), int(lengths[m])
-            if L and L + (s & 15) <= 4096:
+            if L and L + (s & 15) <= C:
                 assert covered.get(m) == set(range(s, s + L)), m
 
 
