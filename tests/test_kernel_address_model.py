@@ -438,6 +438,81 @@ def test_small_kernel_loads_stay_in_messages(seed, count, G, lanes):
                 assert covered.get(m) == set(range(s, s + L)), m
 
 
+def small_kernel_repack_loads(starts, lengths, G):
+    """Replays crc32_small_kernel<512, SLOT, false, 32>'s REPACK loop (crc_small.hip): a wave with
+    at most 32 tiles whose window's messages all have E = L + (s & 15) <= 2,048 regroups its 2 nk
+    messages rg to a tile (rg = 1 .. 16 lanes each, the least with 128 rg >= every E): packed
+    tile j's lane i takes window entry e = j (64 / rg) + i / rg (the record lane e loaded: message
+    2 (t0 + (e / 2) nw) + e % 2) and loads line i % rg of it, clamped like load_lines; loads past
+    the wave's entries (the loop's tile nt) read the step table. Yields (message or None, block
+    address or None) for the repacking waves only, ('msg', m) for each non-empty message they
+    compute, then ('waves', number of them)."""
+    count = len(starts)
+    ntiles = (count + 1) // 2
+    nw = 8 * G
+    waves = 0
+    for b in range(G):
+        for wid in range(8):
+            t0 = front_slot(b, G, wid)
+            nk = (ntiles - t0 + nw - 1) // nw if t0 < ntiles else 0
+            if nk == 0 or nk > 32:
+                continue
+            live = [(2 * (t0 + (e // 2) * nw) + e % 2) for e in range(64)]
+            live = [m if e < 2 * nk and m < count else None for e, m in enumerate(live)]
+            ext = [int(lengths[m]) + (int(starts[m]) & 15) if m is not None else 0 for m in live]
+            if max(ext) > 2048:
+                continue
+            waves += 1
+            for m in live:
+                if m is not None and lengths[m]:
+                    yield "msg", m
+            rg = 1
+            while rg < 16 and max(ext) > 128 * rg:
+                rg *= 2
+            per = 64 // rg
+            nt = (2 * nk + per - 1) // per
+            for j in list(range(nt)) + [nt]:
+                for i in range(64):
+                    e = j * per + i // rg
+                    m = live[e] if e < 64 else None
+                    if m is None or lengths[m] == 0:
+                        yield None, None
+                        continue
+                    s, E = int(starts[m]), ext[e]
+                    lastb = (E - 1) & ~15
+                    for blk in range(8):
+                        yield m, (s & ~15) + min(128 * (i % rg) + 16 * blk, lastb)
+    yield "waves", waves
+
+
+@pytest.mark.parametrize("seed,count,G,top", [(20, 1, 1, 64), (21, 65, 1, 300), (22, 999, 63, 2048),
+                                              (23, 4001, 31, 1000), (24, 20001, 256, 129)])
+def test_small_kernel_repack_loads_stay_in_messages(seed, count, G, top):
+    """REPACK's loads obey the same rule as the tile loop's: every block holds a byte of its own
+    message and every byte of every message it computes is loaded, for each lane group size the
+    window's largest message selects."""
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(0, top + 1, count)
+    starts = np.cumsum(np.concatenate([[0], lengths[:-1] + rng.integers(0, 40, count - 1)])) + 3
+    starts = starts - (starts & 15) * (rng.random(count) < 0.5)  # some 16-B aligned
+    covered, waves, want = {}, 0, set()
+    for m, addr in small_kernel_repack_loads(starts, lengths, G):
+        if m == "waves":
+            waves = addr
+            continue
+        if m == "msg":
+            want.add(addr)
+            continue
+        if m is None:
+            continue
+        s, e = int(starts[m]), int(starts[m] + lengths[m])
+        assert addr % 16 == 0 and addr + 16 > s and addr < e, (m, s, e, addr)
+        covered.setdefault(m, set()).update(range(max(addr, s), min(addr + 16, e)))
+    assert waves > 0 and set(covered) == want
+    for m, byts in covered.items():
+        assert byts == set(range(int(starts[m]), int(starts[m] + lengths[m]))), m
+
+
 def uniform_fast_reads(count, L, stride, G, grid):
     """Replays crc_small.hip's UNIFORM FAST loads (a uniform batch of L-byte messages, stride
     16-B aligned, G lanes per message, C = 128 G >= L): for every tile the kernel loads, the byte
