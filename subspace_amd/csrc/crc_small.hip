@@ -119,8 +119,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // m * ustride and ulen (a kernel-argument branch)
   auto record = [&](u64 m, u64& s, u64& L) __attribute__((always_inline)) {
     if (a.offsets) {
-      s = a.offsets[m * a.ostride];
-      L = a.lengths[m * a.lstride];
+      const u64* po = a.offsets + m * a.ostride;
+      const u64* pl = a.lengths + m * a.lstride;
+      s = *po;
+      L = *pl;
+      asm volatile("" ::"v"(po), "v"(pl));  // (addresses live past the loads: load_at)
     } else {
       s = m * a.ustride;
       L = a.ulen;
@@ -471,37 +474,65 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     if (ti < nt && (u32)(e >> 32) == 0u) a.out[m] = r ^ a.final_xor;
     wave_lds_sync();
   };
-  // REPACK (G = 32 kernels): a wave whose window (every tile of the wave) holds no message
-  // longer than 2 KiB (extended) -- a channel of large slots carrying shorter messages -- packs
-  // its window's 64 messages rg lanes each (rg = 1 .. 16, the wave's own choice), rg tiles for
-  // the 64 instead of 32; message e of the window (lane e's records, read by ds_bpermute) is
-  // slot e % rM of packed tile e / rM. Lane li' applies Z_{128 (31-li')} -- the value as if the
-  // message filled a half-tile (its lines past rg from 0 contribute 0) -- so the ring, codes
-  // (p = 4096 - E) and flush are the general loop's.
-  u32 rg = 32, rlg = 5;
+  // REPACK (G = 32 kernels): a wave whose window is every tile of the wave (nk <= 32) and not
+  // FAST packs its window's messages into tiles by size: entry e (lane e's record, read by
+  // ds_bpermute) of E = L + (s & 15) bytes in [1, 4096] gets g_e = 2^c lanes, the least power of
+  // two with 128 g_e >= E; the entries are laid out by class, 32-lane ones first, so every
+  // group sits on a multiple of its size and never straddles a tile (sum of g_e / 64 tiles
+  // instead of nk). Lane li' of a group applies Z_{128 (31-li')} -- the value as if the message
+  // filled a half-tile (its lines past g_e contribute 0) -- then the butterfly's first c steps
+  // (row_bcast:15 for the 32-lane step), so the ring, codes (p = 4096 - E) and flush are the
+  // general loop's. Entries without lanes (none, empty, longer than 4 KiB, SLOT oversize) have
+  // their codes written to the ring in the prologue.
+  // class c's first lane position | first sorted index << 16, in lane c (one VGPR: kept out of
+  // the SGPRs the other loops use)
+  u32 vbn = 0;
+  u32 vT = 0, vS = 0, rnt = 0;  // lane positions used; sorted index (this lane) -> entry; tiles
+  u32 rcmax = 0;        // the largest class present
+  bool rident = false;  // uniform layout: entry = position >> rcmax (entries with lanes: rmask)
+  u64 rmask = 0;
   auto bperm = [&](u32 e, u32 v) __attribute__((always_inline)) {
     return (u32)__builtin_amdgcn_ds_bpermute((int)(e << 2), (int)v);
   };
-  auto rp_rec = [&](u32 j, u64& s, u64& L, bool& pres) __attribute__((always_inline)) {
-    const u32 e = (j << (6u - rlg)) + ((u32)lane >> rlg);
-    const bool in = e < 2u * nk;
-    const u32 ec = in ? e : 0u;
-    s = ((u64)bperm(ec, (u32)(wS >> 32)) << 32) | (u64)bperm(ec, (u32)wS);
-    L = (u64)bperm(ec, (u32)wL);
-    pres = in && bperm(ec, flive ? 1u : 0u) != 0u;
+  // packed tile j, this lane: entry | line in its group << 8 | class << 16 | present << 24
+  auto rp_map = [&](u32 j) __attribute__((always_inline)) -> u32 {
+    const u32 P = (j << 6) + (u32)lane;
+    if (rident) {  // (wave-uniform) entry e at lanes e 2^rcmax .. (a channel's common case)
+      const u32 e = P >> rcmax;
+      const bool pres = P < vT && ((rmask >> (e & 63u)) & 1ull);
+      return (pres ? e : 0u) | ((P & ((1u << rcmax) - 1u)) << 8) | (rcmax << 16) | ((u32)pres << 24);
+    }
+    u32 c = 5u, b0 = 0u, n0 = 0u;
+#pragma unroll
+    for (int q = 4; q >= 0; q--) {
+      const u32 bq = (u32)__builtin_amdgcn_readlane((int)vbn, q);
+      const bool in = P >= (bq & 0xFFFFu);
+      c = in ? (u32)q : c;
+      b0 = in ? (bq & 0xFFFFu) : b0;
+      n0 = in ? (bq >> 16) : n0;
+    }
+    const u32 off = P - b0;
+    const bool pres = P < vT;
+    const u32 e = bperm(pres ? n0 + (off >> c) : 0u, vS);
+    return e | ((off & ((1u << c) - 1u)) << 8) | (c << 16) | ((u32)pres << 24);
   };
-  auto rp_ext = [&](u64 s, u64 L, bool pres) __attribute__((always_inline)) -> u32 {
-    return pres && L != 0 ? (u32)(L + (s & 15u)) : 0u;
+  auto rp_rec = [&](u32 map, u64& s, u64& L) __attribute__((always_inline)) {
+    const u32 e = map & 0xFFu;
+    s = ((u64)bperm(e, (u32)(wS >> 32)) << 32) | (u64)bperm(e, (u32)wS);
+    L = (u64)bperm(e, (u32)wL);
   };
-  auto process_rp = [&](const u32x4 (&cur)[8], u64 s, u64 L, bool pres, u32 j) __attribute__((always_inline)) {
-    const u32 rli = (u32)lane & (rg - 1u);
+  auto rp_ext = [&](u64 s, u64 L, u32 map) __attribute__((always_inline)) -> u32 {
+    return (map >> 24) ? (u32)(L + (s & 15u)) : 0u;
+  };
+  auto process_rp = [&](const u32x4 (&cur)[8], u64 s, u64 L, u32 map) __attribute__((always_inline)) {
+    const u32 rli = (map >> 8) & 31u, c = (map >> 16) & 7u, g = 1u << c;
     const u32 mis = (u32)s & 15u;
-    const u32 E = rp_ext(s, L, pres);
+    const u32 E = rp_ext(s, L, map);
     u32x4 d[8];
 #pragma unroll
     for (int b = 0; b < 8; b++) d[b] = cur[b];
     const bool head = E != 0u && mis != 0u && rli == 0u;
-    if (__any(head || E < 128u * rg)) {
+    if (__any(head || E < 128u * g)) {
       const int v0 = (int)E - 128 * (int)rli;
       const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
       keep_bytes(d, head ? mis : 0u, hi);
@@ -510,13 +541,29 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     if (seed != 0u && __any(head)) seed = inv_bits(seed, mis, 4);
     const u32 crc = line_crc32_2chain(d, rli == 0u ? seed : 0u, lc0, lc1, z64);
     u32 v = lane_shift(sbase + kLdsOps + 4u * (31u - rli), crc);
-    if (rg >= 2u) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    if (rg >= 4u) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    if (rg >= 8u) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-    if (rg >= 16u) v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false); // row_mirror
-    const u32 code = !pres ? kCodeSkip : L == 0 ? kCodeEmpty : (kSmallMaxExt - E) | (mis << 12);
-    const u32 e = (j << (6u - rlg)) + ((u32)lane >> rlg);
-    if (rli == rg - 1u) lds_st64(sring + 8u * e, (u64)v | ((u64)code << 32));
+    // (each step only when some group needs it: the wave-uniform largest class)
+    if (rcmax >= 1u) {
+      const u32 t = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+      v ^= c >= 1u ? t : 0u;
+    }
+    if (rcmax >= 2u) {
+      const u32 t = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+      v ^= c >= 2u ? t : 0u;
+    }
+    if (rcmax >= 3u) {
+      const u32 t = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+      v ^= c >= 3u ? t : 0u;
+    }
+    if (rcmax >= 4u) {
+      const u32 t = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+      v ^= c >= 4u ? t : 0u;
+    }
+    if (rcmax >= 5u) {
+      const u32 t = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 (rows 1, 3)
+      v ^= c >= 5u ? t : 0u;
+    }
+    const u32 code = (kSmallMaxExt - E) | (mis << 12);
+    if ((map >> 24) && rli == g - 1u) lds_st64(sring + 8u * (map & 0xFFu), (u64)v | ((u64)code << 32));
   };
   // SLOT: lane i's message of the first window (fm): its record's prefix offset, and (after
   // the barrier) the prefix terms, from words loaded in the prologue
@@ -618,7 +665,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   if constexpr (G == 32) {
     record(fmc, wS, wL);
   }
-  if constexpr (SLOT) fpre = a.prefixes[(flive ? fm : 0) * a.pstride];
+  if constexpr (SLOT) {
+    const u64* pp = a.prefixes + (flive ? fm : 0) * a.pstride;
+    fpre = *pp;
+    asm volatile("" ::"v"(pp));
+  }
   fill.store(sbase);
   if constexpr (SLOT && G < 32) {  // Z_C into its LDS slot
     if (threadIdx.x < 128u)
@@ -639,19 +690,63 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   const bool fastu = !SLOT && G < 32 && a.offsets == nullptr && a.ulen != 0 && a.ulen <= (u64)C &&
                      (a.ustride & 15u) == 0 && ((uintptr_t)base & 15u) == 0;
   bool repack = false;
+  u32 rcode0 = 0;  // (REPACK) this lane's entry's code when it has no lanes, written after tile 0's loads
   if constexpr (G == 32) {
-    if (!fast && nk <= kSmallRingTiles) {
+    if (__builtin_expect(!fast && nk <= kSmallRingTiles, 0)) {
+      __builtin_amdgcn_sched_barrier(0);
+      repack = true;
       const u64 Ew = wL + (wS & 15u);
-      const bool fits = !flive || (Ew <= 2048u && (!SLOT || wL <= a.max_len));
-      if (__ballot(!fits) == 0) {
-        repack = true;
-        rg = 1u;
-        rlg = 0u;
-        while (rg < 16u && __ballot(flive && Ew > 128u * rg) != 0) {
-          rg <<= 1;
-          rlg++;
+      const u32 code0 = !flive                          ? kCodeSkip
+                      : SLOT && wL > a.max_len          ? kCodeOversize
+                      : Ew > (u64)kSmallMaxExt          ? kCodeLong
+                      : wL == 0                         ? kCodeEmpty
+                                                        : 0u;
+      const u32 nl = ((u32)Ew + 127u) >> 7;  // (1 .. 32 when code0 == 0)
+      const int cls = code0 ? -1 : (nl <= 1u ? 0 : 32 - __builtin_clz(nl - 1u));
+      // the common case first: every placed entry in one class, the placed entries lanes 0 .. n-1
+      const u64 mpl = __ballot(cls >= 0);
+      const int c0 = mpl ? __builtin_amdgcn_readlane(cls, (int)__builtin_ctzll(mpl)) : 0;
+      rident = (mpl & (mpl + 1ull)) == 0ull && __ballot(cls >= 0 && cls != c0) == 0ull;
+      rmask = mpl;
+      if (rident) {
+        rcmax = (u32)c0;
+        vT = (u32)__builtin_popcountll(mpl) << c0;
+      } else {  // per class: lane positions and sorted indices; each entry's sorted index; inverse
+        u32 base = 0, sorted = 0, ncls = 0;
+        u64 mqs[6];
+#pragma unroll
+        for (int q = 5; q >= 0; q--) {
+          const u64 mq = __ballot(cls == q);
+          mqs[q] = mq;
+          vbn = lane == q ? base | (sorted << 16) : vbn;
+          base += (u32)__builtin_popcountll(mq) << q;
+          sorted += (u32)__builtin_popcountll(mq);
+          if (mq) {
+            rcmax = ncls ? rcmax : (u32)q;
+            ncls++;
+          }
+        }
+        vT = base;
+        // every entry up to the last placed one at 2^rcmax lanes (the uniform layout, no sort)
+        // unless sorting saves tiles: two, or one of four or more (r05bo, r05bp: for a window of
+        // one or two tiles the sort's prologue costs more than the tile it saves)
+        const u32 nu = (u32)(64 - __builtin_clzll(mpl)) << rcmax;
+        const u32 tu = (nu + 63u) >> 6, ts = (vT + 63u) >> 6;
+        if (!(ts < tu && (tu >= 4u || ts + 2u <= tu))) {
+          rident = true;
+          vT = nu;
+        } else {
+          const u64 below = (1ull << lane) - 1ull;
+          u32 pos = sorted + (u32)__builtin_popcountll(~mpl & below);
+#pragma unroll
+          for (int q = 5; q >= 0; q--)
+            if (cls == q) pos = ((u32)__builtin_amdgcn_readlane((int)vbn, q) >> 16) + (u32)__builtin_popcountll(mqs[q] & below);
+          vS = (u32)__builtin_amdgcn_ds_permute((int)(pos << 2), lane);
         }
       }
+      rnt = (vT + 63u) >> 6;
+      rcode0 = cls < 0 ? code0 : 0u;
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   if constexpr (probe) pt[1] = __builtin_amdgcn_s_memrealtime();
@@ -670,14 +765,20 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   }
   u32x4 A[8], B[8];
   u64 sc = sA, Lc = LA;
-  bool pc = false;  // (REPACK: tile 0's slot holds a message)
+  u32 pc = 0;  // (REPACK: packed tile 0's map)
   if (repack) {
-    rp_rec(0u, sc, Lc, pc);
-    load_lines_at(A, sc, rp_ext(sc, Lc, pc), (u32)lane & (rg - 1u));
+    pc = rp_map(0u);
+    rp_rec(pc, sc, Lc);
+    load_lines_at(A, sc, rp_ext(sc, Lc, pc), (pc >> 8) & 31u);
+    if (rcode0) lds_st64(sring + 8u * (u32)lane, (u64)rcode0 << 32);
   } else {
     load_lines(A, sc, ext(0, sc, Lc));  // (FAST: the same addresses as load_at's)
   }
   __syncthreads();
+  // (nothing hoisted above the barrier: hipcc otherwise moved the span hash's first step there,
+  // with a wait for tile 0's lines, so every wave of the workgroup waited for the slowest
+  // wave's tile 0 -- ~1 us per slot-list call, r05bm)
+  __builtin_amdgcn_sched_barrier(0);
   if constexpr (probe) pt[2] = __builtin_amdgcn_s_memrealtime();
   if constexpr (SLOT && SUBSPACE_SMALL_VARIANT != 1) eH = span_hash(pwords, pmeta, eF, eS, ehas);
 
@@ -703,34 +804,32 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       process_fast(A, k);
     }
   } else if (repack) {
-    // the general loop's ping-pong over the wave's rg packed tiles (64 messages)
-    const u32 nt = (2u * nk + (64u >> rlg) - 1u) >> (6u - rlg);
-    const u32 rli = (u32)lane & (rg - 1u);
+    // the general loop's ping-pong over the wave's rnt packed tiles
     u32 j = 0;
-    for (; j + 1 < nt; j += 2) {
+    for (; j + 1 < rnt; j += 2) {
+      const u32 p1 = rp_map(j + 1);
       u64 s1, L1;
-      bool p1;
-      rp_rec(j + 1, s1, L1, p1);
+      rp_rec(p1, s1, L1);
       issue_prio_hi();
       drain_before_issue();  // tile j's lines
-      load_lines_at(B, s1, rp_ext(s1, L1, p1), rli);
+      load_lines_at(B, s1, rp_ext(s1, L1, p1), (p1 >> 8) & 31u);
       issue_prio_lo();
-      process_rp(A, sc, Lc, pc, j);
+      process_rp(A, sc, Lc, pc);
+      const u32 p2 = rp_map(j + 2);
       u64 s2, L2;
-      bool p2;
-      rp_rec(j + 2, s2, L2, p2);
+      rp_rec(p2, s2, L2);
       issue_prio_hi();
       drain_before_issue();
-      load_lines_at(A, s2, rp_ext(s2, L2, p2), rli);
+      load_lines_at(A, s2, rp_ext(s2, L2, p2), (p2 >> 8) & 31u);
       issue_prio_lo();
-      process_rp(B, s1, L1, p1, j + 1);
+      process_rp(B, s1, L1, p1);
       sc = s2;
       Lc = L2;
       pc = p2;
     }
-    if (j < nt) {
+    if (j < rnt) {
       drain_before_issue();
-      process_rp(A, sc, Lc, pc, j);
+      process_rp(A, sc, Lc, pc);
     }
   } else if (fastu) {
     // the general loop's schedule (windows of W tiles) with the FAST loop's loads and compute
@@ -837,7 +936,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u64 xcc = (u64)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
     const u64 v = lane == 0 ? pt[0] : lane == 1 ? pt[1] : lane == 2 ? pt[2] : lane == 3 ? pt[3]
                 : lane == 4 ? pt[4] : lane == 5 ? pt[5] : lane == 6 ? pt[6]
-                : (xcc | ((u64)nk << 32) | ((u64)fast << 48) | ((u64)repack << 49) | ((u64)rg << 52));
+                : (xcc | ((u64)nk << 32) | ((u64)fast << 48) | ((u64)repack << 49) | ((u64)rnt << 52));
     if (lane < kProbeWords) r[lane] = v;
   }
 }

@@ -182,12 +182,12 @@ def test_slot_list_packed(gpu_ctx, oracle, count, max_size, cs, ms, misaligned, 
                                                       (700, 30_001, 3000, 4, 0), (500, 20_001, 0, 8, 16),
                                                       (500, 20_001, 0, 4, 100)])
 def test_slot_list_repack(gpu_ctx, oracle, lib, gen_max, count, spoil, cs, ms):
-    """A channel of 4 KiB slots (max_message_size 4096) carrying shorter messages: each wave
-    whose window holds nothing longer than 2 KiB repacks it (crc_small.hip REPACK, rg lanes per
-    message); `spoil` puts one 3,000-B message in every 50th window, so repacked and general
-    waves share the launch; a metadata span (fused), and metadata over 64 B (the small kernel +
-    the slot-finish kernel). Publish and verify bit-exact against the oracle (payload starts off
-    16-B boundaries included)."""
+    """A channel of 4 KiB slots (max_message_size 4096) carrying shorter messages: every wave
+    that is not FAST packs its window (crc_small.hip REPACK: 2^c lanes per message by size, the
+    uniform or the sorted layout); `spoil` puts one 3,000-B message in every 50th window (one
+    32-lane group among short ones: the sorted layout); a metadata span (fused), and metadata
+    over 64 B (the small kernel + the slot-finish kernel). Publish and verify bit-exact against
+    the oracle (payload starts off 16-B boundaries included)."""
     pre, pay, pay_off, sizes, order, ps = build_slot_list(count, count + gen_max, cs, ms, gen_max, 0.2, 0.0)
     if spoil:  # (payload room: build_slot_list sized it for gen_max, so give the slot a fresh area)
         extra = []
@@ -221,13 +221,12 @@ def test_slot_list_repack(gpu_ctx, oracle, lib, gen_max, count, spoil, cs, ms):
                                                               ms, 4096, gpu.SLOT_VERIFY))
         live = (r[:, 0] > 0) & (((r[:, 7] >> np.uint64(32)) & np.uint64(0xFFFF)) > 0)
         rp = ((r[:, 7] >> np.uint64(49)) & np.uint64(1)) == 1
-        windows_spoiled = len(range(0, count, 64 * 50)) if spoil else 0
-        assert int((live & ~rp).sum()) <= windows_spoiled and int((live & rp).sum()) > 0
+        assert int((live & ~rp).sum()) == 0 and int((live & rp).sum()) > 0
 
 
 def wave_records(ctx, lib, run):
     """The fused slot kernel's per-wave experiment records (crc_small.hip PROBE: lane 7 = nk << 32
-    | fast << 48 | repack << 49 | rg << 52) for one call `run()`."""
+    | fast << 48 | repack << 49 | packed tiles << 52) for one call `run()`."""
     waves = int(lib.subspace_crc_testutil_probe_waves(ctx._h, 1 << 22))
     rb = torch.zeros(waves * 8, dtype=torch.int64, device=DEV)
     assert lib.subspace_crc_testutil_probe(ctx._h, rb.data_ptr()) == 0

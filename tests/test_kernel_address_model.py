@@ -440,13 +440,16 @@ def test_small_kernel_loads_stay_in_messages(seed, count, G, lanes):
 
 def small_kernel_repack_loads(starts, lengths, G):
     """Replays crc32_small_kernel<512, SLOT, false, 32>'s REPACK loop (crc_small.hip): a wave with
-    at most 32 tiles whose window's messages all have E = L + (s & 15) <= 2,048 regroups its 2 nk
-    messages rg to a tile (rg = 1 .. 16 lanes each, the least with 128 rg >= every E): packed
-    tile j's lane i takes window entry e = j (64 / rg) + i / rg (the record lane e loaded: message
-    2 (t0 + (e / 2) nw) + e % 2) and loads line i % rg of it, clamped like load_lines; loads past
-    the wave's entries (the loop's tile nt) read the step table. Yields (message or None, block
-    address or None) for the repacking waves only, ('msg', m) for each non-empty message they
-    compute, then ('waves', number of them)."""
+    at most 32 tiles that is not FAST packs its window's entries (entry e = the record lane e
+    loaded: message 2 (t0 + (e / 2) nw) + e % 2) by size: an entry of E = L + (s & 15) in
+    [1, 4096] has class c (2^c lanes, the least with 128 2^c >= E); empty, absent and longer
+    entries get no lanes. Uniform layout (one class with the placed entries first, or sorting
+    saves too little): entry e at lanes e 2^cmax ..; sorted layout: the entries by class, largest
+    first, each class's in lane order. Packed tile j's lane i (position P = 64 j + i) loads line
+    P - (its group's first position) of its entry, clamped like load_lines; positions past the
+    layout (the loop's tile rnt among them) read the step table. Yields (message or None, block
+    address or None) for the packing waves, ('msg', m) for each message they compute with lanes,
+    then ('waves', number of them)."""
     count = len(starts)
     ntiles = (count + 1) // 2
     nw = 8 * G
@@ -457,40 +460,66 @@ def small_kernel_repack_loads(starts, lengths, G):
             nk = (ntiles - t0 + nw - 1) // nw if t0 < ntiles else 0
             if nk == 0 or nk > 32:
                 continue
-            live = [(2 * (t0 + (e // 2) * nw) + e % 2) for e in range(64)]
-            live = [m if e < 2 * nk and m < count else None for e, m in enumerate(live)]
-            ext = [int(lengths[m]) + (int(starts[m]) & 15) if m is not None else 0 for m in live]
-            if max(ext) > 2048:
-                continue
+            ent = [2 * (t0 + (e // 2) * nw) + e % 2 for e in range(64)]
+            ent = [m if e < 2 * nk and m < count else None for e, m in enumerate(ent)]
+            if all(m is None or (int(lengths[m]) == 4096 and int(starts[m]) % 16 == 0) for m in ent):
+                continue  # FAST
             waves += 1
-            for m in live:
-                if m is not None and lengths[m]:
-                    yield "msg", m
-            rg = 1
-            while rg < 16 and max(ext) > 128 * rg:
-                rg *= 2
-            per = 64 // rg
-            nt = (2 * nk + per - 1) // per
-            for j in list(range(nt)) + [nt]:
+            cls = []
+            for m in ent:
+                E = int(lengths[m]) + (int(starts[m]) & 15) if m is not None else 0
+                if m is None or lengths[m] == 0 or E > 4096:
+                    cls.append(-1)
+                else:
+                    cls.append(max(0, (((E + 127) >> 7) - 1).bit_length()))
+            placed = [e for e in range(64) if cls[e] >= 0]
+            for e in placed:
+                yield "msg", ent[e]
+            if not placed:
+                continue
+            cmax = max(cls[e] for e in placed)
+            lanes = sum(1 << cls[e] for e in placed)
+            nu = (placed[-1] + 1) << cmax
+            tu, ts = (nu + 63) >> 6, (lanes + 63) >> 6
+            prefix_one = placed == list(range(len(placed))) and len({cls[e] for e in placed}) == 1
+            owner = {}  # position -> (entry, line in its group)
+            if prefix_one or not (ts < tu and (tu >= 4 or ts + 2 <= tu)):
+                for e in placed:
+                    for li in range(1 << cmax):
+                        owner[(e << cmax) + li] = (e, li)
+                total = nu if not prefix_one else len(placed) << cmax
+            else:
+                pos = 0
+                for c in range(5, -1, -1):
+                    for e in placed:
+                        if cls[e] == c:
+                            assert pos % (1 << c) == 0 and pos // 64 == (pos + (1 << c) - 1) // 64
+                            for li in range(1 << c):
+                                owner[pos + li] = (e, li)
+                            pos += 1 << c
+                total = pos
+            rnt = (total + 63) >> 6
+            for j in list(range(rnt)) + [rnt]:
                 for i in range(64):
-                    e = j * per + i // rg
-                    m = live[e] if e < 64 else None
-                    if m is None or lengths[m] == 0:
+                    if (64 * j + i) not in owner:
                         yield None, None
                         continue
-                    s, E = int(starts[m]), ext[e]
-                    lastb = (E - 1) & ~15
+                    e, li = owner[64 * j + i]
+                    m = ent[e]
+                    s = int(starts[m])
+                    lastb = (int(lengths[m]) + (s & 15) - 1) & ~15
                     for blk in range(8):
-                        yield m, (s & ~15) + min(128 * (i % rg) + 16 * blk, lastb)
+                        yield m, (s & ~15) + min(128 * li + 16 * blk, lastb)
     yield "waves", waves
 
 
 @pytest.mark.parametrize("seed,count,G,top", [(20, 1, 1, 64), (21, 65, 1, 300), (22, 999, 63, 2048),
-                                              (23, 4001, 31, 1000), (24, 20001, 256, 129)])
+                                              (23, 4001, 31, 1000), (24, 20001, 256, 129), (25, 3001, 7, 4096),
+                                              (26, 999, 5, 5000), (27, 2001, 40, 256)])
 def test_small_kernel_repack_loads_stay_in_messages(seed, count, G, top):
     """REPACK's loads obey the same rule as the tile loop's: every block holds a byte of its own
-    message and every byte of every message it computes is loaded, for each lane group size the
-    window's largest message selects."""
+    message and every byte of every message it computes with lanes is loaded, in the uniform and
+    the sorted layout (messages up to `top` bytes: past 4 KiB they take no lanes)."""
     rng = np.random.default_rng(seed)
     lengths = rng.integers(0, top + 1, count)
     starts = np.cumsum(np.concatenate([[0], lengths[:-1] + rng.integers(0, 40, count - 1)])) + 3
