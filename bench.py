@@ -100,7 +100,7 @@ def parse():
                          "E: 8 Mi x 4 KiB sharded round-robin over the GPUs (strong scaling) + RCCL gather")
     ap.add_argument("--configs", default=None,
                     help="secondary configs timed after the headline at N = 1 (comma list of C, Cu, D, Du, S, "
-                         "Usmall, S_short; default C,D,Du,S,Usmall,S_short with workload B, none otherwise; "
+                         "Usmall, S_short, S_mixed; default C,D,Du,S,Usmall,S_short,S_mixed with workload B, none otherwise; "
                          "'none' disables)")
     ap.add_argument("--config-iters", type=int, default=20)
     ap.add_argument("--no-solo", action="store_true", help="N > 1: skip rank 0's single-GPU reference leg")
@@ -647,7 +647,8 @@ def config_traffic(name):
     try:
         tj = json.loads(f.read_text())
         c = tj["configs"][name]
-        return c["hbm_bytes_per_call"], (f"profiles/traffic_configs.json ({tj.get('source', '?')}; PMC FETCH_SIZE x2 + "
+        return c["hbm_bytes_per_call"], (f"profiles/traffic_configs.json ({c.get('source', tj.get('source', '?'))}; "
+                                         f"PMC FETCH_SIZE x2 + "
                                          f"WRITE_SIZE per call, ratio {c['ratio']} of the algorithmic bytes; not "
                                          f"measured in this run)")
     except (OSError, ValueError, KeyError):
@@ -717,6 +718,8 @@ def secondary_configs(ctx, dev, names, iters) -> dict:
             res[name] = small_uniform_config(ctx, dev)
         elif name == "S_short":
             res[name] = short_slots_config(ctx, dev)
+        elif name == "S_mixed":
+            res[name] = short_slots_config(ctx, dev, mixed=True)
 
     # No torch.cuda.empty_cache() between configs: VRAM given back to the driver is wiped in the
     # background for seconds (every HBM-bound kernel ~2-4 % slower meanwhile: config S after
@@ -763,23 +766,24 @@ def small_uniform_config(ctx, dev) -> dict:
     return line
 
 
-def short_slots_config(ctx, dev) -> dict:
+def short_slots_config(ctx, dev, mixed=False) -> dict:
     """Informational (no BASELINE config): a channel of 65,536 4 KiB slots (stride 4,160)
-    carrying 256-B messages, published by the fused strided kernel, then drained as shuffled
-    device slot lists (max_message_size 4096) through subspace_crc32_slots -- the small kernel's
-    waves repack their windows two lanes per message (crc_small.hip REPACK); 4 rotated copies.
+    carrying 256-B messages (S_short) or messages of 1 .. 4,096 B, uniformly random (S_mixed),
+    published by the fused strided kernel, then drained as shuffled device slot lists
+    (max_message_size 4096) through subspace_crc32_slots -- the small kernel's waves pack their
+    windows by message size (crc_small.hip REPACK: 2^c lanes per message); 4 rotated copies.
     Bytes: span 0 + payload per slot. Check: every slot verifies (publish and verify are
     different kernels)."""
     import torch
     from subspace_amd import gpu, slots
     n, area, L, cs, ms_, nbuf = MSGS, MSG_BYTES, 256, 4, 0, 4
     ps, stride = slots.compute_prefix_size(cs, ms_), slots.slot_stride(area, cs, ms_)
-    rng = np.random.default_rng(0x5EED0257)
+    rng = np.random.default_rng(0x5EED0258 if mixed else 0x5EED0257)
+    sizes = rng.integers(1, area + 1, n).astype(np.uint64) if mixed else np.full(n, L, dtype=np.uint64)
     host = rng.integers(0, 256, stride * n, dtype=np.uint8)
-    host.reshape(n, stride)[:, :ps] = slots.make_prefixes(n, np.full(n, L, dtype=np.uint64), checksum_size=cs,
-                                                          metadata_size=ms_, seed=7)
+    host.reshape(n, stride)[:, :ps] = slots.make_prefixes(n, sizes, checksum_size=cs, metadata_size=ms_, seed=7)
     bufs = [torch.from_numpy(host).to(dev) for _ in range(nbuf)]
-    d_sizes = torch.full((n,), L, dtype=torch.int64, device=dev)
+    d_sizes = torch.from_numpy(sizes.view(np.int64)).to(dev)
     for b in bufs:
         ctx.crc32_slots_strided(b, stride, n, sizes=d_sizes, checksum_size=cs, metadata_size=ms_,
                                 mode=gpu.SLOT_CALCULATE)
@@ -788,7 +792,7 @@ def short_slots_config(ctx, dev) -> dict:
     for b in bufs:
         b0 = np.uint64(b.data_ptr())
         r = np.stack([b0 + order * np.uint64(stride), b0 + order * np.uint64(stride) + np.uint64(ps),
-                      np.full(n, L, dtype=np.uint64)], axis=1)
+                      sizes[order.astype(np.int64)]], axis=1)
         recs.append(torch.from_numpy(np.ascontiguousarray(r).view(np.int64)).to(dev))
     status = torch.empty(n, dtype=torch.int32, device=dev)
     errs = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -801,10 +805,12 @@ def short_slots_config(ctx, dev) -> dict:
     ms = time_calls(call, 400)
     torch.cuda.synchronize()
     ok = int(errs.item()) == 0 and bool((status == 0).all().item())
-    line = config_line(n * (L + 44), ms, ok, "subspace_crc32_slots: crc32_small_kernel<512, true, false, 32> "
-                       "(REPACK: two lanes per message)", name="S_short", extra={
-                           "workload": "S_short (informational): 65,536 slots of 4 KiB (stride 4,160) carrying 256-B "
-                                       "messages, shuffled device slot lists, verify, 4 copies rotated",
+    name = "S_mixed" if mixed else "S_short"
+    what = "messages of 1 .. 4,096 B (uniformly random)" if mixed else "256-B messages"
+    line = config_line(int(sizes.sum()) + 44 * n, ms, ok, "subspace_crc32_slots: crc32_small_kernel<512, true, "
+                       "false, 32> (REPACK: 2^c lanes per message by size)", name=name, extra={
+                           "workload": f"{name} (informational): 65,536 slots of 4 KiB (stride 4,160) carrying {what}, "
+                                       "shuffled device slot lists, verify, 4 copies rotated",
                            "slots_per_s": round(n / (ms * 1e-3), 1),
                            "check": "every slot verifies (published by the fused strided kernel)"})
     del bufs, recs, status
@@ -1208,7 +1214,7 @@ def main():
             return {"error": f"{type(e).__name__}: {e}"[:300]}
 
     configs = None
-    cfg_names = args.configs if args.configs is not None else ("C,D,Du,S,Usmall,S_short" if args.workload == "B"
+    cfg_names = args.configs if args.configs is not None else ("C,D,Du,S,Usmall,S_short,S_mixed" if args.workload == "B"
                                                                else "none")
     if world == 1 and cfg_names != "none":
         configs = optional(lambda: secondary_configs(ctx, dev, [c for c in cfg_names.split(",") if c],

@@ -7,7 +7,7 @@ calls made and writes profiles/traffic_configs.json, which bench.py reads.
 
   python tools/pmc_configs.py <config> [calls]
   config: C, Cu, D, Du, S_publish, S_verify, S_meta_publish, S_meta_verify, S_list_publish,
-          S_list_verify, Usmall, S_short (bench.py's secondary configs, the same shapes and
+          S_list_verify, Usmall, S_short, S_mixed (bench.py's secondary configs, the same shapes and
           synthetic data)
 
 Prints one JSON line: the config, the calls made and the algorithmic bytes per call (bench.py's
@@ -66,20 +66,21 @@ def main():
             ctx.crc32_uniform(bufs[i[0] % 4], L, L, n, out)
             i[0] += 1
         nbytes = n * L
-    elif name == "S_short":  # bench.py short_slots_config: 256-B messages in 4 KiB slots, shuffled list
+    elif name in ("S_short", "S_mixed"):  # bench.py short_slots_config: 256-B / 1..4096-B messages in 4 KiB slots
         n, area, L, cs = 65536, 4096, 256, 4
         ps, stride = slots.compute_prefix_size(cs, 0), slots.slot_stride(area, cs, 0)
-        rng = np.random.default_rng(0x5EED0257)
+        mixed = name == "S_mixed"
+        rng = np.random.default_rng(0x5EED0258 if mixed else 0x5EED0257)
+        sizes = rng.integers(1, area + 1, n).astype(np.uint64) if mixed else np.full(n, L, dtype=np.uint64)
         host = rng.integers(0, 256, stride * n, dtype=np.uint8)
-        host.reshape(n, stride)[:, :ps] = slots.make_prefixes(n, np.full(n, L, dtype=np.uint64), checksum_size=cs,
-                                                              metadata_size=0, seed=7)
+        host.reshape(n, stride)[:, :ps] = slots.make_prefixes(n, sizes, checksum_size=cs, metadata_size=0, seed=7)
         bufs = [torch.from_numpy(host).to(dev) for _ in range(4)]
         order = rng.permutation(n).astype(np.uint64)
         recs = []
         for b in bufs:
             b0 = np.uint64(b.data_ptr())
             r = np.stack([b0 + order * np.uint64(stride), b0 + order * np.uint64(stride) + np.uint64(ps),
-                          np.full(n, L, dtype=np.uint64)], axis=1)
+                          sizes[order.astype(np.int64)]], axis=1)
             recs.append(torch.from_numpy(np.ascontiguousarray(r).view(np.int64)).to(dev))
         status = torch.empty(n, dtype=torch.int32, device=dev)
         errs = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -89,7 +90,7 @@ def main():
             ctx.crc32_slots(recs[i[0] % 4], max_message_size=area, checksum_size=cs, metadata_size=0,
                             mode=gpu.SLOT_VERIFY, status=status, error_count=errs)
             i[0] += 1
-        nbytes = n * (L + 44)
+        nbytes = int(sizes.sum()) + 44 * n
     else:  # config S's slots (bench.py slot_configs): 65,536 x 4 KiB payloads, 4 rotated copies
         n, size, cs = 65536, 4096, 4
         ms_ = 16 if name.startswith("S_meta") else 0
