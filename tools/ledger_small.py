@@ -25,6 +25,11 @@ subspace_crc32_slots (the small-message kernel, crc_small.hip) or read by the pr
               mismatch count only)
   strided  -- the fused uniform slot kernel (subspace_crc32_slots_strided), verify, rotated:
               config S's S_verify, the same slots read in channel order
+  mixed    -- the shuffled lists with message sizes 1 .. 4,096 B (uniformly random; bench.py's
+              S_mixed shape: the repack by size), verify (mismatches: the same reads);
+              mixed_alias its compute-only twin (every record at slot 0 of copy 0, the same
+              sizes); mixed_probe0 slot_list_read_kernel<0> over the mixed lists (clamped lines
+              of each message's length: the access shape's read ceiling, no CRC)
 
   python tools/ledger_small.py <mode>[,<mode>...] [launches] [settle] [rounds]
 
@@ -66,13 +71,16 @@ def main():
     errs = torch.zeros(1, dtype=torch.int32, device=dev)
     perm = rng.permutation(N).astype(np.uint64)
 
-    def recs(buf, order):
+    def recs(buf, order, sizes=None):
         b0 = np.uint64(buf.data_ptr())
         r = np.stack([b0 + order * np.uint64(stride), b0 + order * np.uint64(stride) + np.uint64(ps),
-                      np.full(len(order), SIZE, dtype=np.uint64)], axis=1)
+                      np.full(len(order), SIZE, dtype=np.uint64) if sizes is None else sizes], axis=1)
         return torch.from_numpy(np.ascontiguousarray(r).view(np.int64)).to(dev)
 
     shuffled = [recs(b, perm) for b in bufs]
+    msz = np.random.default_rng(0x5EED0258).integers(1, SIZE + 1, N).astype(np.uint64)
+    mixed = [recs(b, perm, msz) for b in bufs] if any(m.startswith("mixed") for m in modes) else []
+    mixed_alias = recs(bufs[0], np.zeros(N, dtype=np.uint64), msz) if "mixed_alias" in modes else None
     ordered = [recs(b, np.arange(N, dtype=np.uint64)) for b in bufs]
     alias = recs(bufs[0], np.zeros(N, dtype=np.uint64))
     sink = torch.empty(2048 * 512, dtype=torch.int32, device=dev)
@@ -111,6 +119,9 @@ def main():
         "probe5": lambda i: probe(shuffled[i % NB], 5),
         "probe5o": lambda i: probe(ordered[i % NB], 5),
         "probe6": lambda i: probe(ordered[i % NB], 6),
+        "mixed": lambda i: slot_list(mixed[i % NB]),
+        "mixed_alias": lambda i: slot_list(mixed_alias),
+        "mixed_probe0": lambda i: probe(mixed[i % NB], 0),
         "strided": lambda i: ctx.crc32_slots_strided(bufs[i % NB], stride, N, message_size=SIZE, checksum_size=CS,
                                                      metadata_size=MS, mode=gpu.SLOT_VERIFY, status=status,
                                                      error_count=errs),
@@ -128,7 +139,7 @@ def main():
             b.record()
             torch.cuda.synchronize()
             us = a.elapsed_time(b) * 1e3 / launches
-            nbytes = N * (SIZE + 44)  # checksummed bytes (bench.py's S_list)
+            nbytes = (int(msz.sum()) + 44 * N) if mode.startswith("mixed") else N * (SIZE + 44)  # checksummed bytes
             line = {"mode": mode, "round": r, "launches": launches, "settle": settle, "us_per_launch": round(us, 3),
                     "pct_of_hbm_peak": round(100 * nbytes / us / 1e3 / 8000.0, 2)}
             if check and mode in ("list", "list1", "ordered", "alias", "strided", "list_ns", "ordered_ns", "strided_ns"):
