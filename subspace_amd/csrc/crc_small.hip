@@ -25,6 +25,9 @@
 //    kernel with the flush moved out of the loop -- 0 SGPR spills, no full drain in the loop
 //    -- measured 2.3-3.4 us slower per 65,536-slot list, with or without loop padding:
 //    profiles/r04/README.md.)
+//  * G = 32: a wave whose window holds only whole aligned 4 KiB messages runs the FAST loop
+//    (the uniform kernel's loads); any other wave packs its window by message size, 2^c lanes
+//    per message (REPACK, below), so a short message takes a few lanes rather than a half-tile.
 //  * Every line load stays inside its message: block b of lane l is read from s0 +
 //    min(128 l + 16 b, last block), so the lanes past the end re-read the last block (one
 //    cache line) instead of branching around loads, and a half with nothing to read (no
