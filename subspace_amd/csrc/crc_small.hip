@@ -426,7 +426,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32 code = (k < nk && msg_of(k) < count) ? 0u : kCodeSkip;
     if (l == 31u) lds_st64(sring + 8u * (2u * (k & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
   };
-  // UNIFORM FAST (G < 32, no slots): a uniform batch of messages of L <= C bytes on 16-B
+  // UNIFORM FAST (no slots; G = 32 too since r05ca: 2-4 KiB messages 14-20 % faster than the
+  // repack loop): a uniform batch of messages of L <= C bytes on 16-B
   // boundaries -- the tile's address from m * stride, one address and 8 immediate-offset loads
   // (reading C bytes per message: past L they are the next messages' bytes, masked), one padding
   // p = C - L for every message, no codes. A tile holding a message whose C bytes would reach
@@ -700,12 +701,12 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // r05z)
   const bool conf = !flive || (wL == (u64)kSmallMaxExt && (wS & 15u) == 0 && (!SLOT || wL <= a.max_len));
   const bool fast = G == 32 && nk <= kSmallRingTiles && __ballot(!conf) == 0;
-  const bool fastu = !SLOT && G < 32 && a.offsets == nullptr && a.ulen != 0 && a.ulen <= (u64)C &&
+  const bool fastu = !SLOT && a.offsets == nullptr && a.ulen != 0 && a.ulen <= (u64)C &&
                      (a.ustride & 15u) == 0 && ((uintptr_t)base & 15u) == 0;
   bool repack = false;
   u32 rcode0 = 0;  // (REPACK) this lane's entry's code when it has no lanes, written after tile 0's loads
   if constexpr (G == 32) {
-    if (__builtin_expect(!fast && nk <= kSmallRingTiles, 0)) {
+    if (__builtin_expect(!fast && !fastu && nk <= kSmallRingTiles, 0)) {
       __builtin_amdgcn_sched_barrier(0);
       repack = true;
       const u64 Ew = wL + (wS & 15u);
