@@ -575,7 +575,9 @@ def uniform_fast_reads(count, L, stride, G, grid):
 
 @pytest.mark.parametrize("count,L,stride,G,grid", [(1000, 1000, 1008, 8, 4), (5000, 16, 16, 1, 8), (301, 129, 144, 2, 3),
                                                    (70, 100, 112, 1, 2), (4097, 2000, 2000, 16, 16),
-                                                   (63, 512, 512, 4, 1), (2, 17, 32, 1, 1)])
+                                                   (63, 512, 512, 4, 1), (2, 17, 32, 1, 1),
+                                                   (3001, 3000, 3008, 32, 12), (65, 4000, 4000, 32, 1),
+                                                   (2, 2100, 2112, 32, 1)])
 def test_uniform_fast_reads_stay_in_the_batch(count, L, stride, G, grid):
     """The packed uniform FAST loop reads past a message's L bytes (into the next messages) but
     never past the batch: every range it reads lies in [0, end) with end the batch's last byte
