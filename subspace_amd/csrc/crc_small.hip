@@ -707,6 +707,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   u32 rcode0 = 0;  // (REPACK) this lane's entry's code when it has no lanes, written after tile 0's loads
   if constexpr (G == 32) {
     if (__builtin_expect(!fast && !fastu && nk <= kSmallRingTiles, 0)) {
+      // (fenced off from the FAST path's prologue; measured neutral, r05bm, kept as validated)
       __builtin_amdgcn_sched_barrier(0);
       repack = true;
       const u64 Ew = wL + (wS & 15u);
