@@ -4,7 +4,7 @@ of n messages of L bytes (stride = L rounded up to 16 B) through subspace_crc32_
 event-timed over `launches` back-to-back calls after `settle` untimed ones, rotated over buffers
 large enough to leave the 256 MB MALL behind.
 
-  python tools/small_sizes.py [L,L,...] [launches] [settle] [uniform|slots|slots_ordered|slots4k|slots4k_rand|ragged_rand]
+  python tools/small_sizes.py [L,L,...] [launches] [settle] [uniform|uniform_packed|slots|slots_ordered|slots4k|slots4k_rand|ragged_rand]
 
 slots: a channel of L-byte slots (MessagePrefix 64 B + payload, the reference's stride) per
 256 MiB, published once, then verified as shuffled device slot lists (subspace_crc32_slots,
@@ -39,7 +39,7 @@ def main():
         return slot_lists(ctx, dev, sizes, launches, settle, ordered=mode == "slots_ordered",
                           slot_size=4096 if mode.startswith("slots4k") else 0, rand=mode == "slots4k_rand")
     for L in sizes:
-        stride = (L + 15) & ~15
+        stride = L if mode == "uniform_packed" else (L + 15) & ~15
         n = (256 << 20) // stride  # 256 MiB of messages per batch
         nb = 4
         bufs = [torch.empty(n * stride, dtype=torch.uint8, device=dev) for _ in range(nb)]
