@@ -8,12 +8,18 @@ CSRC := subspace_amd/csrc
 LIB := subspace_amd/libsubspace_crc.so
 OBJDIR := build/obj
 
-HIP_SRCS := $(CSRC)/crc_uniform.hip $(CSRC)/crc_small.hip $(CSRC)/crc_ragged.hip $(CSRC)/crc_long.hip $(CSRC)/crc_combine.hip $(CSRC)/crc_slots.hip $(CSRC)/capi.hip $(CSRC)/testutil.hip
+HIP_SRCS := $(CSRC)/crc_uniform.hip $(CSRC)/crc_small.hip $(CSRC)/crc_ragged.hip $(CSRC)/crc_long.hip $(CSRC)/crc_combine.hip $(CSRC)/crc_slots.hip $(CSRC)/capi.hip
 CPP_SRCS := $(CSRC)/host_crc.cpp $(CSRC)/split_alloc.cpp
-HDRS := $(CSRC)/crc_device.h $(CSRC)/crc_math.h include/subspace_crc.h
+HDRS := $(CSRC)/crc_device.h $(CSRC)/crc_math.h $(CSRC)/ctx.h include/subspace_crc.h
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))
+# the product library exports exactly the public header's functions (exports.map)
+EXPORTS := $(CSRC)/exports.map
+# tests / bench / tools only: development knobs, probes, synthetic-payload generators and read
+# probes (devtools.hip, testutil.hip); never linked by a client, not needed by the product
+DEVLIB := subspace_amd/libsubspace_crc_dev.so
+DEV_OBJS := $(OBJDIR)/devtools.o $(OBJDIR)/testutil.o
 
-all: $(LIB) oracle tools/config_a tools/drain_demo tools/batch_gates
+all: $(LIB) $(DEVLIB) oracle tools/config_a tools/drain_demo tools/batch_gates
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -23,8 +29,19 @@ $(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	g++ -O3 -std=c++17 -fPIC -Wall -c $< -o $@
 
-$(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+$(LIB): $(OBJS) $(EXPORTS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,--version-script=$(EXPORTS) -o $@ $(OBJS)
+
+$(OBJDIR)/devtools.o: $(CSRC)/devtools.hip $(CSRC)/crc_small.hip $(CSRC)/crc_uniform.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/testutil.o: $(CSRC)/testutil.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(DEVLIB): $(DEV_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(DEV_OBJS)
 
 oracle:
 	$(MAKE) -C oracle
@@ -74,8 +91,8 @@ $(ASAN_DIR)/capi.o: $(CSRC)/capi.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -g -Xarch_host -fsanitize=address,undefined -Xarch_host -fno-sanitize-recover=all \
 	    -Xarch_host -fno-omit-frame-pointer -c $< -o $@
 
-$(ASAN_LIB): $(ASAN_HOST_OBJS) $(ASAN_HIP_OBJS)
-	$(ASAN_CXX) -shared -fPIC $(ASAN_FLAGS) -o $@ $(ASAN_HOST_OBJS) $(ASAN_HIP_OBJS) -L/opt/rocm/lib -lamdhip64 \
+$(ASAN_LIB): $(ASAN_HOST_OBJS) $(ASAN_HIP_OBJS) $(EXPORTS)
+	$(ASAN_CXX) -shared -fPIC $(ASAN_FLAGS) -Wl,--version-script=$(EXPORTS) -o $@ $(ASAN_HOST_OBJS) $(ASAN_HIP_OBJS) -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,/opt/rocm/lib
 
 $(ASAN_DIR)/config_a: tools/config_a.cpp include/subspace/checksum.h $(ASAN_LIB)
@@ -130,7 +147,7 @@ tsan-test: tsan
 	TSAN_OPTIONS=halt_on_error=1:exitcode=66 $(TSAN_DIR)/tsan_stress 8 200
 
 clean:
-	rm -rf build $(LIB) tools/config_a tools/drain_demo tools/batch_gates
+	rm -rf build $(LIB) $(DEVLIB) tools/config_a tools/drain_demo tools/batch_gates
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle test-cpu clean asan asan-test tsan tsan-test

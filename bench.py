@@ -100,7 +100,7 @@ def parse():
                          "E: 8 Mi x 4 KiB sharded round-robin over the GPUs (strong scaling) + RCCL gather")
     ap.add_argument("--configs", default=None,
                     help="secondary configs timed after the headline at N = 1 (comma list of C, Cu, D, Du, S, "
-                         "Usmall, S_short, S_mixed; default C,D,Du,S,Usmall,S_short,S_mixed with workload B, none otherwise; "
+                         "Usmall, S_short, S_mixed; default C,Cu,D,Du,S,Usmall,S_short,S_mixed with workload B, none otherwise; "
                          "'none' disables)")
     ap.add_argument("--config-iters", type=int, default=20)
     ap.add_argument("--no-solo", action="store_true", help="N > 1: skip rank 0's single-GPU reference leg")
@@ -1111,7 +1111,12 @@ def main():
     if world != args.gpus:
         die(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch with --nproc-per-node equal to --gpus")
     if args.print_rank_env:  # tests: what a rank runs with, before anything else happens
-        print(json.dumps({"rank": rank, "env": {k: os.environ.get(k) for k in RANK_ENV_REPORTED}}), flush=True)
+        # one write(2) of the whole line: ranks share the parent's stdout pipe, and print() under
+        # PYTHONUNBUFFERED issues the record and its newline as two writes, which two ranks can
+        # interleave into one line (the round-5 CPU-gate flake: JSONDecodeError "Extra data")
+        sys.stdout.flush()
+        rec = json.dumps({"rank": rank, "env": {k: os.environ.get(k) for k in RANK_ENV_REPORTED}}) + "\n"
+        os.write(sys.stdout.fileno(), rec.encode())
         sys.exit(0)
     if args.workload is None:
         args.workload = "B" if world == 1 else "E"
@@ -1214,7 +1219,7 @@ def main():
             return {"error": f"{type(e).__name__}: {e}"[:300]}
 
     configs = None
-    cfg_names = args.configs if args.configs is not None else ("C,D,Du,S,Usmall,S_short,S_mixed" if args.workload == "B"
+    cfg_names = args.configs if args.configs is not None else ("C,Cu,D,Du,S,Usmall,S_short,S_mixed" if args.workload == "B"
                                                                else "none")
     if world == 1 and cfg_names != "none":
         configs = optional(lambda: secondary_configs(ctx, dev, [c for c in cfg_names.split(",") if c],

@@ -13,8 +13,14 @@ from pathlib import Path
 
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = _HERE / "libsubspace_crc.so"
-if os.environ.get("SUBSPACE_CRC_PROBE_LIB"):  # investigation builds (tools/ubench/build_probes.sh)
+if os.environ.get("SUBSPACE_CRC_PROBE_LIB"):  # investigation builds (tools/ab_lib.sh)
     LIB_PATH = Path(os.environ["SUBSPACE_CRC_PROBE_LIB"])
+# Development library (tests, bench.py, tools only; devtools.hip + testutil.hip): path knobs,
+# fault injection, PROBE hooks, synthetic-payload generators, read-ceiling probes. It works on
+# contexts the product library creates (ctx.h); the product library never loads it.
+DEV_LIB_PATH = _HERE / "libsubspace_crc_dev.so"
+if os.environ.get("SUBSPACE_CRC_PROBE_DEV_LIB"):  # an A/B build's matching dev library
+    DEV_LIB_PATH = Path(os.environ["SUBSPACE_CRC_PROBE_DEV_LIB"])
 
 # Every symbol include/subspace_crc.h declares (tests check they are all exported).
 EXPORTED_SYMBOLS = (
@@ -43,6 +49,7 @@ EXPORTED_SYMBOLS = (
 )
 
 _lib = None
+_dev = None
 
 
 class LibraryNotBuilt(RuntimeError):
@@ -94,6 +101,20 @@ def load() -> ctypes.CDLL:
     lib.subspace_crc_host_register.argtypes = [vp, u64]
     lib.subspace_crc_host_unregister.restype = i32
     lib.subspace_crc_host_unregister.argtypes = [vp]
+    _lib = lib
+    return lib
+
+
+def load_dev() -> ctypes.CDLL:
+    """Load (once) the development library (tests / bench / tools: never the product path)."""
+    global _dev
+    if _dev is not None:
+        return _dev
+    load()  # the product library first: the dev library acts on its contexts
+    if not DEV_LIB_PATH.exists():
+        raise LibraryNotBuilt(f"{DEV_LIB_PATH} not found: run `make` (or __graft_entry__.build()) first")
+    lib = ctypes.CDLL(os.fspath(DEV_LIB_PATH), mode=ctypes.RTLD_LOCAL)
+    u32, u64, vp, i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int
     lib.subspace_crc_testutil_fill_uniform.restype = i32
     lib.subspace_crc_testutil_fill_uniform.argtypes = [vp, u64, u64, u64, u64, u64, u64, vp]
     lib.subspace_crc_testutil_fill_ragged.restype = i32
@@ -112,10 +133,13 @@ def load() -> ctypes.CDLL:
     lib.subspace_crc_testutil_probe.argtypes = [vp, vp]
     lib.subspace_crc_testutil_probe_waves.restype = u64
     lib.subspace_crc_testutil_probe_waves.argtypes = [vp, u64]
-    if hasattr(lib, "subspace_crc_testutil_slot_list_read"):  # (absent from older A/B builds)
-        lib.subspace_crc_testutil_slot_list_read.restype = i32
-        lib.subspace_crc_testutil_slot_list_read.argtypes = [vp, u64, u32, u64, u32, vp, u64, vp]
-    _lib = lib
+    lib.subspace_crc_testutil_slot_list_read.restype = i32
+    lib.subspace_crc_testutil_slot_list_read.argtypes = [vp, u64, u32, u64, u32, vp, u64, vp]
+    lib.subspace_crc_testutil_fault_words.restype = i32
+    lib.subspace_crc_testutil_fault_words.argtypes = [vp, vp, vp]
+    lib.subspace_crc_testutil_call_gen.restype = u32
+    lib.subspace_crc_testutil_call_gen.argtypes = [vp]
+    _dev = lib
     return lib
 
 

@@ -13,6 +13,7 @@
 #include "../../include/subspace_crc.h"
 #include "crc_device.h"
 #include "crc_math.h"
+#include "ctx.h"
 
 namespace subspace_amd {
 
@@ -107,92 +108,6 @@ int set_error(int code, const char* fmt, ...) {
 }
 }  // namespace subspace_amd
 
-struct subspace_crc_ctx {
-  int device = 0;
-  uint32_t poly = kPoly;  // reflected CRC polynomial of every table and operator below
-  int num_cus = 256;
-  u32* d_tab = nullptr;  // 4 x 256 slice tables
-  u32* d_rops = nullptr;  // ragged kernel: line-shift operators, Z_4096, tile shifts, padding inverses
-  u32* d_pow2 = nullptr;  // Z_{2^k}, k = 0..63, nibble operators (slot checksums)
-  u32* d_laneops = nullptr;  // uniform kernel: Z_{128*s}, s = 0..31, as [nibble][value][s]; Z_4096
-  Tables host_tab;
-  Mat32 zinv1;  // Z_1^{-1}: the ragged kernel's head seeds Z_r^{-1}(init)
-  // ragged workspace
-  u64* d_tbase = nullptr;    // count + 1: tiles before each message (exclusive scan)
-  u64 ws_messages = 0;
-  uint8_t* d_desc = nullptr;
-  u32* d_tilecrc = nullptr;  // per-tile values, wave-major (desc_capacity + one tile per wave)
-  u32* d_local = nullptr;    // per-segment inclusive XOR prefixes of the values, tile order
-  u32* d_segx = nullptr;     // per-segment XORs, then their exclusive XOR prefixes
-  u64 desc_capacity = 0;
-  // look-back scan state: word 0 = the two workgroup tickets (u32 each), then the
-  // tile-count scan's status words (scan_a_words), then the segment scan's (scan_b_words).
-  // Zeroed at allocation; each call's later kernels zero what its scans used
-  // (crc_device.h reset_scan_state). scan_dirty: a call failed between a scan and its reset.
-  u64* d_scan_state = nullptr;
-  u64 scan_a_words = 0, scan_b_words = 0;
-  bool scan_dirty = false;
-  u64 mem_tiles = 0;  // device memory / 8 KiB: bounds the descriptor workspace
-  u32* d_overflow = nullptr;  // [0] overflow, [1] wide batch, [2] a tile past the fused kernel's 8-B range
-  bool fused_prep = true;     // knob "fused_prep": known-arena batches take crc32_ragged_count_desc_kernel
-  int uniform_wg = 512;    // workgroup size of the uniform kernel (256/512/640/768/1024)
-  int uniform_blocks = 0;  // 0 = one workgroup per CU
-  int uniform_order = 0;   // tile order: 0 XCD-spread sweep, 1 per-workgroup region, 2 plain sweep, 3 XCD-grouped
-  bool long_path = true;   // whole-8 KiB-piece uniform batches take crc32_long_kernel
-  u32* zero_word = nullptr;  // zeroed by the next uniform or ragged launch (slot mismatch count)
-  u64* d_uoff = nullptr;  // offsets/lengths materialised for non-4K uniform batches
-  u64* d_ulen = nullptr;
-  u64 u_capacity = 0;
-  // host-slot pipeline (subspace_crc32_host_slots): one compute stream (the kernels share
-  // the context's workspaces), a copy stream and staging per in-flight chunk
-  hipStream_t hcompute = nullptr;
-  struct HostStage {
-    hipStream_t stream = nullptr;  // H2D copies of this stage's chunks
-    hipEvent_t copied = nullptr;   // the chunk is on the device
-    hipEvent_t done = nullptr;     // its results are on the host
-    uint8_t* dbuf = nullptr;   // device copy of a chunk of slots
-    u64* dsizes = nullptr;     // its message sizes (optional)
-    u32* dres = nullptr;       // per-slot results: stored checksum (CALCULATE) / status (VERIFY)
-    u32* derr = nullptr;       // mismatch count of the chunk
-    u32* hres = nullptr;       // pinned host copies of dres / derr
-    u32* herr = nullptr;
-  } hstage[2];
-  u64 h_bytes = 0, h_slots = 0;  // staging capacities
-  // host slot lists (subspace_crc32_host_slot_list): translated records and statuses
-  subspace_crc_slot* l_hrec = nullptr;
-  subspace_crc_slot* l_drec = nullptr;
-  u32* l_dstatus = nullptr;  // count statuses + the mismatch count
-  u32* l_hstatus = nullptr;
-  u64 l_capacity = 0;
-  u32* d_crc0 = nullptr;  // slot batches: payload CRCs from init 0
-  u64* d_soff = nullptr;  // slot batches: payload offsets of the contiguous layout
-  u64* d_slen = nullptr;  // strided slots with per-slot sizes: the sizes, an oversize one as 0
-  u64 s_capacity = 0;
-  // fused slot kernel: a ring of counter words, (workgroups done << 32) | mismatches, each 0
-  // between calls (the last workgroup resets its word); consecutive calls take consecutive
-  // words, so even calls that overlap on the device never share one
-  u64* d_slot_counter = nullptr;
-  u32 slot_counter_next = 0;
-  bool fused_slots = true;        // contiguous 4 KiB slot batches take the fused uniform kernel
-  bool small_path = true;         // batches of messages <= 4 KiB take the small-message kernel (crc_small.hip)
-  u64* probe = nullptr;           // experiment hook: per-wave timestamps (subspace_crc_testutil_probe)
-  u32* d_fault = nullptr;         // fault words (crc_device.h FaultRef): [0] kFault* bits, read and cleared by
-                                  // subspace_crc_ctx_check; [1] the generation of the last call whose scan faulted
-  u32 call_gen = 0;               // generation of the latest ragged / long call (never 0 once used)
-  // One call at a time per context (a recursive mutex: the host-slot paths call the device
-  // paths), and device workspace use ordered across streams: a call that uses the context's
-  // device workspaces (ragged / long / two-kernel slot paths, the host-slot staging) on another
-  // stream than the previous such call first waits for ws_done, recorded at the end of every
-  // such call on its own stream. Calls that use no context workspace (the uniform 4 KiB kernel,
-  // the fused slot kernel) take neither step.
-  std::recursive_mutex mu;
-  int depth = 0;                  // nesting of public calls on this thread (under mu)
-  hipEvent_t ws_done = nullptr;
-  hipStream_t ws_stream = nullptr;
-  bool ws_recorded = false;       // ws_done holds the last workspace call
-  bool ws_waited = false;         // the current (outermost) call has ordered its stream
-  hipStream_t ws_call_stream = nullptr;
-};
 
 namespace {
 
@@ -265,7 +180,13 @@ int fault_status(subspace_crc_ctx* c, hipStream_t st) {
   // hipDeviceSynchronize would stall other contexts' streams and break another thread's
   // global-mode graph capture). A bit raised by a kernel still running elsewhere
   // is reported by the next check.
-  HIP_TRY(hipMemsetAsync(c->d_fault, 0, 2 * sizeof(u32), st));
+  // Only word[0] (the kFault* bits): word[1], the generation mark of a faulted scan, stays
+  // until a later scan of that generation clears it (a graph replay's first scan) or the
+  // context moves on to a new generation (every non-graph call). Clearing it here would let
+  // a replay still running on another stream -- graph replays record no workspace event, so
+  // the check cannot wait for them -- stop skipping and index with its untrusted tile_base
+  // (ADVICE r05).
+  HIP_TRY(hipMemsetAsync(c->d_fault, 0, sizeof(u32), st));
   HIP_TRY(hipStreamSynchronize(st));
   c->scan_dirty = true;
   return fail(SUBSPACE_CRC_EFAULT, "device fault 0x%x: %s; the results of the calls since the last check are not valid",
@@ -498,10 +419,11 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
   a.out = out;
   a.rops = c->d_rops;
   a.pow2 = c->d_pow2;
-  a.probe = c->probe;
+  a.probe = c->dev.probe;
   // one workgroup per CU, or more, so that no wave gets more than 32 tiles (G = 32: one ring
   // window, the kernel's in-loop flush then never runs: crc_small.hip); g lanes per message
-  if (c->probe) g = 32;  // (the timestamp-recording instantiation is G = 32's)
+  const bool probe = c->dev.probe && c->dev.small_slot;
+  if (probe) g = 32;  // (the dev library's timestamp-recording instantiation is G = 32's)
   const u64 tiles = ceil_div(count, 64ull / g);
   const unsigned blocks =
       (unsigned)std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSmallRingTiles));
@@ -518,8 +440,8 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
     a.crc_out = slot->crc_out;
     a.error_count = slot->error_count;
     a.counter = c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters);
-    if (c->probe) {  // experiment hook: the timestamp-recording instantiation (tools/small_timeline.py)
-      crc32_small_kernel<512, true, true, 32><<<blocks, 512, lds, st>>>(c->d_tab, c->d_laneops, a);
+    if (probe) {  // development hook (libsubspace_crc_dev.so: tools/small_timeline.py)
+      HIP_TRY(c->dev.small_slot(blocks, lds, st, c->d_tab, c->d_laneops, a));
     } else {
       switch (g) {
 #define SMALL_SLOT_CASE(G) \
@@ -624,6 +546,7 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   HIP_TRY(hipSetDevice(device));
 
   auto* c = new subspace_crc_ctx();
+  c->layout_bytes = (uint32_t)sizeof(subspace_crc_ctx);
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
   c->mem_tiles = (u64)prop.totalGlobalMem / 8192;
@@ -684,21 +607,12 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess) e = hipMemcpy(c->d_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_rops, rops.data(), rops.size() * 4, hipMemcpyHostToDevice);
-#define SET_LDS(WGV)                                                                                         \
-  if (e == hipSuccess)                                                                                       \
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<WGV, false, false>,                                  \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_lds_bytes(WGV / 64));
-  SET_LDS(256) SET_LDS(512) SET_LDS(768) SET_LDS(1024)
-#undef SET_LDS
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, false, false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_lds_bytes(8));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)uniform_slot_lds_bytes(8));
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, false, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_lds_bytes(8));
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)uniform_slot_lds_bytes(8));
   if (e == hipSuccess) e = hipMalloc(&c->d_slot_counter, kSlotCounters * sizeof(u64));
   if (e == hipSuccess) e = hipMemset(c->d_slot_counter, 0, kSlotCounters * sizeof(u64));
   if (e == hipSuccess) e = hipMalloc(&c->d_fault, 4 * sizeof(u32));
@@ -719,8 +633,7 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
         (const void*)crc32_small_kernel<512, false, false, 4>,  (const void*)crc32_small_kernel<512, true, false, 4>,
         (const void*)crc32_small_kernel<512, false, false, 8>,  (const void*)crc32_small_kernel<512, true, false, 8>,
         (const void*)crc32_small_kernel<512, false, false, 16>, (const void*)crc32_small_kernel<512, true, false, 16>,
-        (const void*)crc32_small_kernel<512, false, false, 32>, (const void*)crc32_small_kernel<512, true, false, 32>,
-        (const void*)crc32_small_kernel<512, true, true, 32>};
+        (const void*)crc32_small_kernel<512, false, false, 32>, (const void*)crc32_small_kernel<512, true, false, 32>};
     for (const void* f : small_fns)
       if (e == hipSuccess)
         e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)small_lds_bytes() + 16);
@@ -833,30 +746,20 @@ int subspace_crc32_batch_uniform(subspace_crc_ctx* c, const void* dev_base, uint
   const bool fast = length == 4096 && (stride % 16) == 0 && ((uintptr_t)dev_base % 16) == 0;
   if (fast) {
     const u64 tiles = (count + 1) / 2;
-    const int wg = c->uniform_wg;
-    int blocks = grid_for(c, tiles, wg / 64);
+    int blocks = grid_for(c, tiles, 8);
     if (c->uniform_blocks > 0 && (u64)c->uniform_blocks < (u64)blocks) blocks = c->uniform_blocks;
     const auto* b = static_cast<const uint8_t*>(dev_base);
     const int ord = c->uniform_order;
-    if (c->probe != nullptr) {  // experiment hook: the timestamp-recording instantiation (512 threads)
+    if (c->dev.probe && c->dev.uniform) {  // development hook (libsubspace_crc_dev.so: tools/wave_timeline.py)
       SlotArgs sa{};
-      sa.probe = c->probe;
-      crc32_uniform4k_kernel<512, false, true><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), st>>>(
-          b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, sa);
+      sa.probe = c->dev.probe;
+      HIP_TRY(c->dev.uniform(false, (unsigned)grid_for(c, tiles, 8), st, b, stride, count, c->d_tab, c->d_laneops, init,
+                             final_xor, dev_out, c->zero_word, sa));
       c->zero_word = nullptr;
-      HIP_TRY(hipGetLastError());
       return SUBSPACE_CRC_OK;
     }
-#define LAUNCH(WGV)                                                                                           \
-  crc32_uniform4k_kernel<WGV, false, false><<<blocks, WGV, uniform_lds_bytes(WGV / 64), st>>>(                             \
-      b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, SlotArgs{})
-    switch (wg) {
-      case 256: LAUNCH(256); break;
-      case 768: LAUNCH(768); break;
-      case 1024: LAUNCH(1024); break;
-      default: LAUNCH(512); break;
-    }
-#undef LAUNCH
+    crc32_uniform4k_kernel<512, false, false><<<blocks, 512, uniform_lds_bytes(8), st>>>(
+        b, stride, count, c->d_tab, c->d_laneops, init, final_xor, dev_out, ord, c->zero_word, SlotArgs{});
     c->zero_word = nullptr;
     HIP_TRY(hipGetLastError());
     return SUBSPACE_CRC_OK;
@@ -1003,11 +906,11 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
     const u64 tiles = (count + 1) / 2;
     const u64 blocks = std::max<u64>(grid_for(c, tiles, 512 / 64), ceil_div(tiles, 8ull * kSlotRingRounds));
     SlotArgs sa{prefix_size, mode, dev_status, dev_crc_out, dev_error_count,
-                c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters), c->probe, c->d_fault,
+                c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters), c->dev.probe, c->d_fault,
                 (u32)checksum_size, (u32)metadata_size};
-    if (c->probe)  // experiment hook: the timestamp-recording instantiation
-      crc32_uniform4k_kernel<512, true, true><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
-          buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, 0, nullptr, sa);
+    if (c->dev.probe && c->dev.uniform)  // development hook (libsubspace_crc_dev.so)
+      HIP_TRY(c->dev.uniform(true, (unsigned)blocks, st, buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops,
+                             0u, 0xFFFFFFFFu, nullptr, nullptr, sa));
     else
       crc32_uniform4k_kernel<512, true, false><<<(unsigned)blocks, 512, uniform_slot_lds_bytes(8), st>>>(
           buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops, 0u, 0xFFFFFFFFu, nullptr, 0, nullptr, sa);
@@ -1315,94 +1218,6 @@ int subspace_crc32_host_slot_list(subspace_crc_ctx* c, const subspace_crc_slot* 
   if (rc) return rc;
   if (host_status) std::memcpy(host_status, c->l_hstatus, count * sizeof(u32));
   if (host_error_count) *host_error_count = c->l_hstatus[count];
-  return SUBSPACE_CRC_OK;
-}
-
-// Experiment hook (not part of the public header): named knobs.
-//   "long_path":   1 (default) whole-8 KiB-piece uniform batches take crc32_long_kernel,
-//                  0 they take the ragged path
-//   "fused_slots": 1 (default) contiguous 4 KiB slot batches without metadata take the
-//                  fused slot kernel, 0 the payload kernel + crc32_slot_finish_kernel
-//   "fused_prep":  1 (default) ragged batches with a known arena of at most 2^37 bytes take the
-//                  fused tile-count scan + descriptor kernel, 0 the two kernels
-int subspace_crc_testutil_set(subspace_crc_ctx* c, const char* key, int value) {
-  if (!c || !key) return SUBSPACE_CRC_EINVAL;
-  CallScope scope(c);
-  if (!std::strcmp(key, "stale_ticket")) {
-    // plant a stale tile-count scan ticket (the state a racing or half-finished call could
-    // leave): the next ragged call must report SUBSPACE_CRC_EFAULT through subspace_crc_ctx_check
-    int rc = ensure_ragged_ws(c, 1, 16);
-    if (rc) return rc;
-    const u32 v = (u32)value;
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(c->d_scan_state, &v, sizeof(u32), hipMemcpyHostToDevice));
-    return SUBSPACE_CRC_OK;
-  }
-  if (!std::strcmp(key, "long_path")) {
-    c->long_path = value != 0;
-    return SUBSPACE_CRC_OK;
-  }
-  if (!std::strcmp(key, "fused_slots")) {
-    c->fused_slots = value != 0;
-    return SUBSPACE_CRC_OK;
-  }
-  if (!std::strcmp(key, "fused_prep")) {  // 0: every ragged batch takes the separate descriptor kernel
-    c->fused_prep = value != 0;
-    return SUBSPACE_CRC_OK;
-  }
-  if (!std::strcmp(key, "small_path")) {  // 0: messages <= 4 KiB take the ragged path (A/B, parity)
-    c->small_path = value != 0;
-    return SUBSPACE_CRC_OK;
-  }
-  return SUBSPACE_CRC_EINVAL;
-}
-
-// Experiment hook (not part of the public header): while dev_words is non-null, fixed-size 4 KiB
-// batches run the uniform kernel's PROBE instantiation (512 threads, all CUs), which writes
-// kProbeWords u64 per wave (timestamps, HW_ID, XCC_ID, tile count) to dev_words; the caller
-// sizes it for grid x 8 waves (subspace_crc_testutil_probe_waves).
-int subspace_crc_testutil_probe(subspace_crc_ctx* c, void* dev_words) {
-  if (!c) return SUBSPACE_CRC_EINVAL;
-  c->probe = static_cast<u64*>(dev_words);
-  return SUBSPACE_CRC_OK;
-}
-
-// The number of waves (records) the PROBE launch of a count-message batch has.
-uint64_t subspace_crc_testutil_probe_waves(subspace_crc_ctx* c, uint64_t count) {
-  if (!c) return 0;
-  // the larger of the uniform kernel's grid and the slot kernel's (more workgroups than CUs
-  // when a wave would get more than kSlotRingRounds tiles)
-  const u64 tiles = (count + 1) / 2;
-  return std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSlotRingRounds)) * 8u;
-}
-
-// Experiment hook (not part of the public header): the uniform 4 KiB kernel's product
-// instantiation over `count` messages that all alias the same 4 KiB at dev_base (stride 0), so
-// every line load hits the cache: the kernel's compute-only time at the headline's grid and
-// tile count (the ledger's "compute" row, tools/pmc_ledger.sh). out[i] = the CRC of that one
-// message for every i.
-int subspace_crc_testutil_uniform_alias(subspace_crc_ctx* c, const void* dev_base, uint64_t count, uint32_t* dev_out,
-                                        void* stream) {
-  if (!c || !dev_base || !dev_out || count == 0 || ((uintptr_t)dev_base % 16)) return SUBSPACE_CRC_EINVAL;
-  CallScope scope(c);
-  HIP_TRY(hipSetDevice(c->device));
-  const u64 tiles = (count + 1) / 2;
-  crc32_uniform4k_kernel<512, false, false><<<grid_for(c, tiles, 8), 512, uniform_lds_bytes(8), (hipStream_t)stream>>>(
-      static_cast<const uint8_t*>(dev_base), 0, count, c->d_tab, c->d_laneops, 0u, 0u, dev_out, 0, nullptr,
-      SlotArgs{});
-  HIP_TRY(hipGetLastError());
-  return SUBSPACE_CRC_OK;
-}
-
-// Tuning hook for experiments (not part of the public header): uniform-kernel workgroup
-// size (512/768/1024) and an optional cap on the number of workgroups.
-int subspace_crc_testutil_tune(subspace_crc_ctx* c, int uniform_wg, int uniform_blocks, int uniform_order) {
-  if (!c) return SUBSPACE_CRC_EINVAL;
-  if (uniform_wg != 256 && uniform_wg != 512 && uniform_wg != 768 && uniform_wg != 1024) return SUBSPACE_CRC_EINVAL;
-  if (uniform_order < 0 || uniform_order > 3) return SUBSPACE_CRC_EINVAL;
-  c->uniform_wg = uniform_wg;
-  c->uniform_blocks = uniform_blocks;
-  c->uniform_order = uniform_order;
   return SUBSPACE_CRC_OK;
 }
 

@@ -63,11 +63,15 @@
 //    (the fused uniform slot kernel's scheme: no fences, no memset).
 #include "crc_device.h"
 
-// Timing-only investigation builds (tools/ab_lib.sh -DSUBSPACE_SMALL_VARIANT=n; the product is
-// 0, the others compute nothing valid): 1 no prologue span loads / hash; 2 no flush; 3 no
-// prefix reload in later windows; 4 no byte masking in the repack loop.
+// Timing-only investigation builds (tools/ab_lib.sh -DSUBSPACE_AB_BUILD -DSUBSPACE_SMALL_VARIANT=n;
+// the product is 0, the others compute nothing valid): 1 no prologue span loads / hash; 2 no
+// flush; 3 no prefix reload in later windows; 4 no byte masking in the repack loop. A variant
+// outside an A/B build is a build error (a stray -D must not ship wrong CRCs).
 #ifndef SUBSPACE_SMALL_VARIANT
 #define SUBSPACE_SMALL_VARIANT 0
+#endif
+#if SUBSPACE_SMALL_VARIANT != 0 && !defined(SUBSPACE_AB_BUILD)
+#error "SUBSPACE_SMALL_VARIANT is a timing-only A/B knob (tools/ab_lib.sh defines SUBSPACE_AB_BUILD)"
 #endif
 
 namespace subspace_amd {
@@ -797,6 +801,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   if constexpr (probe) pt[2] = __builtin_amdgcn_s_memrealtime();
   if constexpr (SLOT && SUBSPACE_SMALL_VARIANT != 1) eH = span_hash(pwords, pmeta, eF, eS, ehas);
 
+  // PROBE: tile 0 landed (the first wait of whichever loop form runs; stamped once)
+  auto stamp_tile0 = [&]() __attribute__((always_inline)) {
+    if constexpr (probe)
+      if (pt[3] == 0) pt[3] = __builtin_amdgcn_s_memrealtime();
+  };
   u32 k = 0;
   if (fast) {
     // ping-pong, unrolled by two, one tile in flight (crc_uniform.hip's loop)
@@ -804,18 +813,21 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       const u64 qB = fast_off(k + 1);
       issue_prio_hi();
       drain_before_issue();  // tile k's lines
+      stamp_tile0();
       load_at(B, qB);
       issue_prio_lo();
       process_fast(A, k);
       const u64 qA = fast_off(k + 2);
       issue_prio_hi();
       drain_before_issue();
+      stamp_tile0();
       load_at(A, qA);
       issue_prio_lo();
       process_fast(B, k + 1);
     }
     if (k < nk) {
       drain_before_issue();
+      stamp_tile0();
       process_fast(A, k);
     }
   } else if (repack) {
@@ -827,6 +839,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       rp_rec(p1, s1, L1);
       issue_prio_hi();
       drain_before_issue();  // tile j's lines
+      stamp_tile0();
       load_lines_at(B, s1, rp_ext(s1, L1, p1), (p1 >> 8) & 31u);
       issue_prio_lo();
       process_rp(A, sc, Lc, pc);
@@ -835,6 +848,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       rp_rec(p2, s2, L2);
       issue_prio_hi();
       drain_before_issue();
+      stamp_tile0();
       load_lines_at(A, s2, rp_ext(s2, L2, p2), (p2 >> 8) & 31u);
       issue_prio_lo();
       process_rp(B, s1, L1, p1);
@@ -844,6 +858,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
     if (j < rnt) {
       drain_before_issue();
+      stamp_tile0();
       process_rp(A, sc, Lc, pc);
     }
   } else if (fastu) {
@@ -852,6 +867,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       const u64 qB = u_off(k + 1);
       issue_prio_hi();
       drain_before_issue();  // tile k's lines
+      stamp_tile0();
       u_load(B, k + 1, qB);
       issue_prio_lo();
       if (k && (k & kWinMask) == 0u) flush_u(k - W, W);
@@ -859,6 +875,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       const u64 qA = u_off(k + 2);
       issue_prio_hi();
       drain_before_issue();
+      stamp_tile0();
       u_load(A, k + 2, qA);
       issue_prio_lo();
       if constexpr (W == 1) flush_u(k, 1u);
@@ -866,6 +883,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
     if (k < nk) {
       drain_before_issue();
+      stamp_tile0();
       if (k && (k & kWinMask) == 0u) flush_u(k - W, W);
       process_u(A, k);
     }
@@ -879,6 +897,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     for (; k + 1 < nk; k += 2) {
       issue_prio_hi();       // (crc_device.h)
       drain_before_issue();  // tile k's lines and tile k+1's record
+      stamp_tile0();
       const bool wb = k && (k & kWinMask) == 0u;
       if constexpr (kSplit) {
         if (wb) flush_issue(k - W);
@@ -891,6 +910,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       process(A, sc, Lc, k);
       issue_prio_hi();
       drain_before_issue();
+      stamp_tile0();
       if constexpr (kSplit && W == 1) flush_issue(k);
       const u64 s2 = sA, L2 = LA;
       fetch(k + 3, sB, LB);
@@ -903,6 +923,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
     if (k < nk) {
       drain_before_issue();
+      stamp_tile0();
       if (k && (k & kWinMask) == 0u) flush(k - (kWinMask + 1u), kWinMask + 1u);
       process(A, sc, Lc, k);
     }
@@ -956,6 +977,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   }
 }
 
+// The product instantiations (devtools.hip includes this file for its PROBE instantiation
+// only: libsubspace_crc_dev.so)
+#ifndef SUBSPACE_DEV_TU
 #define SUBSPACE_SMALL_INST(G)                                                                          \
   template __global__ void crc32_small_kernel<512, false, false, G>(const u32*, const u32*, SmallArgs); \
   template __global__ void crc32_small_kernel<512, true, false, G>(const u32*, const u32*, SmallArgs);
@@ -966,6 +990,6 @@ SUBSPACE_SMALL_INST(8)
 SUBSPACE_SMALL_INST(16)
 SUBSPACE_SMALL_INST(32)
 #undef SUBSPACE_SMALL_INST
-template __global__ void crc32_small_kernel<512, true, true, 32>(const u32*, const u32*, SmallArgs);
+#endif
 
 }  // namespace subspace_amd

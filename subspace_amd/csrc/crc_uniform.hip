@@ -49,6 +49,9 @@
 #ifndef SUBSPACE_SLOT_VARIANT
 #define SUBSPACE_SLOT_VARIANT 0
 #endif
+#if SUBSPACE_SLOT_VARIANT != 0 && !defined(SUBSPACE_AB_BUILD)
+#error "SUBSPACE_SLOT_VARIANT is a timing-only A/B knob (define SUBSPACE_AB_BUILD)"
+#endif
 
 namespace subspace_amd {
 
@@ -404,13 +407,12 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
 #define INST(WGV, SL, PR)                                                                                 \
   template __global__ void crc32_uniform4k_kernel<WGV, SL, PR>(const uint8_t*, u64, u64, const u32*, const u32*, u32, \
                                                                u32, u32*, int, u32*, SlotArgs);
-INST(256, false, false)
+// The product instantiations (512 threads: the round-4/5 workgroup sweeps);
+// devtools.hip includes this file for its PROBE ones (libsubspace_crc_dev.so)
+#ifndef SUBSPACE_DEV_TU
 INST(512, false, false)
-INST(768, false, false)
-INST(1024, false, false)
 INST(512, true, false)
-INST(512, false, true)
-INST(512, true, true)
+#endif
 #undef INST
 
 }  // namespace subspace_amd

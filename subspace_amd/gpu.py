@@ -199,12 +199,12 @@ def host_unregister(host) -> None:
 def fill_uniform(buf, stride: int, length: int, count: int, *, seed: int, first_id: int = 0, id_stride: int = 1,
                  stream=None) -> None:
     """Deterministic payloads (SURVEY.md 8d generator) for a fixed-size batch, on device."""
-    _check(_lib.load().subspace_crc_testutil_fill_uniform(
+    _check(_lib.load_dev().subspace_crc_testutil_fill_uniform(
         _ptr(buf), stride, length, count, first_id, id_stride, seed, _stream_ptr(stream)), "fill_uniform")
 
 
 def fill_ragged(buf, offsets, lengths, *, seed: int, first_id: int = 0, id_stride: int = 1, stream=None) -> None:
-    _check(_lib.load().subspace_crc_testutil_fill_ragged(
+    _check(_lib.load_dev().subspace_crc_testutil_fill_ragged(
         _ptr(buf), _ptr(offsets), _ptr(lengths), int(offsets.numel()), first_id, id_stride, seed,
         _stream_ptr(stream)), "fill_ragged")
 
@@ -215,7 +215,7 @@ def slot_list_read(records, count: int, out, mode: int = 4, stride: int = 0, lds
     window's records in registers, one address and 8 immediate offsets per tile, the first
     window's prefix words) -- with an XOR fold instead of the CRC; out: int32 device tensor of at
     least the kernel's grid x 512 words (256 * 512 covers every count up to 2^22 slots)."""
-    _check(_lib.load().subspace_crc_testutil_slot_list_read(
+    _check(_lib.load_dev().subspace_crc_testutil_slot_list_read(
         _ptr(records), int(count), int(mode), int(stride), 1 if lds else 0, _ptr(out), int(out.numel()),
         _stream_ptr(stream)), "slot_list_read")
 
@@ -225,5 +225,5 @@ def stream_read(buf, out, stream=None) -> None:
     out: int32 device tensor of 256 * 512 words."""
     if int(out.numel()) < 256 * 512:
         raise ValueError("out needs 131072 words")
-    _check(_lib.load().subspace_crc_testutil_stream_read(
+    _check(_lib.load_dev().subspace_crc_testutil_stream_read(
         _ptr(buf), int(buf.numel() * buf.element_size()), _ptr(out), _stream_ptr(stream)), "stream_read")

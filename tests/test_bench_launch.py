@@ -105,8 +105,24 @@ def test_settle_waits_for_a_steady_launch_rate():
 
 
 def _rank_envs(stdout: str) -> dict:
-    recs = [json.loads(ln) for ln in stdout.splitlines() if ln.startswith('{"rank"')]
+    """The rank records in the launcher's stdout. Each rank writes its record as one write(2) of
+    a whole line (bench.py), so lines never interleave; the records are still decoded wherever
+    they start in a line, so a launcher's own output on the same line cannot hide one."""
+    dec, recs = json.JSONDecoder(), []
+    for ln in stdout.splitlines():
+        i = ln.find('{"rank"')
+        while i >= 0:
+            rec, end = dec.raw_decode(ln, i)
+            recs.append(rec)
+            i = ln.find('{"rank"', end)
     return {r["rank"]: r["env"] for r in recs}
+
+
+def test_rank_records_parse_even_when_two_share_a_line():
+    a = json.dumps({"rank": 0, "env": {"X": "1"}})
+    b = json.dumps({"rank": 1, "env": {"X": "1"}})
+    assert _rank_envs(a + b + "\n\n") == {0: {"X": "1"}, 1: {"X": "1"}}
+    assert _rank_envs("noise " + a + "\n" + b + "\n") == {0: {"X": "1"}, 1: {"X": "1"}}
 
 
 def test_both_launch_forms_give_ranks_the_same_environment():
@@ -116,6 +132,7 @@ def test_both_launch_forms_give_ranks_the_same_environment():
     apply_rank_env, first thing in main), even when the parent environment lacks it."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "HSA_ENABLE_IPC_MODE_LEGACY")}
+    env["PYTHONUNBUFFERED"] = "1"  # (the condition of the round-5 flake: print's two writes per record)
     spawn = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--print-rank-env"],
                            capture_output=True, text=True, timeout=120, env=env, cwd=str(ROOT))
     assert spawn.returncode == 0, spawn.stderr[-3000:]

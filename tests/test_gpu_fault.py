@@ -8,6 +8,8 @@ in the fault words) skip work that would index with an untrusted tile_base, and
 subspace_crc_ctx_check returns SUBSPACE_CRC_EFAULT (then clears the fault and resets the scan
 state). A later call is correct with or without a check in between.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -33,7 +35,6 @@ def test_stale_scan_ticket_reports_efault(gpu_ctx, oracle, ticket):
     """ticket 2^30: every workgroup's ticket is beyond the grid (kFaultTicket, no wait);
     ticket 1: tickets 1.. wait for a predecessor that never publishes (kFaultLookbackSpin
     after the bounded spin, ~1 s) and the last one is beyond the grid."""
-    lib = _lib.load()
     n = 3 * 4096  # four count-scan workgroups
     buf, d_off, d_len, lengths = _ragged_batch(n, seed=0xFA17)
     want = oracle.synth_crc_batch(0xFA17, lengths)
@@ -42,7 +43,7 @@ def test_stale_scan_ticket_reports_efault(gpu_ctx, oracle, ticket):
     gpu_ctx.crc32_ragged(buf, d_off, d_len, out)
     gpu_ctx.check()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
-    assert lib.subspace_crc_testutil_set(gpu_ctx._h, b"stale_ticket", ticket) == 0
+    assert _lib.load_dev().subspace_crc_testutil_set(gpu_ctx._h, b"stale_ticket", ticket) == 0
     gpu_ctx.crc32_ragged(buf, d_off, d_len, out)  # asynchronous: returns OK
     with pytest.raises(gpu.CrcError) as ei:
         gpu_ctx.check()
@@ -80,13 +81,13 @@ def test_fault_marks_only_its_own_call(gpu_ctx, oracle):
     not every later one. A caller that never calls check still gets correct CRCs from the next
     call (whose kernels start from the state the faulted call's later kernels reset), and the
     fault is still reported by the next check."""
-    lib = _lib.load()
     n = 3 * 4096
     buf, d_off, d_len, lengths = _ragged_batch(n, seed=0xFA18)
     want = oracle.synth_crc_batch(0xFA18, lengths)
     out = torch.zeros(n, dtype=torch.int32, device=DEV)
+    gpu_ctx.reserve(n, 4 * n)  # (the stale ticket is planted in the ragged workspace)
     gpu_ctx.check()
-    assert lib.subspace_crc_testutil_set(gpu_ctx._h, b"stale_ticket", 1 << 30) == 0
+    assert _lib.load_dev().subspace_crc_testutil_set(gpu_ctx._h, b"stale_ticket", 1 << 30) == 0
     gpu_ctx.crc32_ragged(buf, d_off, d_len, out)  # faults: its kernels skip
     out2 = torch.zeros(n, dtype=torch.int32, device=DEV)
     gpu_ctx.crc32_ragged(buf, d_off, d_len, out2)  # no check in between
@@ -103,7 +104,6 @@ def test_fault_mark_does_not_outlive_a_graph_replay(gpu_ctx, oracle):
     in one replay marks that generation; the next replay's tile-count scan (ticket 0) clears the
     mark, so the replay after a faulted one computes every CRC without a check in between, and
     the fault is still reported by the next check."""
-    lib = _lib.load()
     n = 3 * 4096
     buf, d_off, d_len, lengths = _ragged_batch(n, seed=0xFA19)
     want = oracle.synth_crc_batch(0xFA19, lengths)
@@ -123,7 +123,7 @@ def test_fault_mark_does_not_outlive_a_graph_replay(gpu_ctx, oracle):
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
     gpu_ctx.check()
-    assert lib.subspace_crc_testutil_set(gpu_ctx._h, b"stale_ticket", 1 << 30) == 0
+    assert _lib.load_dev().subspace_crc_testutil_set(gpu_ctx._h, b"stale_ticket", 1 << 30) == 0
     g.replay()  # faults: its kernels skip
     torch.cuda.synchronize()
     out.zero_()
@@ -138,5 +138,42 @@ def test_fault_mark_does_not_outlive_a_graph_replay(gpu_ctx, oracle):
     out.zero_()
     g.replay()
     torch.cuda.synchronize()
+    gpu_ctx.check()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
+def _fault_words(ctx):
+    w = (ctypes.c_uint32 * 2)()
+    assert _lib.load_dev().subspace_crc_testutil_fault_words(ctx._h, w, None) == 0
+    return int(w[0]), int(w[1])
+
+
+def test_check_clears_the_fault_bits_but_keeps_the_generation_mark(gpu_ctx, oracle):
+    """subspace_crc_ctx_check clears word 0 (the kFault* bits) only. Word 1, the
+    generation of the call whose scan faulted, stays: a graph replay of that generation still
+    running on another stream (replays record no workspace event, so the check cannot wait for
+    them) must keep skipping its tile_base-indexed work. A later non-graph call takes a new
+    generation and runs normally."""
+    n = 3 * 4096
+    buf, d_off, d_len, lengths = _ragged_batch(n, seed=0xFA1A)
+    want = oracle.synth_crc_batch(0xFA1A, lengths)
+    out = torch.zeros(n, dtype=torch.int32, device=DEV)
+    gpu_ctx.crc32_ragged(buf, d_off, d_len, out)
+    gpu_ctx.check()
+    assert _fault_words(gpu_ctx)[0] == 0
+    assert _lib.load_dev().subspace_crc_testutil_set(gpu_ctx._h, b"stale_ticket", 1 << 30) == 0
+    gpu_ctx.crc32_ragged(buf, d_off, d_len, out)  # faults
+    gen = int(_lib.load_dev().subspace_crc_testutil_call_gen(gpu_ctx._h))
+    torch.cuda.synchronize()
+    bits, mark = _fault_words(gpu_ctx)
+    assert bits != 0 and mark == gen
+    with pytest.raises(gpu.CrcError) as ei:
+        gpu_ctx.check()
+    assert ei.value.code == gpu.EFAULT
+    bits, mark = _fault_words(gpu_ctx)
+    assert bits == 0 and mark == gen  # the mark outlives the check
+    out.zero_()
+    gpu_ctx.crc32_ragged(buf, d_off, d_len, out)  # a new generation: not skipped
+    assert int(_lib.load_dev().subspace_crc_testutil_call_gen(gpu_ctx._h)) != gen
     gpu_ctx.check()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)

@@ -13,9 +13,6 @@ N, SIZE = 65536, 4096
 def _probe_lib(gpu_ctx):
     from subspace_amd import _lib
     lib = _lib.load()
-    lib.subspace_crc_testutil_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    lib.subspace_crc_testutil_probe_waves.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    lib.subspace_crc_testutil_probe_waves.restype = ctypes.c_uint64
     return lib
 
 
@@ -37,18 +34,18 @@ def test_probe_uniform_matches_product(gpu_ctx):
     import torch
     from subspace_amd import gpu
     lib = _probe_lib(gpu_ctx)
-    waves = int(lib.subspace_crc_testutil_probe_waves(gpu_ctx._h, N))
+    waves = int(_lib.load_dev().subspace_crc_testutil_probe_waves(gpu_ctx._h, N))
     buf = torch.empty(N * SIZE, dtype=torch.uint8, device="cuda")
     gpu.fill_uniform(buf, SIZE, SIZE, N, seed=0x5EED000B)
     ref = torch.empty(N, dtype=torch.int32, device="cuda")
     out = torch.empty_like(ref)
     gpu_ctx.crc32_uniform(buf, SIZE, SIZE, N, ref)
     rec = torch.zeros((waves, 8), dtype=torch.int64, device="cuda")
-    lib.subspace_crc_testutil_probe(gpu_ctx._h, ctypes.c_void_p(rec.data_ptr()))
+    _lib.load_dev().subspace_crc_testutil_probe(gpu_ctx._h, ctypes.c_void_p(rec.data_ptr()))
     try:
         gpu_ctx.crc32_uniform(buf, SIZE, SIZE, N, out)
     finally:
-        lib.subspace_crc_testutil_probe(gpu_ctx._h, None)
+        _lib.load_dev().subspace_crc_testutil_probe(gpu_ctx._h, None)
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
     r = rec.cpu().numpy()
@@ -64,7 +61,7 @@ def test_probe_slots_matches_product(gpu_ctx):
     from subspace_amd import gpu, slots
     lib = _probe_lib(gpu_ctx)
     n = 4099  # odd: the last tile has one slot
-    waves = int(lib.subspace_crc_testutil_probe_waves(gpu_ctx._h, n))
+    waves = int(_lib.load_dev().subspace_crc_testutil_probe_waves(gpu_ctx._h, n))
     ps, stride = slots.compute_prefix_size(4, 0), slots.slot_stride(SIZE, 4, 0)
     host = np.random.default_rng(11).integers(0, 256, stride * n, dtype=np.uint8)
     host.reshape(n, stride)[:, :ps] = slots.make_prefixes(n, np.full(n, SIZE, dtype=np.uint64), checksum_size=4,
@@ -73,11 +70,11 @@ def test_probe_slots_matches_product(gpu_ctx):
     b = torch.from_numpy(host.copy()).cuda()
     gpu_ctx.crc32_slots_strided(a, stride, n, message_size=SIZE, mode=gpu.SLOT_CALCULATE)
     rec = torch.zeros((waves, 8), dtype=torch.int64, device="cuda")
-    lib.subspace_crc_testutil_probe(gpu_ctx._h, ctypes.c_void_p(rec.data_ptr()))
+    _lib.load_dev().subspace_crc_testutil_probe(gpu_ctx._h, ctypes.c_void_p(rec.data_ptr()))
     try:
         gpu_ctx.crc32_slots_strided(b, stride, n, message_size=SIZE, mode=gpu.SLOT_CALCULATE)
     finally:
-        lib.subspace_crc_testutil_probe(gpu_ctx._h, None)
+        _lib.load_dev().subspace_crc_testutil_probe(gpu_ctx._h, None)
     torch.cuda.synchronize()
     assert torch.equal(a, b)  # identical prefixes written
     r = rec.cpu().numpy()

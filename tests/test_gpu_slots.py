@@ -443,12 +443,12 @@ def test_fused_and_two_kernel_slot_paths_agree(gpu_ctx):
     host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=4242)
     out = []
     for fused in (0, 1):
-        assert lib.subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", fused) == 0
+        assert _lib.load_dev().subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", fused) == 0
         try:
             dev, status = publish_strided(gpu_ctx, host.copy(), stride, count, cs, ms, message_size=4096)
             out.append((dev.cpu().numpy(), status))
         finally:
-            lib.subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", 1)
+            _lib.load_dev().subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", 1)
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
 
 
@@ -490,12 +490,12 @@ def test_calculate_zeroes_error_count(gpu_ctx, fused):
     host, ps, stride = build_channel(count, 4096, cs, ms, sizes, seed=606)
     dev = torch.from_numpy(host).to(DEV)
     err = torch.full((1,), 777, dtype=torch.int32, device=DEV)
-    assert lib.subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", fused) == 0
+    assert _lib.load_dev().subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", fused) == 0
     try:
         gpu_ctx.crc32_slots_strided(dev, stride, count, message_size=4096, mode=gpu.SLOT_CALCULATE, error_count=err)
         torch.cuda.synchronize()
     finally:
-        lib.subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", 1)
+        _lib.load_dev().subspace_crc_testutil_set(gpu_ctx._h, b"fused_slots", 1)
     assert int(err.item()) == 0
 
 

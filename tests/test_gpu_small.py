@@ -14,7 +14,7 @@ import pytest
 
 torch = pytest.importorskip("torch")
 
-from subspace_amd import gpu, slots  # noqa: E402
+from subspace_amd import _lib, gpu, slots  # noqa: E402
 from test_gpu_parity import M32, expected_uniform, run_uniform  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -94,7 +94,7 @@ def run_slot_list(ctx, pre_host, pay_host, pay_off, sizes, order, ps, cs, ms, ma
     status = torch.full((n,), 7, dtype=torch.int32, device=DEV)
     err = torch.full((1,), 12345, dtype=torch.int32, device=DEV)
     if lib is not None:
-        assert lib.subspace_crc_testutil_set(ctx._h, b"small_path", int(small)) == 0
+        assert _lib.load_dev().subspace_crc_testutil_set(ctx._h, b"small_path", int(small)) == 0
     try:
         ctx.crc32_slots(d_rec, max_message_size=max_size, checksum_size=cs, metadata_size=ms, mode=mode,
                         status=status, error_count=err if mode == gpu.SLOT_VERIFY else None)
@@ -102,7 +102,7 @@ def run_slot_list(ctx, pre_host, pay_host, pay_off, sizes, order, ps, cs, ms, ma
         ctx.check()
     finally:
         if lib is not None:
-            lib.subspace_crc_testutil_set(ctx._h, b"small_path", 1)
+            _lib.load_dev().subspace_crc_testutil_set(ctx._h, b"small_path", 1)
     st = np.empty(n, dtype=np.uint32)
     st[order] = status.cpu().numpy().view(np.uint32)  # back to slot order
     assert np.array_equal(d_pay.cpu().numpy(), pay_host)  # payloads are never written
@@ -227,13 +227,13 @@ def test_slot_list_repack(gpu_ctx, oracle, lib, gen_max, count, spoil, cs, ms):
 def wave_records(ctx, lib, run):
     """The fused slot kernel's per-wave experiment records (crc_small.hip PROBE: lane 7 = nk << 32
     | fast << 48 | repack << 49 | packed tiles << 52) for one call `run()`."""
-    waves = int(lib.subspace_crc_testutil_probe_waves(ctx._h, 1 << 22))
+    waves = int(_lib.load_dev().subspace_crc_testutil_probe_waves(ctx._h, 1 << 22))
     rb = torch.zeros(waves * 8, dtype=torch.int64, device=DEV)
-    assert lib.subspace_crc_testutil_probe(ctx._h, rb.data_ptr()) == 0
+    assert _lib.load_dev().subspace_crc_testutil_probe(ctx._h, rb.data_ptr()) == 0
     try:
         run()
     finally:
-        lib.subspace_crc_testutil_probe(ctx._h, None)
+        _lib.load_dev().subspace_crc_testutil_probe(ctx._h, None)
     return rb.cpu().numpy().view(np.uint64).reshape(waves, 8)
 
 

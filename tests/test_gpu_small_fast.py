@@ -10,7 +10,7 @@ import pytest
 
 torch = pytest.importorskip("torch")
 
-from subspace_amd import gpu, slots  # noqa: E402
+from subspace_amd import _lib, gpu, slots  # noqa: E402
 from test_gpu_small import oracle_arena, run_slot_list  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -44,13 +44,13 @@ def general_waves(ctx, lib, run):
     """Runs `run()` (one slot call) with the kernel's experiment hook on and returns (waves with
     tiles, of which general -- not FAST) from its per-wave records (crc_small.hip: lane 7 stores
     nk << 32 | fast << 48)."""
-    waves = int(lib.subspace_crc_testutil_probe_waves(ctx._h, 1 << 22))
+    waves = int(_lib.load_dev().subspace_crc_testutil_probe_waves(ctx._h, 1 << 22))
     rb = torch.zeros(waves * 8, dtype=torch.int64, device=DEV)
-    assert lib.subspace_crc_testutil_probe(ctx._h, rb.data_ptr()) == 0
+    assert _lib.load_dev().subspace_crc_testutil_probe(ctx._h, rb.data_ptr()) == 0
     try:
         run()
     finally:
-        lib.subspace_crc_testutil_probe(ctx._h, None)
+        _lib.load_dev().subspace_crc_testutil_probe(ctx._h, None)
     r = rb.cpu().numpy().view(np.uint64).reshape(waves, 8)
     nk = (r[:, 7] >> np.uint64(32)) & np.uint64(0xFFFF)
     fast = (r[:, 7] >> np.uint64(48)) & np.uint64(1)

@@ -71,6 +71,11 @@ for s in $STEPS; do
         timeout -k 10 300 python tools/wave_timeline.py --mode $m --launches 20 > "$OUT/timeline_$m.jsonl" 2> "$OUT/timeline_$m.err"
         stop_if_fault $? "timeline_$m"
       done ;;
+    smalltl)  # small-kernel timelines (PROBE hook): S_short's and S_mixed's shuffled lists, config S's
+      for z in 256 mixed 4096; do
+        timeout -k 10 300 python tools/small_timeline.py --sizes $z --launches 20 > "$OUT/smalltl_$z.json" 2> "$OUT/smalltl_$z.err"
+        stop_if_fault $? "smalltl_$z"
+      done ;;
     *)
       echo "unknown step $s" >> "$OUT/status.txt" ;;
   esac

@@ -32,7 +32,7 @@ def main():
 
     def lds(nbytes):
         def f(b):
-            rc = lib.subspace_crc_testutil_stream_read_lds(b.data_ptr(), N * SIZE, sink.data_ptr(), nbytes, st)
+            rc = _lib.load_dev().subspace_crc_testutil_stream_read_lds(b.data_ptr(), N * SIZE, sink.data_ptr(), nbytes, st)
             assert rc == 0
         return f
     variants = {"read": lambda b: gpu.stream_read(b, sink), "read_lds0": lds(0), "read_lds64k": lds(64 << 10),

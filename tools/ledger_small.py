@@ -91,7 +91,7 @@ def main():
                         status=status if st_out else None, error_count=errs)
 
     def probe(r, rec, lds=1):
-        rc = lib.subspace_crc_testutil_slot_list_read(r.data_ptr(), N, rec, stride, lds, sink.data_ptr(), sink.numel(),
+        rc = _lib.load_dev().subspace_crc_testutil_slot_list_read(r.data_ptr(), N, rec, stride, lds, sink.data_ptr(), sink.numel(),
                                                       st.cuda_stream)
         if rc != 0:
             raise SystemExit(f"slot_list_read failed: {rc}")

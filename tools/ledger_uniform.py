@@ -30,7 +30,7 @@ def main():
     ctx = gpu.CrcContext(0)
     lib = _lib.load()
     wg = int(os.environ.get("UNIFORM_WG", "512"))  # the tuning hook's workgroup size (512: the product's)
-    if wg != 512 and lib.subspace_crc_testutil_tune(ctx._h, wg, 0, 0) != 0:
+    if wg != 512 and _lib.load_dev().subspace_crc_testutil_tune(ctx._h, wg, 0, 0) != 0:
         raise SystemExit(f"tune failed: {_lib.last_error()}")
     dev = torch.device("cuda", 0)
     bufs = [torch.empty(count * 4096, dtype=torch.uint8, device=dev) for _ in range(nb)]
@@ -44,7 +44,7 @@ def main():
         if mode == "hbm":
             ctx.crc32_uniform(bufs[i % nb], 4096, 4096, count, out)
         elif mode == "l2":
-            rc = lib.subspace_crc_testutil_uniform_alias(ctx._h, bufs[0].data_ptr(), count, out.data_ptr(),
+            rc = _lib.load_dev().subspace_crc_testutil_uniform_alias(ctx._h, bufs[0].data_ptr(), count, out.data_ptr(),
                                                          st.cuda_stream)
             if rc != 0:
                 raise SystemExit(f"uniform_alias failed: {_lib.last_error()}")

@@ -10,6 +10,11 @@ and prints, as medians over launches, the percentiles over waves of each stamp r
 launch's first entry, and per-wave phase durations. Clock: s_memrealtime, 100 MHz.
 
   python tools/small_timeline.py [--launches 20] [--order shuffled|ordered] [--mode verify|publish]
+                                 [--sizes 4096|256|mixed]
+--sizes: the channel's messages -- 4096 (config S), 256 (S_short: 256-B messages in the 4 KiB
+slots) or mixed (S_mixed: 1 .. 4,096 B uniformly random); the slot list's max_message_size is
+4,096 for all. With the repack loop (S_short, S_mixed) the record also carries each wave's
+packed tile count (rnt), and the output relates it to the wave's loop time.
 """
 import argparse
 import ctypes
@@ -38,22 +43,22 @@ def main():
     ap.add_argument("--order", default="shuffled", choices=["shuffled", "ordered", "alias"],
                     help="alias: every record points at slot 0 of copy 0 (the compute-only run)")
     ap.add_argument("--mode", default="verify", choices=["verify", "publish"])
+    ap.add_argument("--sizes", default="4096", choices=["4096", "256", "mixed"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ctx = gpu.CrcContext(0)
     lib = _lib.load()
-    lib.subspace_crc_testutil_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    lib.subspace_crc_testutil_probe_waves.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    lib.subspace_crc_testutil_probe_waves.restype = ctypes.c_uint64
-    waves = int(lib.subspace_crc_testutil_probe_waves(ctx._h, N))
+    waves = int(_lib.load_dev().subspace_crc_testutil_probe_waves(ctx._h, N))
     ps, stride = slots.compute_prefix_size(4, 0), slots.slot_stride(SIZE, 4, 0)
     rng = np.random.default_rng(0x5EED0005)
+    sizes = {"4096": np.full(N, SIZE, dtype=np.uint64), "256": np.full(N, 256, dtype=np.uint64),
+             "mixed": rng.integers(1, SIZE + 1, N).astype(np.uint64)}[a.sizes]
     host = rng.integers(0, 256, stride * N, dtype=np.uint8)
-    host.reshape(N, stride)[:, :ps] = slots.make_prefixes(N, np.full(N, SIZE, dtype=np.uint64), checksum_size=4,
-                                                          metadata_size=0, seed=5)
+    host.reshape(N, stride)[:, :ps] = slots.make_prefixes(N, sizes, checksum_size=4, metadata_size=0, seed=5)
     bufs = [torch.from_numpy(host).to(dev) for _ in range(NB)]
+    d_sizes = torch.from_numpy(sizes.view(np.int64)).to(dev)
     for b in bufs:
-        ctx.crc32_slots_strided(b, stride, N, message_size=SIZE, checksum_size=4, metadata_size=0,
+        ctx.crc32_slots_strided(b, stride, N, sizes=d_sizes, checksum_size=4, metadata_size=0,
                                 mode=gpu.SLOT_CALCULATE)
     order = {"shuffled": rng.permutation(N).astype(np.uint64), "ordered": np.arange(N, dtype=np.uint64),
              "alias": np.zeros(N, dtype=np.uint64)}[a.order]
@@ -61,7 +66,7 @@ def main():
     for b in (bufs if a.order != "alias" else bufs[:1] * NB):
         b0 = np.uint64(b.data_ptr())
         r = np.stack([b0 + order * np.uint64(stride), b0 + order * np.uint64(stride) + np.uint64(ps),
-                      np.full(N, SIZE, dtype=np.uint64)], axis=1)
+                      sizes[order.astype(np.int64)]], axis=1)
         recs.append(torch.from_numpy(np.ascontiguousarray(r).view(np.int64)).to(dev))
     status = torch.empty(N, dtype=torch.int32, device=dev)
     errs = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -76,12 +81,12 @@ def main():
     rec_bufs = [torch.zeros(waves * WORDS, dtype=torch.int64, device=dev) for _ in range(a.launches)]
     torch.cuda.synchronize()
     for i, rb in enumerate(rec_bufs):
-        lib.subspace_crc_testutil_probe(ctx._h, rb.data_ptr())
+        _lib.load_dev().subspace_crc_testutil_probe(ctx._h, rb.data_ptr())
         launch(a.settle + i)
-    lib.subspace_crc_testutil_probe(ctx._h, None)
+    _lib.load_dev().subspace_crc_testutil_probe(ctx._h, None)
     torch.cuda.synchronize()
     per = {k: [] for k in STAMPS}
-    dur = {"records": [], "fill": [], "loop": [], "flush": [], "tail": [], "total": []}
+    dur = {"records": [], "fill": [], "tile0": [], "loop": [], "flush": [], "tail": [], "total": []}
     gaps = []
     prev_exit = None
     for rb in rec_bufs:
@@ -93,11 +98,10 @@ def main():
             gaps.append((t0 - prev_exit) * TICK_US)
         prev_exit = r[:, 6].max()
         for j, k in enumerate(STAMPS):
-            if k == "tile0":
-                continue
             per[k].append([pct((r[:, j] - t0) * TICK_US, q) for q in (0, 10, 50, 90, 100)])
         dur["records"].append(np.median((r[:, 1] - r[:, 0]) * TICK_US))
         dur["fill"].append(np.median((r[:, 2] - r[:, 1]) * TICK_US))
+        dur["tile0"].append(np.median((r[:, 3] - r[:, 2]) * TICK_US))
         dur["loop"].append(np.median((r[:, 4] - r[:, 2]) * TICK_US))
         dur["flush"].append(np.median((r[:, 5] - r[:, 4]) * TICK_US))
         dur["tail"].append(np.median((r[:, 6] - r[:, 5]) * TICK_US))
@@ -110,7 +114,28 @@ def main():
         w = np.arange(waves) % 8
         by_wave["loop_end"].append([np.median((r[w == i, 4] - t0) * TICK_US) for i in range(8)])
         by_wave["exit"].append([np.median((r[w == i, 6] - t0) * TICK_US) for i in range(8)])
-    out = {"order": a.order, "mode": a.mode, "launches": a.launches, "waves": waves, "fast_waves": fast,
+    # the repack loop's packed tiles per wave (record word 7 bits 52..) against the wave's loop time
+    last = rec_bufs[-1].cpu().numpy().view(np.uint64).reshape(waves, WORDS)
+    rnt = ((last[:, 7] >> 52) & 0xFFF).astype(np.int64)
+    nk = ((last[:, 7] >> 32) & 0xFFFF).astype(np.int64)
+    lr = last.astype(np.int64)
+    loop_us = (lr[:, 4] - lr[:, 2]) * TICK_US
+    live = lr[:, 0] > 0
+    rep = {}
+    if (rnt[live] > 0).any():
+        t0l = lr[live, 0].min()
+        rep = {"rnt_p0_p50_p100": [int(np.percentile(rnt[live], q)) for q in (0, 50, 100)],
+               "nk_p50": int(np.median(nk[live])),
+               "loop_us_by_rnt": {int(v): round(float(np.median(loop_us[live & (rnt == v)])), 2)
+                                  for v in np.unique(rnt[live])},
+               "flush_end_us_by_rnt": {int(v): round(float(np.median((lr[live & (rnt == v), 5] - t0l) * TICK_US)), 2)
+                                       for v in np.unique(rnt[live])},
+               # the two waves of a SIMD (wave slots w, w + 4 of a workgroup: front_slot pairs)
+               "simd_pair_tiles_p50_p100": [int(np.percentile((rnt.reshape(-1, 8)[:, :4] + rnt.reshape(-1, 8)[:, 4:]), q))
+                                            for q in (50, 100)],
+               "cu_tiles_p50_p100": [int(np.percentile(rnt.reshape(-1, 8).sum(1), q)) for q in (50, 100)]}
+    out = {"order": a.order, "mode": a.mode, "sizes": a.sizes, "launches": a.launches, "waves": waves,
+           "fast_waves": fast, "repack": rep,
            "stamp_us_p0_p10_p50_p90_p100": {k: np.median(np.array(v), axis=0).round(2).tolist()
                                              for k, v in per.items() if v},
            "median_wave_phase_us": {k: round(float(np.median(v)), 2) for k, v in dur.items()},

@@ -37,7 +37,7 @@ def main():
         ref = None
         for r in range(rounds):
             for wg, order, nb_cap in [(a, b, c) for a in wgs for b in orders for c in blocks]:
-                if lib.subspace_crc_testutil_tune(ctx._h, wg, nb_cap, order) != 0:
+                if _lib.load_dev().subspace_crc_testutil_tune(ctx._h, wg, nb_cap, order) != 0:
                     raise SystemExit(f"bad variant wg={wg} order={order}")
                 if r == 0:  # every variant must produce the same CRCs
                     ctx.crc32_uniform(bufs[0], 4096, 4096, count, out)

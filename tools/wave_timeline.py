@@ -42,10 +42,10 @@ def main():
     dev = torch.device("cuda", 0)
     ctx = gpu.CrcContext(0)
     lib = _lib.load()
-    lib.subspace_crc_testutil_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    lib.subspace_crc_testutil_probe_waves.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    lib.subspace_crc_testutil_probe_waves.restype = ctypes.c_uint64
-    waves = int(lib.subspace_crc_testutil_probe_waves(ctx._h, N))
+    _lib.load_dev().subspace_crc_testutil_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    _lib.load_dev().subspace_crc_testutil_probe_waves.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    _lib.load_dev().subspace_crc_testutil_probe_waves.restype = ctypes.c_uint64
+    waves = int(_lib.load_dev().subspace_crc_testutil_probe_waves(ctx._h, N))
     out = torch.empty(N, dtype=torch.int32, device=dev)
     errs = torch.zeros(1, dtype=torch.int32, device=dev)
     if a.mode == "uniform":
@@ -81,22 +81,22 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     for i in range(a.launches):
-        lib.subspace_crc_testutil_probe(ctx._h, ctypes.c_void_p(rec[i].data_ptr()))
+        _lib.load_dev().subspace_crc_testutil_probe(ctx._h, ctypes.c_void_p(rec[i].data_ptr()))
         launch(bufs[(a.settle + i) % NBUF], out)
     ev1.record()
-    lib.subspace_crc_testutil_probe(ctx._h, None)
+    _lib.load_dev().subspace_crc_testutil_probe(ctx._h, None)
     torch.cuda.synchronize()
     span_ms = ev0.elapsed_time(ev1) / a.launches
     # the probe launch computes the same results
-    lib.subspace_crc_testutil_probe(ctx._h, ctypes.c_void_p(rec[0].data_ptr()))
+    _lib.load_dev().subspace_crc_testutil_probe(ctx._h, ctypes.c_void_p(rec[0].data_ptr()))
     launch(bufs[0], out)
-    lib.subspace_crc_testutil_probe(ctx._h, None)
+    _lib.load_dev().subspace_crc_testutil_probe(ctx._h, None)
     torch.cuda.synchronize()
     check = not os.environ.get("SLOT_GAP_NOCHECK")  # (timing-only builds compute nothing valid)
     if a.mode != "publish" and check:
         assert torch.equal(out, ref), "PROBE instantiation results differ"
     if a.mode in ("uniform", "uniform4160"):
-        lib.subspace_crc_testutil_probe(ctx._h, None)
+        _lib.load_dev().subspace_crc_testutil_probe(ctx._h, None)
     assert int(errs.item()) == 0 or not check
     r = rec.cpu().numpy()[1:]  # launch 0 was overwritten by the check above
     if a.out:
