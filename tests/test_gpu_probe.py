@@ -5,13 +5,14 @@ import ctypes
 import numpy as np
 import pytest
 
+from subspace_amd import _lib
+
 pytestmark = pytest.mark.gpu
 
 N, SIZE = 65536, 4096
 
 
 def _probe_lib(gpu_ctx):
-    from subspace_amd import _lib
     lib = _lib.load()
     return lib
 
