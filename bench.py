@@ -100,7 +100,7 @@ def parse():
                          "E: 8 Mi x 4 KiB sharded round-robin over the GPUs (strong scaling) + RCCL gather")
     ap.add_argument("--configs", default=None,
                     help="secondary configs timed after the headline at N = 1 (comma list of C, Cu, D, Du, S, "
-                         "Usmall, S_short, S_mixed; default C,Cu,D,Du,S,Usmall,S_short,S_mixed with workload B, none otherwise; "
+                         "Usmall, S_short, S_mixed, S_large; default C,Cu,D,Du,S,Usmall,S_short,S_mixed,S_large with workload B, none otherwise; "
                          "'none' disables)")
     ap.add_argument("--config-iters", type=int, default=20)
     ap.add_argument("--no-solo", action="store_true", help="N > 1: skip rank 0's single-GPU reference leg")
@@ -720,6 +720,8 @@ def secondary_configs(ctx, dev, names, iters) -> dict:
             res[name] = short_slots_config(ctx, dev)
         elif name == "S_mixed":
             res[name] = short_slots_config(ctx, dev, mixed=True)
+        elif name == "S_large":
+            res.update(large_slots_config(ctx, dev))
 
     # No torch.cuda.empty_cache() between configs: VRAM given back to the driver is wiped in the
     # background for seconds (every HBM-bound kernel ~2-4 % slower meanwhile: config S after
@@ -815,6 +817,106 @@ def short_slots_config(ctx, dev, mixed=False) -> dict:
                            "check": "every slot verifies (published by the fused strided kernel)"})
     del bufs, recs, status
     return line
+
+
+def large_slots_config(ctx, dev, nbuf=4) -> dict:
+    """S_large: the reference's own checksum channel shape,
+    LatencyTest.PublisherLatencyPayloadChecksum (client/latency_test.cc:731-745): 32 KiB slots
+    (stride 32,832) carrying payloads of rand() % 32,767 + 1 bytes, checksums on -- 65,536 slots,
+    drained as shuffled device slot lists (max_message_size 32,768) through subspace_crc32_slots,
+    verify and publish, 4 rotated channel copies (8.6 GB). Bytes: span 0 + payload per slot. Read
+    ceiling: the tile-list probe (testutil.hip tile_list_read_kernel) over the same messages' 8 KiB
+    tiles in list order, the ragged kernel's loads without the CRC. Checks: verify passes every
+    slot of a channel published by the other path (subspace_crc32_slots_strided: the arena
+    pipeline); a publish over a copy with checksums and flags cleared leaves 64 sampled slots with
+    the host drop-in's CalculateCRC32Checksum<3> and the flag."""
+    import torch
+    from subspace_amd import checksum, gpu, slots
+    n, area, cs, ms_ = MSGS, 32768, 4, 0
+    ps, stride = slots.compute_prefix_size(cs, ms_), slots.slot_stride(area, cs, ms_)
+    rng = np.random.default_rng(0x5EED0259)
+    sizes = rng.integers(1, area, n).astype(np.uint64)  # rand() % (kMaxPayloadSize - 1) + 1
+    d_sizes = torch.from_numpy(sizes.view(np.int64)).to(dev)
+    d_pre = torch.from_numpy(slots.make_prefixes(n, sizes, checksum_size=cs, metadata_size=ms_, seed=9)).to(dev)
+    d_offs = torch.from_numpy((np.arange(n, dtype=np.uint64) * np.uint64(stride) + np.uint64(ps)).view(np.int64)).to(dev)
+    bufs = []
+    for k in range(nbuf):
+        b = torch.empty(n * stride, dtype=torch.uint8, device=dev)
+        b.view(n, stride)[:, :ps] = d_pre
+        gpu.fill_ragged(b, d_offs, d_sizes, seed=0x5EED0259 + k)
+        ctx.crc32_slots_strided(b, stride, n, sizes=d_sizes, checksum_size=cs, metadata_size=ms_,
+                                mode=gpu.SLOT_CALCULATE)
+        bufs.append(b)
+    order = rng.permutation(n).astype(np.uint64)
+    so = sizes[order.astype(np.int64)]
+    nt = (so + np.uint64(8191)) // np.uint64(8192)
+    recs, tiles = [], []
+    for b in bufs:
+        b0 = np.uint64(b.data_ptr())
+        pay = b0 + order * np.uint64(stride) + np.uint64(ps)
+        r = np.stack([b0 + order * np.uint64(stride), pay, so], axis=1)
+        recs.append(torch.from_numpy(np.ascontiguousarray(r).view(np.int64)).to(dev))
+        first = np.repeat(np.cumsum(nt) - nt, nt.astype(np.int64))
+        t = np.arange(int(nt.sum()), dtype=np.uint64) - first.astype(np.uint64)  # tile index in its message
+        msg_len = np.repeat(so, nt.astype(np.int64))
+        tl = np.stack([np.repeat(pay, nt.astype(np.int64)) + t * np.uint64(8192),
+                       np.minimum(np.uint64(8192), msg_len - t * np.uint64(8192))], axis=1)
+        tiles.append(torch.from_numpy(np.ascontiguousarray(tl).view(np.int64)).to(dev))
+    nbytes = int(sizes.sum()) + 44 * n
+    sink = torch.empty(256 * 512, dtype=torch.int32, device=dev)
+    j = [0]
+
+    def probe():
+        gpu.tile_list_read(tiles[j[0] % nbuf], sink)
+        j[0] += 1
+    pms = time_calls(probe, 100)
+    ceiling = {"GBps": round(nbytes / (pms * 1e-3) / 1e9, 1), "us_per_launch": round(pms * 1e3, 2),
+               "tiles": int(nt.sum()),
+               "kernel": "tile_list_read_kernel (testutil.hip): the ragged kernel's buffer loads over the same "
+                         "messages' 8 KiB tiles in list order, no CRC"}
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    errs = torch.zeros(1, dtype=torch.int32, device=dev)
+    res = {}
+    for mode, key in ((gpu.SLOT_VERIFY, "S_large_verify"), (gpu.SLOT_CALCULATE, "S_large_publish")):
+        i = [0]
+
+        def call():
+            ctx.crc32_slots(recs[i[0] % nbuf], max_message_size=area, checksum_size=cs, metadata_size=ms_, mode=mode,
+                            status=status, error_count=errs if mode == gpu.SLOT_VERIFY else None)
+            i[0] += 1
+        ms = time_calls(call, 100)
+        torch.cuda.synchronize()
+        if mode == gpu.SLOT_VERIFY:
+            ok = int(errs.item()) == 0 and bool((status == 0).all().item())
+            check = "every slot passes (channel published by subspace_crc32_slots_strided)"
+        else:
+            v = bufs[0].view(n, stride)
+            v[:, 48:48 + cs] = 0
+            v[:, 32] &= 0xFB
+            ctx.crc32_slots(recs[0], max_message_size=area, checksum_size=cs, metadata_size=ms_, mode=mode,
+                            status=status)
+            torch.cuda.synchronize()
+            ok = bool((status == 0).all().item())
+            for k in rng.choice(n, 64, replace=False):
+                row = v[int(k)].cpu().numpy()
+                L = int(sizes[k])
+                want = checksum.calculate_crc32_checksum(
+                    checksum.get_message_checksum_data(row[:ps], row[ps:ps + L], L, cs, ms_))
+                ok = ok and bytes(row[48:52]) == want and bool(row[32] & 4)
+            check = "64 sampled slots of copy 0 (flag + checksum cleared before the call) hold the host drop-in's " \
+                    "CalculateCRC32Checksum<3> and the flag"
+        res[key] = config_line(nbytes, ms, ok, "subspace_crc32_slots, max_message_size 32,768: ragged pipeline "
+                               "(absolute addresses) + slot finish", name=key, extra={
+                                   "workload": "S_large: the reference's checksum latency channel "
+                                               "(client/latency_test.cc:731-745): 65,536 slots of 32 KiB (stride "
+                                               "32,832), payloads 1 .. 32,767 B uniformly random, shuffled device slot "
+                                               "lists, 4 copies rotated, " +
+                                               ("verify" if mode == gpu.SLOT_VERIFY else "publish"),
+                                   "slots_per_s": round(n / (ms * 1e-3), 1), "check": check})
+        res[key]["roofline"]["read_ceiling"] = ceiling
+        res[key]["roofline"]["frac_of_read_ceiling"] = round(pms / ms, 4)
+    del bufs, recs, tiles, sink, status
+    return res
 
 
 def slot_leg_check(mode, buf, n, stride, ps, size, cs, ms_, status, errs, rng):
@@ -1219,7 +1321,7 @@ def main():
             return {"error": f"{type(e).__name__}: {e}"[:300]}
 
     configs = None
-    cfg_names = args.configs if args.configs is not None else ("C,Cu,D,Du,S,Usmall,S_short,S_mixed" if args.workload == "B"
+    cfg_names = args.configs if args.configs is not None else ("C,Cu,D,Du,S,Usmall,S_short,S_mixed,S_large" if args.workload == "B"
                                                                else "none")
     if world == 1 and cfg_names != "none":
         configs = optional(lambda: secondary_configs(ctx, dev, [c for c in cfg_names.split(",") if c],

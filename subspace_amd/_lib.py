@@ -135,6 +135,8 @@ def load_dev() -> ctypes.CDLL:
     lib.subspace_crc_testutil_probe_waves.argtypes = [vp, u64]
     lib.subspace_crc_testutil_slot_list_read.restype = i32
     lib.subspace_crc_testutil_slot_list_read.argtypes = [vp, u64, u32, u64, u32, vp, u64, vp]
+    lib.subspace_crc_testutil_tile_list_read.restype = i32
+    lib.subspace_crc_testutil_tile_list_read.argtypes = [vp, u64, vp, u64, vp]
     lib.subspace_crc_testutil_fault_words.restype = i32
     lib.subspace_crc_testutil_fault_words.argtypes = [vp, vp, vp]
     lib.subspace_crc_testutil_call_gen.restype = u32

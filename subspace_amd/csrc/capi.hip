@@ -425,8 +425,10 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
   const bool probe = c->dev.probe && c->dev.small_slot;
   if (probe) g = 32;  // (the dev library's timestamp-recording instantiation is G = 32's)
   const u64 tiles = ceil_div(count, 64ull / g);
-  const unsigned blocks =
-      (unsigned)std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * kSmallRingTiles));
+  // slot waves of the half-tile form take at most kRp2MaxTilesPerWave tiles (32 messages), so a
+  // workgroup's messages fit the workgroup repack's LDS tables (crc_small.hip REPACK2)
+  const u64 per_wave = slot && g == 32 ? kRp2MaxTilesPerWave : kSmallRingTiles;
+  const unsigned blocks = (unsigned)std::max<u64>(grid_for(c, tiles, 8), ceil_div(tiles, 8ull * per_wave));
   const size_t lds = small_lds_bytes() + 16;  // + the mismatch word
   if (slot) {
     a.prefixes = slot->prefixes;

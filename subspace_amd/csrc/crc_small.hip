@@ -381,6 +381,18 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       return v;
     }
   };
+  // Inclusive scan over the wave's 64 lanes (XOR or add): row_shr 1/2/4/8 within rows, then
+  // row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) across them
+  auto wave_scan = [&](u32 x, bool xr) __attribute__((always_inline)) -> u32 {
+    auto op = [&](u32 y) { x = xr ? (x ^ y) : (x + y); };
+    op((u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));  // row_shr:1
+    op((u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));  // row_shr:2
+    op((u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));  // row_shr:4
+    op((u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));  // row_shr:8
+    op((u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    op((u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return x;
+  };
   auto process = [&](const u32x4 (&cur)[8], u64 s, u64 L, u32 k) __attribute__((always_inline)) {
     const u32 mis = (u32)s & 15u;
     const u32 E = ext(k, s, L);
@@ -430,23 +442,37 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32 code = (k < nk && msg_of(k) < count) ? 0u : kCodeSkip;
     if (l == 31u) lds_st64(sring + 8u * (2u * (k & (kSmallRingTiles - 1u)) + h), (u64)v | ((u64)code << 32));
   };
+  auto bperm = [&](u32 e, u32 v) __attribute__((always_inline)) {  // lane e's v
+    return (u32)__builtin_amdgcn_ds_bpermute((int)(e << 2), (int)v);
+  };
   // UNIFORM FAST (no slots; G = 32 too since r05ca: 2-4 KiB messages 14-20 % faster than the
-  // repack loop): a uniform batch of messages of L <= C bytes on 16-B
-  // boundaries -- the tile's address from m * stride, one address and 8 immediate-offset loads
-  // (reading C bytes per message: past L they are the next messages' bytes, masked), one padding
-  // p = C - L for every message, no codes. A tile holding a message whose C bytes would reach
-  // past the batch (the last few) takes the clamped loads instead.
+  // repack loop): a uniform batch of messages of L bytes -- the tile's address from m * stride,
+  // one address and 8 immediate-offset loads per lane (reading C bytes per message from the
+  // 16-B block holding its first byte: past the message they are the next messages' bytes,
+  // masked). A tile holding a message whose C bytes would reach past the batch (the last few)
+  // takes the clamped loads instead. On 16-B strides every message has the padding p = C - L;
+  // on other strides (round 6, VERDICT r05 item 4: packed application buffers) message m starts
+  // mis = (m * stride) & 15 bytes into its first block, so its line 0 masks those bytes and
+  // starts from Z_mis^{-1}(init) (16 seeds, one per lane, picked by ds_bpermute), its lines keep
+  // E = L + mis bytes (keep_sel: the bytes past E are whatever follows, all masked) and its
+  // padding C - E travels with its value to the flush (the general loop's clamped loads, record
+  // arithmetic and per-tile seed inverses ran 200 / 1,000 / 1,500 / 3,000-B packed messages at
+  // 33-43 % of HBM, r05cc).
   const u64 uL = a.ulen;
   const u32 upad = C - (u32)(uL < C ? uL : C);
+  const bool ua = (a.ustride & 15u) == 0;  // every message at offset 0 of its first block
+  u32 useed = 0;  // (!ua) lane l: Z_{l & 15}^{-1}(init)
   // the last message whose C-byte read stays inside the batch (none: -1)
   const int64_t usafe = upad == 0u ? (int64_t)count - 1
                         : a.ustride == 0 ? -1
                                          : (int64_t)count - 1 - (int64_t)((upad + a.ustride - 1) / a.ustride);
-  auto u_off = [&](u32 k) __attribute__((always_inline)) {
+  auto u_msg = [&](u32 k) __attribute__((always_inline)) {
     const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
-    u64 m = msg_of(kk);
-    m = m < count ? m : count - 1;
-    u64 off = m * a.ustride + 128u * li;
+    const u64 m = msg_of(kk);
+    return m < count ? m : count - 1;
+  };
+  auto u_off = [&](u32 k) __attribute__((always_inline)) {
+    u64 off = ((u_msg(k) * a.ustride) & ~(u64)15) + 128u * li;
     asm volatile("" : "+v"(off));
     return off;
   };
@@ -458,24 +484,29 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     if (u_safe(k)) {
       load_at(D, q);
     } else {
-      const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
-      u64 m = msg_of(kk);
-      m = m < count ? m : count - 1;
-      load_lines(D, m * a.ustride, (u32)uL);
+      const u64 so = u_msg(k) * a.ustride;
+      load_lines(D, so, (u32)uL + ((u32)so & 15u));
     }
   };
   auto process_u = [&](const u32x4 (&cur)[8], u32 k) __attribute__((always_inline)) {
     u32x4 d[8];
 #pragma unroll
     for (int b = 0; b < 8; b++) d[b] = cur[b];
-    if (upad != 0u) {  // (uniform) the bytes from L on
-      const int v0 = (int)uL - 128 * (int)li;
-      keep_bytes(d, 0u, v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0));
+    const u32 mis = ua ? 0u : (u32)(msg_of(k) * a.ustride) & 15u;
+    const u32 E = (u32)uL + mis;
+    const int v0 = (int)E - 128 * (int)li;
+    const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
+    u32 seed = a.init;
+    if (ua) {
+      if (upad != 0u) keep_bytes(d, 0u, hi);  // (uniform) the bytes from L on
+    } else {
+      keep_sel(d, li == 0u ? mis : 0u, hi);
+      seed = bperm(mis, useed);
     }
-    const u32 crc = G == 1 && uL <= 64u ? line_crc32_lo(d, a.init, lc0, lc1, z64)
-                                        : line_crc32_2chain(d, li == 0u ? a.init : 0u, lc0, lc1, z64);
+    const u32 crc = G == 1 && __all(E <= 64u) ? line_crc32_lo(d, seed, lc0, lc1, z64)
+                                              : line_crc32_2chain(d, li == 0u ? seed : 0u, lc0, lc1, z64);
     const u32 v = msg_value(crc);
-    const u32 code = (k < nk && msg_of(k) < count) ? 0u : kCodeSkip;
+    const u32 code = (k < nk && msg_of(k) < count) ? C - E : kCodeSkip;
     if (li == (u32)G - 1u) lds_st64(sring + 8u * ((k & (W - 1u)) * M + mj), (u64)v | ((u64)code << 32));
   };
   auto flush_u = [&](u32 kf, u32 nt) __attribute__((always_inline)) {
@@ -483,8 +514,12 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32 hh = (u32)lane % M, ti = (u32)lane / M;
     const u64 e = lds_ld64(sring + 8u * (u32)lane);
     const u64 m = M * (t0 + (u64)(kf + ti) * nw) + hh;
-    const u32 r = upad ? inv_bits((u32)e, upad, kSmallInvOps) : (u32)e;
-    if (ti < nt && (u32)(e >> 32) == 0u) a.out[m] = r ^ a.final_xor;
+    const u32 code = (u32)(e >> 32);
+    const bool live = ti < nt && code != kCodeSkip;
+    // (a batch on 16-B strides has one padding: its bits only)
+    const u32 r = ua ? (upad ? inv_bits((u32)e, upad, kSmallInvOps) : (u32)e)
+                     : inv_bits((u32)e, live ? code : 0u, kSmallInvOps);
+    if (live) a.out[m] = r ^ a.final_xor;
     wave_lds_sync();
   };
   // REPACK (G = 32 kernels): a wave whose window is every tile of the wave (nk <= 32) and not
@@ -504,9 +539,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   u32 rcmax = 0;        // the largest class present
   bool rident = false;  // uniform layout: entry = position >> rcmax (entries with lanes: rmask)
   u64 rmask = 0;
-  auto bperm = [&](u32 e, u32 v) __attribute__((always_inline)) {
-    return (u32)__builtin_amdgcn_ds_bpermute((int)(e << 2), (int)v);
-  };
   // packed tile j, this lane: entry | line in its group << 8 | class << 16 | present << 24
   auto rp_map = [&](u32 j) __attribute__((always_inline)) -> u32 {
     const u32 P = (j << 6) + (u32)lane;
@@ -705,11 +737,39 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // r05z)
   const bool conf = !flive || (wL == (u64)kSmallMaxExt && (wS & 15u) == 0 && (!SLOT || wL <= a.max_len));
   const bool fast = G == 32 && nk <= kSmallRingTiles && __ballot(!conf) == 0;
-  const bool fastu = !SLOT && a.offsets == nullptr && a.ulen != 0 && a.ulen <= (u64)C &&
-                     (a.ustride & 15u) == 0 && ((uintptr_t)base & 15u) == 0;
+  const bool fastu = !SLOT && a.offsets == nullptr && a.ulen != 0 && a.ulen + ((a.ustride & 15u) ? 15u : 0u) <= (u64)C;
   bool repack = false;
   u32 rcode0 = 0;  // (REPACK) this lane's entry's code when it has no lanes, written after tile 0's loads
-  if constexpr (G == 32) {
+  // REPACK2 (slot kernel, G = 32): the workgroup's messages as one stream of lines (grid-uniform:
+  // the host gives no slot wave more than kRp2MaxTilesPerWave tiles, i.e. 32 messages). Lane i of
+  // each wave classifies message i of its window: a code, its extended bytes E and its lines
+  // ceil(E / 128); the wave's line total and its vote (not FAST) go to LDS before the barrier.
+  const bool wg2 = SLOT && G == 32 && ntiles <= (u64)kRp2MaxTilesPerWave * nw;
+  u32 r2n = 0, r2x = 0, r2E = 0, r2code = 0;  // lines, lines of the wave's earlier entries, E, code
+  if constexpr (SLOT && G == 32) {
+    if (wg2) {
+      __builtin_amdgcn_sched_barrier(0);
+      const u64 Ew = wL + (wS & 15u);
+      r2code = !flive                 ? kCodeSkip
+             : wL > a.max_len         ? kCodeOversize
+             : Ew > (u64)kSmallMaxExt ? kCodeLong
+             : wL == 0                ? kCodeEmpty
+                                      : 0u;
+      r2E = r2code ? 0u : (u32)Ew;
+      r2n = (r2E + 127u) >> 7;
+      const u32 incl = wave_scan(r2n, false);
+      r2x = incl - r2n;
+      if (lane == 63) lds_st(sbase + kRp2Misc + 4u * wid, incl);
+      if (lane == 0) {
+        lds_st(sbase + kRp2Misc + 32u + 4u * wid, fast ? 0u : 1u);
+        lds_st(sbase + kRp2Misc + 64u + 4u * wid, (u32)__builtin_popcountll(__ballot(r2n != 0u)));
+      }
+      if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
+      if (threadIdx.x == 0) lds_st(sbase + kRp2Misc + 96u, 0u);  // the tile ticket
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if constexpr (G == 32 && !SLOT) {
     if (__builtin_expect(!fast && !fastu && nk <= kSmallRingTiles, 0)) {
       // (fenced off from the FAST path's prologue; measured neutral, r05bm, kept as validated)
       __builtin_amdgcn_sched_barrier(0);
@@ -800,14 +860,181 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (probe) pt[2] = __builtin_amdgcn_s_memrealtime();
   if constexpr (SLOT && SUBSPACE_SMALL_VARIANT != 1) eH = span_hash(pwords, pmeta, eF, eS, ehas);
+  if (fastu && !ua) useed = inv_bits(a.init, (u32)lane & 15u, 4);  // the 16 head seeds, one per lane
 
+  // REPACK2 after the barrier: a workgroup whose waves are not all FAST packs its messages as one
+  // stream of 128-B lines (message after message, every wave's entries in order; a message's
+  // lines may straddle two packed tiles) and its 8 waves take the packed tiles from an LDS
+  // ticket, so the work of a workgroup is shared whatever its messages' sizes and whichever wave
+  // of a SIMD pair the hardware favours (round 5's per-wave repack: waves' loops ended 24 to 45
+  // us into a 48 us mixed-size drain, tools/small_timeline.py). Each lane of a packed tile holds
+  // line li of a message of n = ceil(E / 128) lines and applies Z_{128 (n-1-li)} to its line CRC;
+  // an inclusive XOR scan over the tile and the scan value before the message's first lane in
+  // the tile give the message's part in this tile, which the part's last lane XORs into the
+  // message's LDS ring entry (two parts when the message straddles tiles). The entry then holds
+  // V = Z_p(crc_raw(init, D)) with p = 128 n - E < 128, one padding for 7 bits at most.
+  bool rp2 = false;
+  u32 r2tiles = 0;  // (PROBE) packed tiles this wave computed
+  if constexpr (SLOT && G == 32) {
+    if (wg2) {
+      const u32x4 va = lds_ld4(sbase + kRp2Misc + 32u), vb = lds_ld4(sbase + kRp2Misc + 48u);
+      rp2 = rfl(va.x | va.y | va.z | va.w | vb.x | vb.y | vb.z | vb.w) != 0u;
+    }
+  }
   // PROBE: tile 0 landed (the first wait of whichever loop form runs; stamped once)
   auto stamp_tile0 = [&]() __attribute__((always_inline)) {
     if constexpr (probe)
       if (pt[3] == 0) pt[3] = __builtin_amdgcn_s_memrealtime();
   };
   u32 k = 0;
-  if (fast) {
+  if (rp2) {
+    if constexpr (SLOT && G == 32) {
+      // the entries: first line in the workgroup's stream, record, code; the packed tiles' start
+      // marks and first entries
+      const u32x4 ta = lds_ld4(sbase + kRp2Misc), tb = lds_ld4(sbase + kRp2Misc + 16u);
+      const u32x4 ca = lds_ld4(sbase + kRp2Misc + 64u), cb = lds_ld4(sbase + kRp2Misc + 80u);
+      const u32 tw[8] = {rfl(ta.x), rfl(ta.y), rfl(ta.z), rfl(ta.w), rfl(tb.x), rfl(tb.y), rfl(tb.z), rfl(tb.w)};
+      const u32 cw[8] = {rfl(ca.x), rfl(ca.y), rfl(ca.z), rfl(ca.w), rfl(cb.x), rfl(cb.y), rfl(cb.z), rfl(cb.w)};
+      u32 wbase = 0, T = 0, rbase = 0, NR = 0;
+#pragma unroll
+      for (u32 w = 0; w < 8; w++) {
+        wbase += w < wid ? tw[w] : 0u;
+        T += tw[w];
+        rbase += w < wid ? cw[w] : 0u;
+        NR += cw[w];
+      }
+      const u32 start = wbase + r2x;
+      // entries with lines are numbered in the same order (rank r): a packed tile's lanes find
+      // theirs by counting the tile's start marks, which only entries with lines have
+      const u32 r = rbase + (u32)__builtin_popcountll(__ballot(r2n != 0u) & ((1ull << lane) - 1ull));
+      if (lane < 32) {
+        const u32 q = 32u * wid + (u32)lane;
+        const u32 code = r2code ? r2code : ((128u * r2n - r2E) | (((u32)wS & 15u) << 12) | (r2n << 16));
+        lds_st64(sbase + kRp2Ring + 8u * q, (u64)code << 32);
+        if (r2n) {
+          lds_st64(sbase + kRp2EntS + 8u * r, wS | ((u64)q << 56));
+          lds_st(sbase + kRp2EntM + 4u * r, r2E | (start << 13));
+          __hip_atomic_fetch_or(reinterpret_cast<lds_u64_t*>((uintptr_t)(sbase + kRp2Starts + 8u * (start >> 6))),
+                                1ull << (start & 63u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const u32 jb = (start + 63u) >> 6;  // the packed tile whose line 0 is in this message, if any
+          if (64u * jb < start + r2n) lds_st(sbase + kRp2First + 4u * jb, r);
+        }
+      }
+      // (every wave's tile-0 lines, issued before the barrier for the FAST loop, land first)
+      drain_before_issue();
+      __syncthreads();
+      const u32 ntl = (T + 63u) >> 6;  // packed tiles of the workgroup
+      const u32 tick = sbase + kRp2Misc + 96u;
+      auto grab = [&]() __attribute__((always_inline)) -> u32 {
+        u32 t = 0;
+        if (lane == 0)
+          t = __hip_atomic_fetch_add(reinterpret_cast<lds_u32_t*>((uintptr_t)tick), 1u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+        return (u32)__builtin_amdgcn_readlane((int)t, 0);
+      };
+      // packed tile j, this lane: its entry, line li, the entry's E (0: no line) and first byte, and
+      // the lane where the entry's part in this tile starts
+      auto map2 = [&](u32 j, u64& ms, u32& mE, u32& mli, u32& me, u32& mst) __attribute__((always_inline)) {
+        const u32 jj = j < ntl ? j : (ntl ? ntl - 1u : 0u);
+        const u64 Sj = lds_ld64(sbase + kRp2Starts + 8u * jj);
+        const u32 fe = lds_ld(sbase + kRp2First + 4u * jj);
+        const u64 below = Sj & ((2ull << lane) - 1ull);
+        u32 e = fe + (u32)__builtin_popcountll(below) - (u32)(Sj & 1ull);
+        e = e < NR ? e : (NR ? NR - 1u : 0u);
+        const u32 m = lds_ld(sbase + kRp2EntM + 4u * e);
+        const u64 sq = lds_ld64(sbase + kRp2EntS + 8u * e);
+        ms = sq & ((1ull << 56) - 1ull);
+        const u32 P = 64u * jj + (u32)lane, st = m >> 13;
+        const bool live = j < ntl && P < T;
+        mE = live ? (m & 0x1FFFu) : 0u;
+        mli = live ? P - st : 0u;
+        me = (u32)(sq >> 56);
+        mst = st > 64u * jj ? st - 64u * jj : 0u;
+      };
+      auto process2 = [&](const u32x4 (&cur)[8], u64 ms, u32 mE, u32 mli, u32 me, u32 mst)
+                          __attribute__((always_inline)) {
+        const u32 mis = (u32)ms & 15u;
+        u32x4 d[8];
+#pragma unroll
+        for (int b = 0; b < 8; b++) d[b] = cur[b];
+        const bool head = mE != 0u && mis != 0u && mli == 0u;
+        const int v0 = (int)mE - 128 * (int)mli;
+        const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
+        if (__any(head || hi < 128u)) keep_sel(d, head ? mis : 0u, hi);
+        u32 seed = a.init;
+        if (seed != 0u && __any(head)) seed = inv_bits(seed, mis, 4);
+        const u32 crc = line_crc32_2chain(d, mli == 0u ? seed : 0u, lc0, lc1, z64);
+        const u32 n = (mE + 127u) >> 7;
+        u32 v = lane_shift(sbase + kLdsOps + 4u * ((n - 1u - mli) & 31u), crc);
+        v = mE ? v : 0u;
+        const u32 P = wave_scan(v, true);
+        const u32 pv = bperm(mst ? mst - 1u : 0u, P);
+        const u32 seg = P ^ (mst ? pv : 0u);
+        if (mE != 0u && (mli == n - 1u || lane == 63))
+          __hip_atomic_fetch_xor(reinterpret_cast<lds_u32_t*>((uintptr_t)(sbase + kRp2Ring + 8u * me)), seg,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      };
+      u64 s_a, s_b;
+      u32 E_a, li_a, e_a, st_a, E_b, li_b, e_b, st_b;
+      u32 ja = ntl ? grab() : 0u;
+      map2(ja, s_a, E_a, li_a, e_a, st_a);
+      load_lines_at(A, s_a, E_a, li_a);
+      while (ja < ntl) {
+        const u32 jb = grab();
+        map2(jb, s_b, E_b, li_b, e_b, st_b);
+        issue_prio_hi();
+        drain_before_issue();
+        stamp_tile0();
+        load_lines_at(B, s_b, E_b, li_b);
+        issue_prio_lo();
+        process2(A, s_a, E_a, li_a, e_a, st_a);
+        r2tiles++;
+        if (jb >= ntl) break;
+        ja = grab();
+        map2(ja, s_a, E_a, li_a, e_a, st_a);
+        issue_prio_hi();
+        drain_before_issue();
+        load_lines_at(A, s_a, E_a, li_a);
+        issue_prio_lo();
+        process2(B, s_b, E_b, li_b, e_b, st_b);
+        r2tiles++;
+      }
+      drain_before_issue();
+      if constexpr (probe) pt[4] = __builtin_amdgcn_s_memrealtime();
+      __syncthreads();  // every part is in the ring
+      // the flush: lane i finishes message i of the wave's window (entry 32 wid + i), as flush_any
+      // with p < 128 and Z_{128 n} for the entry's n lines
+      {
+        const u64 ev = lds_ld64(sbase + kRp2Ring + 8u * (32u * wid + ((u32)lane & 31u)));
+        u32 v = (u32)ev;
+        const u32 code = lane < 32 ? (u32)(ev >> 32) : kCodeSkip;
+        u64 msk = __ballot(code == kCodeLong);
+        while (msk) {  // rare: messages longer than 4 KiB, one at a time by the whole wave
+          const u32 src = (u32)__builtin_ctzll(msk);
+          msk &= msk - 1;
+          const u64 mm = 2u * (t0 + (u64)(src >> 1) * nw) + (src & 1u);
+          u64 ls, lL;
+          record(mm, ls, lL);
+          const u32 r = long_crc(ls, lL, a.prefixes[mm * a.pstride]);
+          v = lane == (int)src ? r : v;
+        }
+        const bool half = code < kCodeOversize, oversize = code == kCodeOversize;
+        const bool live = code != kCodeSkip && !oversize;
+        const u32 n = (code >> 16) & 63u;
+        const u32 Hm = inv_bits(eH, half ? (code >> 12) & 15u : 0u, 4);
+        u32 Z = 0;
+        if (__any(half && n == 32u)) Z = opmul(sbase, kUniSlotOpZ4096, Hm);
+        if (__any(half && n < 32u)) {
+          const u32 Zs = lane_shift(sbase + kLdsOps + 4u * (n & 31u), Hm);
+          Z = n == 32u ? Z : Zs;
+        }
+        // Z_p(crc_raw(H, payload)) = Z_{128 n}(Z_mis^{-1}(H)) ^ V, then Z_p undone (p < 128)
+        const u32 R = half ? inv_bits(Z ^ v, code & 0x7Fu, 7) : (code == kCodeLong ? v : eH);
+        slot_store(live, oversize, fm, flive ? base + fpre - a.pdelta : safe, eF, eS, ehas, R);
+      }
+      if constexpr (probe) pt[5] = __builtin_amdgcn_s_memrealtime();
+    }
+  } else if (fast) {
     // ping-pong, unrolled by two, one tile in flight (crc_uniform.hip's loop)
     for (; k + 1 < nk; k += 2) {
       const u64 qB = fast_off(k + 1);
@@ -928,8 +1155,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       process(A, sc, Lc, k);
     }
   }
-  if constexpr (probe) pt[4] = __builtin_amdgcn_s_memrealtime();
-  if (nk && SUBSPACE_SMALL_VARIANT != 2) {
+  if constexpr (probe)
+    if (!rp2) pt[4] = __builtin_amdgcn_s_memrealtime();
+  if (nk && !rp2 && SUBSPACE_SMALL_VARIANT != 2) {
     if (fast) {
       flush_fast(nk);
     } else if (fastu) {
@@ -940,7 +1168,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       flush(kf, nk - kf);
     }
   }
-  if constexpr (probe) pt[5] = __builtin_amdgcn_s_memrealtime();
+  if constexpr (probe)
+    if (!rp2) pt[5] = __builtin_amdgcn_s_memrealtime();
   if constexpr (SLOT) {
     if (a.error_count && lane == 0) {
       if (calc) {
@@ -972,7 +1201,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u64 xcc = (u64)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
     const u64 v = lane == 0 ? pt[0] : lane == 1 ? pt[1] : lane == 2 ? pt[2] : lane == 3 ? pt[3]
                 : lane == 4 ? pt[4] : lane == 5 ? pt[5] : lane == 6 ? pt[6]
-                : (xcc | ((u64)nk << 32) | ((u64)fast << 48) | ((u64)repack << 49) | ((u64)rnt << 52));
+                : (xcc | ((u64)nk << 32) | ((u64)fast << 48) | ((u64)(repack || rp2) << 49) |
+                   ((u64)(rp2 ? r2tiles : rnt) << 52));
     if (lane < kProbeWords) r[lane] = v;
   }
 }

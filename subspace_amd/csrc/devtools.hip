@@ -150,7 +150,7 @@ uint64_t subspace_crc_testutil_probe_waves(subspace_crc_ctx* c, uint64_t count) 
   // the larger of the uniform kernel's grid and the slot kernels' (more workgroups than CUs
   // when a wave would get more than 32 tiles)
   const u64 tiles = (count + 1) / 2;
-  return std::max<u64>((u64)blocks_for(c, tiles), (tiles + 8ull * kSlotRingRounds - 1) / (8ull * kSlotRingRounds)) * 8u;
+  return std::max<u64>((u64)blocks_for(c, tiles), (tiles + 8ull * kRp2MaxTilesPerWave - 1) / (8ull * kRp2MaxTilesPerWave)) * 8u;
 }
 
 // The uniform 4 KiB kernel over `count` messages that all alias the same 4 KiB at dev_base

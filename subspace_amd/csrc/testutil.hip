@@ -249,9 +249,83 @@ __global__ __launch_bounds__(512) void slot_list_read_kernel(const uint64_t* __r
   out[blockIdx.x * 512 + threadIdx.x] = acc;
 }
 
+// Tile-list read probe (S_large): the ragged kernel's access shape over an
+// explicit list of 8 KiB tiles {16-B-aligned start address, bytes <= 8192} -- the same sweep
+// front (tile tau = k * nw + w), lane l reading line l of its wave's tile as 8 x 16-B buffer
+// loads against a per-tile scalar resource (blocks past the tile's bytes read as zeros without
+// touching memory), one tile in flight per wave -- with the CRC replaced by an XOR fold: the read
+// ceiling of a ragged or slot-list drain of large messages.
+__global__ __launch_bounds__(512) void tile_list_read_kernel(const uint64_t* __restrict__ tiles, uint64_t ntiles,
+                                                             unsigned* __restrict__ out) {
+  using namespace subspace_amd;
+  extern __shared__ unsigned lds_unused3[];
+  const int lane = threadIdx.x & 63;
+  const u64 w = front_slot(blockIdx.x, gridDim.x, rfl(threadIdx.x >> 6));
+  const u64 nw = (u64)gridDim.x * 8;
+  const u64 nk = w < ntiles ? (ntiles - w + nw - 1) / nw : 0;
+  u32 vzero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+  auto desc = [&](u64 k, u64& a, u32& n) {
+    const u64 tau = nk ? (k < nk ? k : nk - 1) * nw + w : 0;
+    const u32x4 d = *reinterpret_cast<const u32x4*>(tiles + 2 * (tau + vzero));
+    a = rfl64(d[0], d[1]);
+    n = k < nk ? ((rfl(d[2]) + 15u) & ~15u) : 0u;
+  };
+  auto load = [&](u32x4 (&L)[8], u64 a, u32 n) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a), (short)0, (int)n, kBufferRsrcFlags);
+#pragma unroll
+    for (int b = 0; b < 8; b++) L[b] = __builtin_amdgcn_raw_buffer_load_b128(r, (u32)lane * 128u + 16u * b, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  unsigned acc = 0;
+  auto fold = [&](const u32x4 (&D)[8]) {
+#pragma unroll
+    for (int b = 0; b < 8; b++) acc ^= D[b].x ^ D[b].y ^ D[b].z ^ D[b].w;
+  };
+  u64 a0, a1;
+  u32 n0, n1;
+  desc(0, a0, n0);
+  u32x4 A[8], B[8];
+  load(A, a0, n0);
+  u64 k = 0;
+  for (; k + 1 < nk; k += 2) {
+    desc(k + 1, a1, n1);
+    drain_before_issue();
+    load(B, a1, n1);
+    fold(A);
+    desc(k + 2, a0, n0);
+    drain_before_issue();
+    load(A, a0, n0);
+    fold(B);
+  }
+  drain_before_issue();
+  if (k < nk) fold(A);
+  if (acc == 0x12345678u && ntiles == 1) lds_unused3[threadIdx.x] = acc;  // (keeps the allocation)
+  out[blockIdx.x * 512 + threadIdx.x] = acc;
+}
+
 }  // namespace
 
 extern "C" {
+
+// The tile-list read probe over `ntiles` records {u64 start (16-B aligned), u64 bytes <= 8192}
+// in device memory, one 512-thread workgroup per CU with the ragged kernel's LDS allocation;
+// dev_out holds num_cus * 512 words.
+int subspace_crc_testutil_tile_list_read(const void* dev_tiles, uint64_t ntiles, unsigned* dev_out,
+                                         uint64_t out_words, void* stream) {
+  if (!dev_tiles || !dev_out || ntiles == 0) return -1;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -2;
+  if (out_words < (uint64_t)cus * 512) return -1;
+  const size_t ldsb = subspace_amd::ragged_lds_bytes();
+  if (hipFuncSetAttribute((const void*)tile_list_read_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsb) !=
+      hipSuccess)
+    return -2;
+  tile_list_read_kernel<<<(unsigned)cus, 512, ldsb, (hipStream_t)stream>>>(static_cast<const uint64_t*>(dev_tiles),
+                                                                             ntiles, dev_out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 
 // The slot-list read probe over `count` device records (MODE above; stride: modes 2 and 3's
 // channel stride; lds: allocate the small-message kernel's dynamic LDS, as it runs); dev_out holds

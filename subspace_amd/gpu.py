@@ -220,6 +220,15 @@ def slot_list_read(records, count: int, out, mode: int = 4, stride: int = 0, lds
         _stream_ptr(stream)), "slot_list_read")
 
 
+def tile_list_read(tiles, out, stream=None) -> None:
+    """Tile-list read ceiling probe (testutil.hip tile_list_read_kernel): the ragged kernel's
+    loads over device records {u64 16-B-aligned start, u64 bytes <= 8192} (int64 tensor of
+    shape (ntiles, 2)), an XOR fold instead of the CRC; out: int32 device tensor of 256 * 512
+    words."""
+    _check(_lib.load_dev().subspace_crc_testutil_tile_list_read(
+        _ptr(tiles), int(tiles.shape[0]), _ptr(out), int(out.numel()), _stream_ptr(stream)), "tile_list_read")
+
+
 def stream_read(buf, out, stream=None) -> None:
     """Streaming-read ceiling probe over buf (the CRC kernels' load shape, no CRC);
     out: int32 device tensor of 256 * 512 words."""

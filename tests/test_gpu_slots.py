@@ -561,3 +561,42 @@ def test_strided_oversize_sizes_are_flagged(gpu_ctx, oracle, slot_size, cs, ms):
     torch.cuda.synchronize()
     st = st.cpu().numpy()
     assert np.array_equal(st == gpu.SLOT_OVERSIZE, big) and (st[~big] == 0).all() and int(err.item()) == 0
+
+
+@pytest.mark.parametrize("mode", ["publish", "verify"])
+def test_large_slot_list_latency_channel_shape(gpu_ctx, oracle, mode):
+    """S_large's shape at a reduced count: the reference's checksum latency
+    channel (client/latency_test.cc:731-745) -- 32 KiB slots, payloads of rand() % 32,767 + 1
+    bytes -- as a shuffled device slot list with max_message_size 32,768 (the ragged pipeline at
+    absolute addresses + the slot finish), publish byte-identical to oracle.publish_slots and
+    verify after bit flips equal to oracle.verify_slots."""
+    count, area, cs, ms = 1500, 32768, 4, 0
+    rng = np.random.default_rng(0x5A1A + (mode == "verify"))
+    sizes = rng.integers(1, area, count).astype(np.uint64)
+    sizes[:4] = [1, 8191, 8192, 32767]
+    host, ps, stride = build_channel(count, area, cs, ms, sizes, seed=0x5A1B)
+    po, yo = offsets(count, stride, ps)
+    if mode == "verify":
+        oracle.publish_slots(host, po, yo, sizes, cs, ms)
+        for i in rng.choice(count, count // 3, replace=False):
+            host[int(yo[i]) + int(rng.integers(0, int(sizes[i])))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    dev = torch.from_numpy(host).to(DEV)
+    order = rng.permutation(count)
+    base = np.uint64(dev.data_ptr())
+    rec = slots.slot_records(base + po[order], base + yo[order], sizes[order])
+    d_rec = torch.from_numpy(rec.view(np.int64)).to(DEV)
+    status = torch.full((count,), 7, dtype=torch.int32, device=DEV)
+    err = torch.full((1,), 12345, dtype=torch.int32, device=DEV)
+    gmode = gpu.SLOT_CALCULATE if mode == "publish" else gpu.SLOT_VERIFY
+    gpu_ctx.crc32_slots(d_rec, max_message_size=area, checksum_size=cs, metadata_size=ms, mode=gmode, status=status,
+                        error_count=err if mode == "verify" else None)
+    torch.cuda.synchronize()
+    got = status.cpu().numpy().view(np.uint32)
+    if mode == "publish":
+        oracle.publish_slots(host, po, yo, sizes, cs, ms)
+        assert (got == 0).all()
+        assert np.array_equal(dev.cpu().numpy(), host)
+    else:
+        want = oracle.verify_slots(host, po[order], yo[order], sizes[order], cs, ms)
+        assert np.array_equal(got, want)
+        assert int(err.item()) == int((want == 1).sum()) > 0

@@ -439,7 +439,8 @@ def test_small_kernel_loads_stay_in_messages(seed, count, G, lanes):
 
 
 def small_kernel_repack_loads(starts, lengths, G):
-    """Replays crc32_small_kernel<512, SLOT, false, 32>'s REPACK loop (crc_small.hip): a wave with
+    """Replays crc32_small_kernel<512, false, false, 32>'s REPACK loop (crc_small.hip; the slot
+    instantiation packs per workgroup instead: small_kernel_repack2 below): a wave with
     at most 32 tiles that is not FAST packs its window's entries (entry e = the record lane e
     loaded: message 2 (t0 + (e / 2) nw) + e % 2) by size: an entry of E = L + (s & 15) in
     [1, 4096] has class c (2^c lanes, the least with 128 2^c >= E); empty, absent and longer
@@ -542,11 +543,134 @@ def test_small_kernel_repack_loads_stay_in_messages(seed, count, G, top):
         assert byts == set(range(int(starts[m]), int(starts[m] + lengths[m]))), m
 
 
+def small_kernel_repack2(starts, lengths, grid, rng):
+    """Replays the slot kernel's REPACK2 (crc32_small_kernel<512, true, false, 32>, crc_small.hip):
+    per workgroup, lane i < 32 of wave w holds message i of its window (entry q = 32 w + i,
+    message 2 (t0 + (i / 2) nw) + i % 2); an entry of E = L + (s & 15) in [1, 4096] has n = ceil(E /
+    128) lines, the entries' lines run back to back in entry order (wave totals, then the wave's
+    exclusive prefix), the entries with lines are numbered r = 0, 1, ... in the same order (their
+    records stored at r, the ring entry q in the offset's top byte), the packed tiles' start
+    marks S_j and first entries (by r) are built as the kernel builds them, and packed tile j's
+    lane i finds its entry as r = first_j + popcount(S_j & (2 << i) - 1) - (S_j & 1). Each line
+    gets a random value; the tile's inclusive
+    XOR scan and the scan value before the entry's first lane in the tile give the part its last
+    lane XORs into the entry's ring word. Yields ('load', message, block address) for every load,
+    ('line', q, li) for every line computed, ('ring', q, got, want) per entry with lines, and
+    ('wgs', repacking workgroups) at the end."""
+    count = len(starts)
+    ntiles = (count + 1) // 2
+    nw = 8 * grid
+    assert ntiles <= 16 * nw
+    wgs = 0
+    for b in range(grid):
+        ents = []  # (q, message or None, E, n)
+        fast_all = True
+        for wid in range(8):
+            t0 = front_slot(b, grid, wid)
+            nk = (ntiles - t0 + nw - 1) // nw if t0 < ntiles else 0
+            for i in range(32):
+                m = 2 * (t0 + (i // 2) * nw) + i % 2
+                live = i // 2 < nk and m < count
+                E = int(lengths[m]) + (int(starts[m]) & 15) if live else 0
+                ok = live and int(lengths[m]) != 0 and E <= 4096
+                if live and not (int(lengths[m]) == 4096 and int(starts[m]) % 16 == 0):
+                    fast_all = False
+                ents.append((32 * wid + i, m if live else None, E if ok else 0, (E + 127) >> 7 if ok else 0))
+        if fast_all:
+            continue
+        wgs += 1
+        start = [int(x) for x in np.concatenate([[0], np.cumsum([n for _, _, _, n in ents])])[:-1]]
+        T = sum(n for _, _, _, n in ents)
+        ntl = (T + 63) >> 6
+        S = [0] * max(ntl, 1)
+        first = [None] * max(ntl, 1)
+        withl = [k for k, (q, m, E, n) in enumerate(ents) if n]  # rank r -> entry index
+        for r, k in enumerate(withl):
+            st, n = start[k], ents[k][3]
+            S[st >> 6] |= 1 << (st & 63)
+            jb = (st + 63) >> 6
+            if 64 * jb < st + n:
+                assert first[jb] is None
+                first[jb] = r
+        val = {(q, li): int(rng.integers(0, 1 << 32)) for (q, m, E, n) in ents for li in range(n)}
+        ring = {q: 0 for (q, m, E, n) in ents}
+        for j in range(ntl):
+            lane_e, lane_v, lane_li, lane_st = [], [], [], []
+            for i in range(64):
+                P = 64 * j + i
+                r = first[j] + bin(S[j] & ((2 << i) - 1)).count("1") - (S[j] & 1)
+                e = withl[min(r, len(withl) - 1)]
+                q, m, E, n = ents[e]
+                st = start[e]
+                live = P < T
+                li = P - st if live else 0
+                if live:
+                    assert 0 <= li < n, (j, i, e, st, n)
+                    yield "line", (b, q), li
+                    s0 = int(starts[m])
+                    lastb = (E - 1) & ~15
+                    for blk in range(8):
+                        yield "load", m, (s0 & ~15) + min(128 * li + 16 * blk, lastb)
+                lane_e.append(e)
+                lane_v.append(val[(q, li)] if live else 0)
+                lane_li.append(li if live else None)
+                lane_st.append(st - 64 * j if st > 64 * j else 0)
+            scan, acc = [], 0
+            for v in lane_v:
+                acc ^= v
+                scan.append(acc)
+            for i in range(64):
+                if lane_li[i] is None:
+                    continue
+                q, m, E, n = ents[lane_e[i]]
+                if lane_li[i] == n - 1 or i == 63:
+                    mst = lane_st[i]
+                    ring[q] ^= scan[i] ^ (scan[mst - 1] if mst else 0)
+        for (q, m, E, n) in ents:
+            if n:
+                want = 0
+                for li in range(n):
+                    want ^= val[(q, li)]
+                yield "ring", q, ring[q], want
+    yield "wgs", wgs, None
+
+
+@pytest.mark.parametrize("seed,count,grid,top", [(40, 1, 1, 64), (41, 511, 2, 4096), (42, 4096, 16, 4096),
+                                                 (43, 4095, 16, 300), (44, 2000, 8, 5000), (45, 999, 4, 4096)])
+def test_small_kernel_repack2_packs_every_line_once(seed, count, grid, top):
+    """REPACK2: every line of every message with lines is computed exactly once, every load
+    holds a byte of its own message and every byte is loaded, and the parts XORed into each
+    entry's ring word (messages straddling packed tiles included) make the XOR of all its lines."""
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(0, top + 1, count)
+    lengths[: min(count, 3)] = [4096, 1, 129][: min(count, 3)]
+    starts = np.cumsum(np.concatenate([[0], lengths[:-1] + rng.integers(0, 40, count - 1)])) + 3
+    starts = starts - (starts & 15) * (rng.random(count) < 0.5)
+    lines, covered, want_cov = {}, {}, {}
+    wgs = 0
+    for kind, a, b, *rest in small_kernel_repack2(starts, lengths, grid, rng):
+        if kind == "wgs":
+            wgs = a
+        elif kind == "line":
+            lines[(a, b)] = lines.get((a, b), 0) + 1
+        elif kind == "load":
+            s, e = int(starts[a]), int(starts[a] + lengths[a])
+            assert b % 16 == 0 and b + 16 > s and b < e, (a, s, e, b)
+            covered.setdefault(a, set()).update(range(max(b, s), min(b + 16, e)))
+        elif kind == "ring":
+            assert b == rest[0], (a, b, rest[0])
+    assert wgs > 0 and all(v == 1 for v in lines.values())
+    for m, cov in covered.items():
+        assert cov == set(range(int(starts[m]), int(starts[m] + lengths[m]))), m
+
+
 def uniform_fast_reads(count, L, stride, G, grid):
-    """Replays crc_small.hip's UNIFORM FAST loads (a uniform batch of L-byte messages, stride
-    16-B aligned, G lanes per message, C = 128 G >= L): for every tile the kernel loads, the byte
-    ranges its lanes read -- [m * stride, m * stride + C) for the tile's messages when the tile's
-    last message is at most usafe (u_safe), else the clamped blocks of [m * stride, + L)."""
+    """Replays crc_small.hip's UNIFORM FAST loads (a uniform batch of L-byte messages, G lanes
+    per message, C = 128 G >= L, + 15 when the stride is not 16-B aligned): for every tile the
+    kernel loads, the byte ranges its lanes read -- [s0, s0 + C) from the 16-B block holding the
+    message's first byte, s0 = (m * stride) & ~15, for the tile's messages when the tile's last
+    message is at most usafe (u_safe), else the clamped blocks of the extended message [s0, m *
+    stride + L)."""
     M, C = 64 // G, 128 * G
     upad = C - min(L, C)
     usafe = count - 1 if upad == 0 else (-1 if stride == 0 else count - 1 - -(-upad // stride))
@@ -563,13 +687,14 @@ def uniform_fast_reads(count, L, stride, G, grid):
                 last = M * (t0 + kk * nw) + M - 1
                 for j in range(M):
                     m = min(M * (t0 + kk * nw) + j, count - 1)
+                    s0 = (m * stride) & ~15
                     if last <= usafe:
-                        yield m * stride, m * stride + C
+                        yield s0, s0 + C
                     else:
-                        lastb = (L - 1) & ~15
+                        lastb = (L + (m * stride & 15) - 1) & ~15
                         for li in range(G):
                             for blk in range(8):
-                                o = m * stride + min(128 * li + 16 * blk, lastb)
+                                o = s0 + min(128 * li + 16 * blk, lastb)
                                 yield o, o + 16
 
 
@@ -577,12 +702,16 @@ def uniform_fast_reads(count, L, stride, G, grid):
                                                    (70, 100, 112, 1, 2), (4097, 2000, 2000, 16, 16),
                                                    (63, 512, 512, 4, 1), (2, 17, 32, 1, 1),
                                                    (3001, 3000, 3008, 32, 12), (65, 4000, 4000, 32, 1),
-                                                   (2, 2100, 2112, 32, 1)])
+                                                   (2, 2100, 2112, 32, 1), (3000, 200, 200, 2, 4),
+                                                   (2000, 1000, 1000, 8, 8), (3001, 1500, 1500, 16, 8),
+                                                   (999, 3000, 3000, 32, 16), (77, 100, 100, 1, 2),
+                                                   (5, 4081, 4081, 32, 1), (1000, 17, 17, 1, 3)])
 def test_uniform_fast_reads_stay_in_the_batch(count, L, stride, G, grid):
     """The packed uniform FAST loop reads past a message's L bytes (into the next messages) but
     never past the batch: every range it reads lies in [0, end) with end the batch's last byte
     rounded up to its 16-B block (the clamped loads' rule: whole 16-B blocks holding message
-    bytes), and the unclamped C-byte reads end within the batch itself."""
+    bytes), and the unclamped C-byte reads end within the batch itself -- for 16-B strides and
+    packed ones (round 6)."""
     end = (count - 1) * stride + L
     end16 = (end + 15) & ~15
     for lo, hi in uniform_fast_reads(count, L, stride, G, grid):

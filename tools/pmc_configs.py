@@ -7,7 +7,8 @@ calls made and writes profiles/traffic_configs.json, which bench.py reads.
 
   python tools/pmc_configs.py <config> [calls]
   config: C, Cu, D, Du, S_publish, S_verify, S_meta_publish, S_meta_verify, S_list_publish,
-          S_list_verify, Usmall, S_short, S_mixed (bench.py's secondary configs, the same shapes and
+          S_list_verify, Usmall, S_short, S_mixed, S_large_verify, S_large_publish (bench.py's
+          secondary configs, the same shapes and
           synthetic data)
 
 Prints one JSON line: the config, the calls made and the algorithmic bytes per call (bench.py's
@@ -89,6 +90,37 @@ def main():
         def fn():
             ctx.crc32_slots(recs[i[0] % 4], max_message_size=area, checksum_size=cs, metadata_size=0,
                             mode=gpu.SLOT_VERIFY, status=status, error_count=errs)
+            i[0] += 1
+        nbytes = int(sizes.sum()) + 44 * n
+    elif name.startswith("S_large"):  # bench.py large_slots_config: 32 KiB slots, 1..32,767-B payloads
+        n, area, cs = 65536, 32768, 4
+        ps, stride = slots.compute_prefix_size(cs, 0), slots.slot_stride(area, cs, 0)
+        rng = np.random.default_rng(0x5EED0259)
+        sizes = rng.integers(1, area, n).astype(np.uint64)
+        d_sizes = torch.from_numpy(sizes.view(np.int64)).to(dev)
+        d_pre = torch.from_numpy(slots.make_prefixes(n, sizes, checksum_size=cs, metadata_size=0, seed=9)).to(dev)
+        d_offs = u64t(np.arange(n, dtype=np.uint64) * np.uint64(stride) + np.uint64(ps))
+        bufs = []
+        for k in range(4):
+            b = torch.empty(n * stride, dtype=torch.uint8, device=dev)
+            b.view(n, stride)[:, :ps] = d_pre
+            gpu.fill_ragged(b, d_offs, d_sizes, seed=0x5EED0259 + k)
+            bufs.append(b)
+        order = rng.permutation(n).astype(np.uint64)
+        recs = []
+        for b in bufs:
+            b0 = np.uint64(b.data_ptr())
+            r = np.stack([b0 + order * np.uint64(stride), b0 + order * np.uint64(stride) + np.uint64(ps),
+                          sizes[order.astype(np.int64)]], axis=1)
+            recs.append(torch.from_numpy(np.ascontiguousarray(r).view(np.int64)).to(dev))
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+        errs = torch.zeros(1, dtype=torch.int32, device=dev)
+        mode = gpu.SLOT_CALCULATE if name.endswith("publish") else gpu.SLOT_VERIFY
+        i = [0]
+
+        def fn():
+            ctx.crc32_slots(recs[i[0] % 4], max_message_size=area, checksum_size=cs, metadata_size=0, mode=mode,
+                            status=status, error_count=errs if mode == gpu.SLOT_VERIFY else None)
             i[0] += 1
         nbytes = int(sizes.sum()) + 44 * n
     else:  # config S's slots (bench.py slot_configs): 65,536 x 4 KiB payloads, 4 rotated copies

@@ -7,7 +7,7 @@
 #   then:  python tools/summarize_configs_traffic.py gpurun_out/<tag>   (-> profiles/traffic_configs.json)
 set -u
 TAG=$1
-CONFIGS=${2:-"C Cu D Du S_publish S_verify S_meta_publish S_meta_verify S_list_publish S_list_verify Usmall S_short S_mixed"}
+CONFIGS=${2:-"C Cu D Du S_publish S_verify S_meta_publish S_meta_verify S_list_publish S_list_verify Usmall S_short S_mixed S_large_verify S_large_publish"}
 ROOT=${GRAFT_REPO_ROOT:-$PWD}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
