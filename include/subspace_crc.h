@@ -150,7 +150,12 @@ typedef struct subspace_crc_slot {
  * one kernel launch (up to 64 messages per 8 KiB tile -- as many 128-B lines per message as
  * the bound needs -- the slot checksums finished in the same kernel); larger bounds take the
  * ragged pipeline. Either way a message larger than the
- * bound is still handled correctly, only more slowly.
+ * bound is still handled correctly, only more slowly. The lines per message are sized for
+ * payloads on 16-B boundaries (every channel layout's payloads are 64-B aligned): with a bound
+ * of at most 2,048 B, a payload starting s & 15 bytes into its 16-B block whose size plus s & 15
+ * exceeds the lines' capacity (the least 128 * 2^k >= max_message_size) is computed on its
+ * own by its wave after the tile loop -- correct, but one such message costs about a tile.
+ * Lists of unaligned payloads close to the bound should pass max_message_size + 15.
  * dev_status: optional uint32[count]. dev_error_count: optional uint32, set to the number
  * of SUBSPACE_CRC_SLOT_MISMATCH slots of this call. */
 int subspace_crc32_slots(subspace_crc_ctx* ctx, const subspace_crc_slot* dev_slots, uint64_t count,

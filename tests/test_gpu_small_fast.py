@@ -98,9 +98,12 @@ def test_fast_past_one_window(gpu_ctx, oracle, lib):
 
 @pytest.mark.parametrize("kind", ["short", "mis", "over"])
 def test_fast_and_general_waves_in_one_launch(gpu_ctx, oracle, lib, kind):
-    """One non-conforming message among 8,191 conforming ones: its wave takes the general loop,
-    the others stay FAST; every slot bit-exact (an oversize one: computed whole, correct)."""
-    publish_verify(gpu_ctx, oracle, 8191, 0xFA59, spoil=[(4000, kind)], lib=lib, general=1)
+    """One non-conforming message among 8,191 conforming ones: its workgroup's 8 waves take the
+    workgroup repack (REPACK2, round 6: the FAST decision is the workgroup's, its waves share the
+    packed tiles), every other workgroup stays FAST; every slot bit-exact (an oversize one:
+    computed whole, correct). 8,191 slots on 256 workgroups: 2 tiles per wave, 8 live waves per
+    workgroup."""
+    publish_verify(gpu_ctx, oracle, 8191, 0xFA59, spoil=[(4000, kind)], lib=lib, general=8)
 
 
 def test_fast_metadata_span(gpu_ctx, oracle, lib):
