@@ -740,12 +740,38 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   const bool fastu = !SLOT && a.offsets == nullptr && a.ulen != 0 && a.ulen + ((a.ustride & 15u) ? 15u : 0u) <= (u64)C;
   bool repack = false;
   u32 rcode0 = 0;  // (REPACK) this lane's entry's code when it has no lanes, written after tile 0's loads
-  // REPACK2 (slot kernel, G = 32): the workgroup's messages as one stream of lines (grid-uniform:
-  // the host gives no slot wave more than kRp2MaxTilesPerWave tiles, i.e. 32 messages). Lane i of
-  // each wave classifies message i of its window: a code, its extended bytes E and its lines
-  // ceil(E / 128); the wave's line total and its vote (not FAST) go to LDS before the barrier.
+  // REPACK2 (slot kernel, G = 32; grid-uniform: the host gives no slot wave more than
+  // kRp2MaxTilesPerWave tiles, i.e. 32 messages). Lane i of each wave classifies message i of its
+  // window: a code, its extended bytes E and its lines ceil(E / 128), laid out back to back in
+  // lane order (r2x: the lines before it). The wave's first 64 lines are its local tile, mapped
+  // and loaded before the barrier (its latency hides behind the LDS fill, as the FAST loop's tile
+  // 0 does); the wave's line total and its vote (not FAST) go to LDS for the workgroup's shared
+  // stream of the remaining lines.
   const bool wg2 = SLOT && G == 32 && ntiles <= (u64)kRp2MaxTilesPerWave * nw;
   u32 r2n = 0, r2x = 0, r2E = 0, r2code = 0;  // lines, lines of the wave's earlier entries, E, code
+  // the local tile, this lane: its entry's lane, line in the entry, E (0: none) and first byte
+  u32 lsrc = 0, lli = 0, lE = 0;
+  u64 ls = 0;
+  auto local_map = [&]() __attribute__((always_inline)) {
+    const u32 slm = sbase + kRp2Misc + 112u + 8u * wid;  // this wave's start marks
+    const bool mk = r2n != 0u && r2x < 64u;
+    if (lane == 0) lds_st64(slm, 0ull);
+    if (mk)
+      __hip_atomic_fetch_or(reinterpret_cast<lds_u64_t*>((uintptr_t)slm), 1ull << r2x, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WORKGROUP);
+    const u64 Sl = lds_ld64(slm);
+    // the entries with local lines by rank -> their lanes (ds_permute: rank k's lane to lane k)
+    const u64 mkb = __ballot(mk);
+    const u32 rk = (u32)__builtin_popcountll(mkb & ((1ull << lane) - 1ull));
+    const u32 r2l = (u32)__builtin_amdgcn_ds_permute((int)((mk ? rk : 32u + ((u32)lane & 31u)) << 2), lane);
+    const u32 tl = (u32)__builtin_amdgcn_readlane((int)(r2x + r2n), 63);  // the wave's lines
+    const u32 k = (u32)__builtin_popcountll(Sl & ((2ull << lane) - 1ull));
+    lsrc = bperm(k ? k - 1u : 0u, r2l) & 31u;
+    ls = ((u64)bperm(lsrc, (u32)(wS >> 32)) << 32) | (u64)bperm(lsrc, (u32)wS);
+    const u32 E = bperm(lsrc, r2E);
+    lli = (u32)lane - bperm(lsrc, r2x);
+    lE = (u32)lane < tl && k ? E : 0u;
+  };
   if constexpr (SLOT && G == 32) {
     if (wg2) {
       __builtin_amdgcn_sched_barrier(0);
@@ -762,10 +788,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       if (lane == 63) lds_st(sbase + kRp2Misc + 4u * wid, incl);
       if (lane == 0) {
         lds_st(sbase + kRp2Misc + 32u + 4u * wid, fast ? 0u : 1u);
-        lds_st(sbase + kRp2Misc + 64u + 4u * wid, (u32)__builtin_popcountll(__ballot(r2n != 0u)));
+        lds_st(sbase + kRp2Misc + 64u + 4u * wid, (u32)__builtin_popcountll(__ballot(r2n != 0u && r2x + r2n > 64u)));
       }
       if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
       if (threadIdx.x == 0) lds_st(sbase + kRp2Misc + 96u, 0u);  // the tile ticket
+      if (!fast) local_map();  // (a FAST wave's local tile is its FAST tile 0: same lanes, same loads)
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -850,6 +877,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     rp_rec(pc, sc, Lc);
     load_lines_at(A, sc, rp_ext(sc, Lc, pc), (pc >> 8) & 31u);
     if (rcode0) lds_st64(sring + 8u * (u32)lane, (u64)rcode0 << 32);
+  } else if (wg2 && !fast) {
+    load_lines_at(A, ls, lE, lli);  // REPACK2: the wave's local tile
   } else {
     load_lines(A, sc, ext(0, sc, Lc));  // (FAST: the same addresses as load_at's)
   }
@@ -889,8 +918,10 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   u32 k = 0;
   if (rp2) {
     if constexpr (SLOT && G == 32) {
-      // the entries: first line in the workgroup's stream, record, code; the packed tiles' start
-      // marks and first entries
+      // the shared stream: every wave's lines past its local tile, wave after wave; an entry's
+      // shared part (its lines from local position 64 on) gets a rank among the entries with one,
+      // its record, its first shared position and the line it starts with; the shared tiles'
+      // start marks and first entries (by rank)
       const u32x4 ta = lds_ld4(sbase + kRp2Misc), tb = lds_ld4(sbase + kRp2Misc + 16u);
       const u32x4 ca = lds_ld4(sbase + kRp2Misc + 64u), cb = lds_ld4(sbase + kRp2Misc + 80u);
       const u32 tw[8] = {rfl(ta.x), rfl(ta.y), rfl(ta.z), rfl(ta.w), rfl(tb.x), rfl(tb.y), rfl(tb.z), rfl(tb.w)};
@@ -898,59 +929,29 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       u32 wbase = 0, T = 0, rbase = 0, NR = 0;
 #pragma unroll
       for (u32 w = 0; w < 8; w++) {
-        wbase += w < wid ? tw[w] : 0u;
-        T += tw[w];
+        const u32 sh = tw[w] > 64u ? tw[w] - 64u : 0u;
+        wbase += w < wid ? sh : 0u;
+        T += sh;
         rbase += w < wid ? cw[w] : 0u;
         NR += cw[w];
       }
-      const u32 start = wbase + r2x;
-      // entries with lines are numbered in the same order (rank r): a packed tile's lanes find
-      // theirs by counting the tile's start marks, which only entries with lines have
-      const u32 r = rbase + (u32)__builtin_popcountll(__ballot(r2n != 0u) & ((1ull << lane) - 1ull));
+      const u32 a0 = r2x > 64u ? r2x : 64u;  // the entry's first local position in the shared stream
+      const u32 shn = r2x + r2n > 64u ? r2x + r2n - a0 : 0u;
+      const u32 start = wbase + a0 - 64u;
+      const u32 r = rbase + (u32)__builtin_popcountll(__ballot(shn != 0u) & ((1ull << lane) - 1ull));
       if (lane < 32) {
         const u32 q = 32u * wid + (u32)lane;
         const u32 code = r2code ? r2code : ((128u * r2n - r2E) | (((u32)wS & 15u) << 12) | (r2n << 16));
         lds_st64(sbase + kRp2Ring + 8u * q, (u64)code << 32);
-        if (r2n) {
+        if (shn) {
           lds_st64(sbase + kRp2EntS + 8u * r, wS | ((u64)q << 56));
-          lds_st(sbase + kRp2EntM + 4u * r, r2E | (start << 13));
+          lds_st(sbase + kRp2EntM + 4u * r, r2E | (start << 13) | ((a0 - r2x) << 26));
           __hip_atomic_fetch_or(reinterpret_cast<lds_u64_t*>((uintptr_t)(sbase + kRp2Starts + 8u * (start >> 6))),
                                 1ull << (start & 63u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          const u32 jb = (start + 63u) >> 6;  // the packed tile whose line 0 is in this message, if any
-          if (64u * jb < start + r2n) lds_st(sbase + kRp2First + 4u * jb, r);
+          const u32 jb = (start + 63u) >> 6;  // the shared tile whose line 0 is in this part, if any
+          if (64u * jb < start + shn) lds_st(sbase + kRp2First + 4u * jb, r);
         }
       }
-      // (every wave's tile-0 lines, issued before the barrier for the FAST loop, land first)
-      drain_before_issue();
-      __syncthreads();
-      const u32 ntl = (T + 63u) >> 6;  // packed tiles of the workgroup
-      const u32 tick = sbase + kRp2Misc + 96u;
-      auto grab = [&]() __attribute__((always_inline)) -> u32 {
-        u32 t = 0;
-        if (lane == 0)
-          t = __hip_atomic_fetch_add(reinterpret_cast<lds_u32_t*>((uintptr_t)tick), 1u, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-        return (u32)__builtin_amdgcn_readlane((int)t, 0);
-      };
-      // packed tile j, this lane: its entry, line li, the entry's E (0: no line) and first byte, and
-      // the lane where the entry's part in this tile starts
-      auto map2 = [&](u32 j, u64& ms, u32& mE, u32& mli, u32& me, u32& mst) __attribute__((always_inline)) {
-        const u32 jj = j < ntl ? j : (ntl ? ntl - 1u : 0u);
-        const u64 Sj = lds_ld64(sbase + kRp2Starts + 8u * jj);
-        const u32 fe = lds_ld(sbase + kRp2First + 4u * jj);
-        const u64 below = Sj & ((2ull << lane) - 1ull);
-        u32 e = fe + (u32)__builtin_popcountll(below) - (u32)(Sj & 1ull);
-        e = e < NR ? e : (NR ? NR - 1u : 0u);
-        const u32 m = lds_ld(sbase + kRp2EntM + 4u * e);
-        const u64 sq = lds_ld64(sbase + kRp2EntS + 8u * e);
-        ms = sq & ((1ull << 56) - 1ull);
-        const u32 P = 64u * jj + (u32)lane, st = m >> 13;
-        const bool live = j < ntl && P < T;
-        mE = live ? (m & 0x1FFFu) : 0u;
-        mli = live ? P - st : 0u;
-        me = (u32)(sq >> 56);
-        mst = st > 64u * jj ? st - 64u * jj : 0u;
-      };
       auto process2 = [&](const u32x4 (&cur)[8], u64 ms, u32 mE, u32 mli, u32 me, u32 mst)
                           __attribute__((always_inline)) {
         const u32 mis = (u32)ms & 15u;
@@ -974,34 +975,74 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
           __hip_atomic_fetch_xor(reinterpret_cast<lds_u32_t*>((uintptr_t)(sbase + kRp2Ring + 8u * me)), seg,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       };
-      u64 s_a, s_b;
-      u32 E_a, li_a, e_a, st_a, E_b, li_b, e_b, st_b;
-      u32 ja = ntl ? grab() : 0u;
-      map2(ja, s_a, E_a, li_a, e_a, st_a);
-      load_lines_at(A, s_a, E_a, li_a);
-      while (ja < ntl) {
-        const u32 jb = grab();
-        map2(jb, s_b, E_b, li_b, e_b, st_b);
-        issue_prio_hi();
-        drain_before_issue();
-        stamp_tile0();
-        load_lines_at(B, s_b, E_b, li_b);
-        issue_prio_lo();
-        process2(A, s_a, E_a, li_a, e_a, st_a);
-        r2tiles++;
-        if (jb >= ntl) break;
-        ja = grab();
+      // the local tile (loaded before the barrier; a FAST wave's is its FAST tile 0, mapped here)
+      if (fast) local_map();
+      drain_before_issue();
+      stamp_tile0();
+      process2(A, ls, lE, lli, 32u * wid + lsrc, bperm(lsrc, r2x));
+      r2tiles++;
+      const u32 ntl = (T + 63u) >> 6;  // shared tiles of the workgroup
+      if (ntl) {
+        __syncthreads();  // the shared tables
+        const u32 tick = sbase + kRp2Misc + 96u;
+        auto grab = [&]() __attribute__((always_inline)) -> u32 {
+          u32 t = 0;
+          if (lane == 0)
+            t = __hip_atomic_fetch_add(reinterpret_cast<lds_u32_t*>((uintptr_t)tick), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+          return (u32)__builtin_amdgcn_readlane((int)t, 0);
+        };
+        // shared tile j, this lane: its entry's record and ring entry, its line, the entry's E (0: no
+        // line), and the lane where the entry's part in this tile starts
+        auto map2 = [&](u32 j, u64& ms, u32& mE, u32& mli, u32& me, u32& mst) __attribute__((always_inline)) {
+          const u32 jj = j < ntl ? j : ntl - 1u;
+          const u64 Sj = lds_ld64(sbase + kRp2Starts + 8u * jj);
+          const u32 fe = lds_ld(sbase + kRp2First + 4u * jj);
+          const u64 below = Sj & ((2ull << lane) - 1ull);
+          u32 e = fe + (u32)__builtin_popcountll(below) - (u32)(Sj & 1ull);
+          e = e < NR ? e : NR - 1u;
+          const u32 m = lds_ld(sbase + kRp2EntM + 4u * e);
+          const u64 sq = lds_ld64(sbase + kRp2EntS + 8u * e);
+          ms = sq & ((1ull << 56) - 1ull);
+          const u32 P = 64u * jj + (u32)lane, st = (m >> 13) & 0x1FFFu;
+          const bool live = j < ntl && P < T;
+          mE = live ? (m & 0x1FFFu) : 0u;
+          mli = live ? P - st + (m >> 26) : 0u;
+          me = (u32)(sq >> 56);
+          mst = st > 64u * jj ? st - 64u * jj : 0u;
+        };
+        u64 s_a, s_b;
+        u32 E_a, li_a, e_a, st_a, E_b, li_b, e_b, st_b;
+        u32 ja = grab();
         map2(ja, s_a, E_a, li_a, e_a, st_a);
-        issue_prio_hi();
-        drain_before_issue();
         load_lines_at(A, s_a, E_a, li_a);
-        issue_prio_lo();
-        process2(B, s_b, E_b, li_b, e_b, st_b);
-        r2tiles++;
+        while (ja < ntl) {
+          const u32 jb = grab();
+          map2(jb, s_b, E_b, li_b, e_b, st_b);
+          issue_prio_hi();
+          drain_before_issue();
+          load_lines_at(B, s_b, E_b, li_b);
+          issue_prio_lo();
+          process2(A, s_a, E_a, li_a, e_a, st_a);
+          r2tiles++;
+          if (jb >= ntl) break;
+          ja = grab();
+          map2(ja, s_a, E_a, li_a, e_a, st_a);
+          issue_prio_hi();
+          drain_before_issue();
+          load_lines_at(A, s_a, E_a, li_a);
+          issue_prio_lo();
+          process2(B, s_b, E_b, li_b, e_b, st_b);
+          r2tiles++;
+        }
       }
       drain_before_issue();
       if constexpr (probe) pt[4] = __builtin_amdgcn_s_memrealtime();
-      __syncthreads();  // every part is in the ring
+      // every part is in the ring (without a shared stream every entry is its own wave's alone)
+      if (ntl)
+        __syncthreads();
+      else
+        wave_lds_sync();
       // the flush: lane i finishes message i of the wave's window (entry 32 wid + i), as flush_any
       // with p < 128 and Z_{128 n} for the entry's n lines
       {

@@ -547,27 +547,30 @@ def small_kernel_repack2(starts, lengths, grid, rng):
     """Replays the slot kernel's REPACK2 (crc32_small_kernel<512, true, false, 32>, crc_small.hip):
     per workgroup, lane i < 32 of wave w holds message i of its window (entry q = 32 w + i,
     message 2 (t0 + (i / 2) nw) + i % 2); an entry of E = L + (s & 15) in [1, 4096] has n = ceil(E /
-    128) lines, the entries' lines run back to back in entry order (wave totals, then the wave's
-    exclusive prefix), the entries with lines are numbered r = 0, 1, ... in the same order (their
-    records stored at r, the ring entry q in the offset's top byte), the packed tiles' start
-    marks S_j and first entries (by r) are built as the kernel builds them, and packed tile j's
-    lane i finds its entry as r = first_j + popcount(S_j & (2 << i) - 1) - (S_j & 1). Each line
-    gets a random value; the tile's inclusive
-    XOR scan and the scan value before the entry's first lane in the tile give the part its last
-    lane XORs into the entry's ring word. Yields ('load', message, block address) for every load,
-    ('line', q, li) for every line computed, ('ring', q, got, want) per entry with lines, and
-    ('wgs', repacking workgroups) at the end."""
+    128) lines, laid out back to back in lane order (r2x: the wave's lines before it). The wave's
+    first 64 lines are its local tile: lane P's entry is the entry of rank k - 1, k = popcount(local
+    start marks & (2 << P) - 1), ranks mapped to lanes as the kernel's ds_permute does. The other
+    lines of every wave form the shared stream (wave after wave); entries with shared lines are
+    ranked r = 0, 1, ... in the same order (record at r, ring entry in the offset's top byte,
+    first shared position and first line), the shared tiles' start marks S_j and first entries
+    (by rank) built as the kernel builds them, and shared tile j's lane i finds its entry as r =
+    first_j + popcount(S_j & (2 << i) - 1) - (S_j & 1). Each line gets a random value; every tile's
+    inclusive XOR scan and the scan value before the entry's first lane in the tile give the part
+    its last lane XORs into the entry's ring word. Yields ('load', message, block address) for
+    every load, ('line', (workgroup, q), li) for every line computed, ('ring', q, got, want) per
+    entry with lines, and ('wgs', repacking workgroups) at the end."""
     count = len(starts)
     ntiles = (count + 1) // 2
     nw = 8 * grid
     assert ntiles <= 16 * nw
     wgs = 0
     for b in range(grid):
-        ents = []  # (q, message or None, E, n)
+        waves = []  # per wave: [(q, message or None, E, n)] for lanes 0..31
         fast_all = True
         for wid in range(8):
             t0 = front_slot(b, grid, wid)
             nk = (ntiles - t0 + nw - 1) // nw if t0 < ntiles else 0
+            ents = []
             for i in range(32):
                 m = 2 * (t0 + (i // 2) * nw) + i % 2
                 live = i // 2 < nk and m < count
@@ -576,62 +579,85 @@ def small_kernel_repack2(starts, lengths, grid, rng):
                 if live and not (int(lengths[m]) == 4096 and int(starts[m]) % 16 == 0):
                     fast_all = False
                 ents.append((32 * wid + i, m if live else None, E if ok else 0, (E + 127) >> 7 if ok else 0))
+            waves.append(ents)
         if fast_all:
             continue
         wgs += 1
-        start = [int(x) for x in np.concatenate([[0], np.cumsum([n for _, _, _, n in ents])])[:-1]]
-        T = sum(n for _, _, _, n in ents)
+        vals, ring = {}, {}
+        for ents in waves:
+            for q, m, E, n in ents:
+                ring[q] = 0
+                for li in range(n):
+                    vals[(q, li)] = int(rng.integers(0, 1 << 32))
+        tiles = []  # (lane -> (q, m, E, n, li, first lane of the entry's part in the tile)) per tile
+
+        def emit(lanes):
+            tiles.append(lanes)
+        # local tiles
+        shared = []  # (q, m, E, n, first shared line) in stream order
+        for ents in waves:
+            r2x = [int(x) for x in np.concatenate([[0], np.cumsum([n for *_, n in ents])])[:-1]]
+            tot = sum(n for *_, n in ents)
+            marks = [r2x[i] for i in range(32) if ents[i][3] and r2x[i] < 64]
+            withl = [i for i in range(32) if ents[i][3] and r2x[i] < 64]  # rank -> lane
+            lanes = {}
+            for P in range(min(tot, 64)):
+                k = sum(1 for x in marks if x <= P)
+                i = withl[k - 1]
+                q, m, E, n = ents[i]
+                lanes[P] = (q, m, E, n, P - r2x[i], r2x[i])
+            emit(lanes)
+            for i in range(32):
+                q, m, E, n = ents[i]
+                if n and r2x[i] + n > 64:
+                    a0 = max(r2x[i], 64)
+                    shared.append((q, m, E, n, a0 - r2x[i], r2x[i] + n - a0))
+        # shared stream
+        start = [int(x) for x in np.concatenate([[0], np.cumsum([c for *_, c in shared])])[:-1]]
+        T = sum(c for *_, c in shared)
         ntl = (T + 63) >> 6
         S = [0] * max(ntl, 1)
         first = [None] * max(ntl, 1)
-        withl = [k for k, (q, m, E, n) in enumerate(ents) if n]  # rank r -> entry index
-        for r, k in enumerate(withl):
-            st, n = start[k], ents[k][3]
+        for r, ((q, m, E, n, li0, c), st) in enumerate(zip(shared, start)):
             S[st >> 6] |= 1 << (st & 63)
             jb = (st + 63) >> 6
-            if 64 * jb < st + n:
+            if 64 * jb < st + c:
                 assert first[jb] is None
                 first[jb] = r
-        val = {(q, li): int(rng.integers(0, 1 << 32)) for (q, m, E, n) in ents for li in range(n)}
-        ring = {q: 0 for (q, m, E, n) in ents}
         for j in range(ntl):
-            lane_e, lane_v, lane_li, lane_st = [], [], [], []
+            lanes = {}
             for i in range(64):
                 P = 64 * j + i
+                if P >= T:
+                    continue
                 r = first[j] + bin(S[j] & ((2 << i) - 1)).count("1") - (S[j] & 1)
-                e = withl[min(r, len(withl) - 1)]
-                q, m, E, n = ents[e]
-                st = start[e]
-                live = P < T
-                li = P - st if live else 0
-                if live:
-                    assert 0 <= li < n, (j, i, e, st, n)
+                q, m, E, n, li0, c = shared[min(r, len(shared) - 1)]
+                st = start[r]
+                lanes[i] = (q, m, E, n, P - st + li0, st - 64 * j if st > 64 * j else 0)
+            emit(lanes)
+        for lanes in tiles:
+            scan, acc = [], 0
+            for i in range(64):
+                if i in lanes:
+                    q, m, E, n, li, mst = lanes[i]
+                    assert 0 <= li < n, (q, li, n)
                     yield "line", (b, q), li
                     s0 = int(starts[m])
                     lastb = (E - 1) & ~15
                     for blk in range(8):
                         yield "load", m, (s0 & ~15) + min(128 * li + 16 * blk, lastb)
-                lane_e.append(e)
-                lane_v.append(val[(q, li)] if live else 0)
-                lane_li.append(li if live else None)
-                lane_st.append(st - 64 * j if st > 64 * j else 0)
-            scan, acc = [], 0
-            for v in lane_v:
-                acc ^= v
+                    acc ^= vals[(q, li)]
                 scan.append(acc)
-            for i in range(64):
-                if lane_li[i] is None:
-                    continue
-                q, m, E, n = ents[lane_e[i]]
-                if lane_li[i] == n - 1 or i == 63:
-                    mst = lane_st[i]
+            for i, (q, m, E, n, li, mst) in lanes.items():
+                if li == n - 1 or i == 63:
                     ring[q] ^= scan[i] ^ (scan[mst - 1] if mst else 0)
-        for (q, m, E, n) in ents:
-            if n:
-                want = 0
-                for li in range(n):
-                    want ^= val[(q, li)]
-                yield "ring", q, ring[q], want
+        for ents in waves:
+            for q, m, E, n in ents:
+                if n:
+                    want = 0
+                    for li in range(n):
+                        want ^= vals[(q, li)]
+                    yield "ring", q, ring[q], want
     yield "wgs", wgs, None
 
 

@@ -24,20 +24,23 @@ case ",$STEPS," in *,test,*)
     tests/test_gpu_probe.py tests/test_gpu_parity.py > "$OUT/test.log" 2>&1
   stop $? test ;;
 esac
+ROUNDS=${ROUNDS:-1 2}
+RAND=${RAND:-4096,3000,2048,1024,256}
+FIXED=${FIXED:-3000,1024,256,64}
 case ",$STEPS," in *,sizes,*)
-  for r in 1 2; do
+  for r in $ROUNDS; do
     for v in "$@"; do
-      SUBSPACE_CRC_PROBE_LIB=$(libpath "$v") timeout -k 10 300 python tools/small_sizes.py 4096,3000,2048,1024,256 \
+      SUBSPACE_CRC_PROBE_LIB=$(libpath "$v") timeout -k 10 300 python tools/small_sizes.py $RAND \
         200 200 slots4k_rand > "$OUT/rand${r}_$(stem "$v").jsonl" 2> "$OUT/rand${r}_$(stem "$v").err"
       stop $? "rand_r${r}_$(stem "$v")"
-      SUBSPACE_CRC_PROBE_LIB=$(libpath "$v") timeout -k 10 300 python tools/small_sizes.py 3000,1024,256,64 \
+      SUBSPACE_CRC_PROBE_LIB=$(libpath "$v") timeout -k 10 300 python tools/small_sizes.py $FIXED \
         200 200 slots4k > "$OUT/fixed${r}_$(stem "$v").jsonl" 2> "$OUT/fixed${r}_$(stem "$v").err"
       stop $? "fixed_r${r}_$(stem "$v")"
     done
   done ;;
 esac
 case ",$STEPS," in *,uni,*)
-  for r in 1 2; do
+  for r in $ROUNDS; do
     for v in "$@"; do
       SUBSPACE_CRC_PROBE_LIB=$(libpath "$v") timeout -k 10 300 python tools/small_sizes.py 200,1000,1500,3000,100 \
         200 200 uniform_packed > "$OUT/upk${r}_$(stem "$v").jsonl" 2> "$OUT/upk${r}_$(stem "$v").err"
@@ -49,7 +52,7 @@ case ",$STEPS," in *,uni,*)
   done ;;
 esac
 case ",$STEPS," in *,list,*)
-  for r in 1 2; do
+  for r in $ROUNDS; do
     for v in "$@"; do
       SUBSPACE_CRC_PROBE_LIB=$(libpath "$v") timeout -k 10 200 python tools/ledger_small.py list,ordered 400 400 2 \
         > "$OUT/list${r}_$(stem "$v").jsonl" 2> "$OUT/list${r}_$(stem "$v").err"
