@@ -172,7 +172,7 @@ int fault_status(subspace_crc_ctx* c, hipStream_t st) {
     // (ADVICE r03), then report everything raised
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(&f, c->d_fault, sizeof(u32), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemset(c->d_slot_counter, 0, kSlotCounters * sizeof(u64)));
+    HIP_TRY(hipMemset(c->d_slot_counter, 0, kSlotCounters * kCountWords * sizeof(u64)));
     HIP_TRY(hipDeviceSynchronize());
   }
   // a scan fault: the scan kernels of this context run on the workspace stream, which st
@@ -441,7 +441,7 @@ int small_run(subspace_crc_ctx* c, const uint8_t* base, const u64* offsets, u32 
     a.status = slot->status;
     a.crc_out = slot->crc_out;
     a.error_count = slot->error_count;
-    a.counter = c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters);
+    a.counter = c->d_slot_counter + kCountWords * (c->slot_counter_next++ % kSlotCounters);
     if (probe) {  // development hook (libsubspace_crc_dev.so: tools/small_timeline.py)
       HIP_TRY(c->dev.small_slot(blocks, lds, st, c->d_tab, c->d_laneops, a));
     } else {
@@ -615,8 +615,8 @@ int subspace_crc_ctx_create_poly(int device, uint32_t poly, subspace_crc_ctx** o
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)crc32_uniform4k_kernel<512, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)uniform_slot_lds_bytes(8));
-  if (e == hipSuccess) e = hipMalloc(&c->d_slot_counter, kSlotCounters * sizeof(u64));
-  if (e == hipSuccess) e = hipMemset(c->d_slot_counter, 0, kSlotCounters * sizeof(u64));
+  if (e == hipSuccess) e = hipMalloc(&c->d_slot_counter, kSlotCounters * kCountWords * sizeof(u64));
+  if (e == hipSuccess) e = hipMemset(c->d_slot_counter, 0, kSlotCounters * kCountWords * sizeof(u64));
   if (e == hipSuccess) e = hipMalloc(&c->d_fault, 4 * sizeof(u32));
   if (e == hipSuccess) e = hipMemset(c->d_fault, 0, 4 * sizeof(u32));
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ws_done, hipEventDisableTiming);
@@ -908,7 +908,7 @@ int slots_strided_impl(subspace_crc_ctx* c, void* dev_buffer, uint64_t slot_stri
     const u64 tiles = (count + 1) / 2;
     const u64 blocks = std::max<u64>(grid_for(c, tiles, 512 / 64), ceil_div(tiles, 8ull * kSlotRingRounds));
     SlotArgs sa{prefix_size, mode, dev_status, dev_crc_out, dev_error_count,
-                c->d_slot_counter + (c->slot_counter_next++ % kSlotCounters), c->dev.probe, c->d_fault,
+                c->d_slot_counter + kCountWords * (c->slot_counter_next++ % kSlotCounters), c->dev.probe, c->d_fault,
                 (u32)checksum_size, (u32)metadata_size};
     if (c->dev.probe && c->dev.uniform)  // development hook (libsubspace_crc_dev.so)
       HIP_TRY(c->dev.uniform(true, (unsigned)blocks, st, buf + prefix_size, slot_stride, count, c->d_tab, c->d_laneops,

@@ -67,7 +67,7 @@ struct SlotArgs {
   u32* status;         // optional, per slot
   u32* crc_out;        // optional (CALCULATE): stored checksum per slot
   u32* error_count;    // optional (VERIFY): mismatches of this call
-  u64* counter;        // context word: (workgroups done << 32) | mismatches so far; 0 between calls
+  u64* counter;        // context counter entry (kCountWords words, add_call_mismatches); 0 between calls
   u64* probe;          // PROBE instantiation only: per-wave timestamps (tools/wave_timeline.py)
   u32* fault;          // context fault word (kFault* bits), read by subspace_crc_ctx_check
   u32 checksum_size;   // span 1 = prefix[48 + checksum_size, + metadata_size) (common/channel.h:527-542)
@@ -196,7 +196,7 @@ struct SmallArgs {
   u32* status;       // SLOT, optional: per-slot status
   u32* crc_out;      // SLOT, optional: the stored checksum (CALCULATE)
   u32* error_count;  // SLOT, optional: this call's mismatches (0 for CALCULATE)
-  u64* counter;      // SLOT: context word, (workgroups done << 32) | mismatches; 0 between calls
+  u64* counter;      // SLOT: context counter entry (kCountWords words, add_call_mismatches); 0 between calls
   u32* zero_word;    // !SLOT, optional: zeroed at the end (the next kernel's mismatch count)
   const u32* rops;   // the ragged operator array (Z_8192; Z_4096^{-1}, the 13th padding inverse)
   const u32* pow2;   // SLOT: Z_{2^k}, k < 64 (a long message's Z_L)
@@ -531,6 +531,32 @@ __device__ __forceinline__ void reset_scan_state(u64* status, u64 nwords, u32* t
   const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x, stride = (u64)gridDim.x * blockDim.x;
   for (u64 i = g; i < nwords; i += stride) __hip_atomic_store(&status[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (g == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A slot call's mismatch count over its workgroups, without a memset and without one hot word:
+// the call's entry of the context's counter ring holds a top word and kCountGroups group words
+// (u64, all 0 between calls). Workgroup b adds (1 << 32) | n to group word b % kCountGroups; the
+// workgroup that finds the rest of its group done adds the group's total to the top word and
+// resets its group word; the one that finds every other group done writes the call's total and
+// resets the top word. (One word for all workgroups serialised their 256 atomics at the end of
+// a short drain: the last workgroup of a 65,536-slot S_short call exited ~2.5 us after the
+// median, tools/small_timeline.py, round 6.)
+constexpr u32 kCountGroups = 8;
+constexpr u32 kCountWords = 16;  // per call entry: one 128-B line
+__device__ __forceinline__ void add_call_mismatches(u64* counter, u32 n, u32* error_count) {
+  const u32 G = gridDim.x, g = blockIdx.x % kCountGroups;
+  const u32 ng = (G - g + kCountGroups - 1u) / kCountGroups;  // workgroups of group g
+  const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(counter + 1 + g), (1ull << 32) | (u64)n);
+  if ((u32)(old >> 32) == ng - 1u) {
+    const u32 tot = (u32)old + n;
+    __hip_atomic_store(counter + 1 + g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u32 groups = G < kCountGroups ? G : kCountGroups;
+    const u64 o2 = atomicAdd(reinterpret_cast<unsigned long long*>(counter), (1ull << 32) | (u64)tot);
+    if ((u32)(o2 >> 32) == groups - 1u) {
+      *error_count = (u32)o2 + tot;
+      __hip_atomic_store(counter, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 __device__ __forceinline__ void wave_lds_sync() {

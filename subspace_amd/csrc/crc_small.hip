@@ -1217,19 +1217,12 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
         if (blockIdx.x == 0 && wid == 0) *a.error_count = 0u;  // a publish has no mismatches
       } else {
         // the workgroup's count: one 64-bit LDS atomic per wave, (1 << 40) | its count; the
-        // last wave of the workgroup adds the total and one finished workgroup, (1 << 32) |
-        // count, to the call's word; the workgroup that sees G - 1 finished before it writes
-        // the call's total and resets the word
+        // last wave of the workgroup adds the workgroup's total to the call's counter entry
+        // (crc_device.h add_call_mismatches)
         const u64 o = __hip_atomic_fetch_add(reinterpret_cast<lds_u64_t*>((uintptr_t)smism), (1ull << 40) | mism,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if ((u32)(o >> 40) == (u32)NPW - 1u) {
-          const u32 n = (u32)((o & ((1ull << 40) - 1)) + mism);  // the workgroup's mismatches
-          const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(a.counter), (1ull << 32) | (u64)n);
-          if ((u32)(old >> 32) == gridDim.x - 1u) {
-            *a.error_count = (u32)old + n;
-            __hip_atomic_store(a.counter, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
+        if ((u32)(o >> 40) == (u32)NPW - 1u)
+          add_call_mismatches(a.counter, (u32)((o & ((1ull << 40) - 1)) + mism), a.error_count);
       }
     }
   } else {

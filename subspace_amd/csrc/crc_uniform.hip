@@ -369,19 +369,11 @@ __global__ __launch_bounds__(WG) void crc32_uniform4k_kernel(
           if (blockIdx.x == 0 && wid == 0) *sa.error_count = 0u;
         } else {
           // the workgroup's count: one LDS atomic per finishing wave, (1 << 24) | its count
-          // (< 2^24: at most 512 messages per workgroup); the last of them adds the total and
-          // one finished workgroup, (1 << 32) | count, to the call's word; the workgroup that
-          // sees G - 1 finished before it writes the call's total and resets the word
+          // (< 2^24: at most 512 messages per workgroup); the last of them adds the workgroup's
+          // total to the call's counter entry (crc_device.h add_call_mismatches)
           const u32 o = __hip_atomic_fetch_add(reinterpret_cast<lds_u32_t*>((uintptr_t)smism), (1u << 24) | mism,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if ((o >> 24) == (u32)kSlotFinishers - 1u) {
-            const u32 n = (o + mism) & 0xFFFFFFu;
-            const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(sa.counter), (1ull << 32) | (u64)n);
-            if ((u32)(old >> 32) == gridDim.x - 1u) {
-              *sa.error_count = (u32)old + n;
-              __hip_atomic_store(sa.counter, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-          }
+          if ((o >> 24) == (u32)kSlotFinishers - 1u) add_call_mismatches(sa.counter, (o + mism) & 0xFFFFFFu, sa.error_count);
         }
       }
     }

@@ -970,3 +970,37 @@ def test_desc8_incremental_matches_pack(so, length):
     tiles = list(descs_of(so, length))
     for j in range(2, len(tiles)):
         assert desc8_incremental(so, length, j) == pack_desc8(*tiles[j]), j
+
+
+def call_mismatch_count(G, counts, order):
+    """Replays crc_device.h add_call_mismatches: workgroups in `order` add their counts to group
+    word b % 8; a group's last adds the group total to the top word and resets its word; the last
+    group writes the call's total and resets the top. Returns (writes of the total, words left)."""
+    words = [0] * 9
+    writes = []
+    for b in order:
+        g = b % 8
+        ng = (G - g + 7) // 8
+        old = words[1 + g]
+        words[1 + g] += (1 << 32) | counts[b]
+        if old >> 32 == ng - 1:
+            tot = (old + counts[b]) & 0xFFFFFFFF
+            words[1 + g] = 0
+            o2 = words[0]
+            words[0] += (1 << 32) | tot
+            if o2 >> 32 == min(G, 8) - 1:
+                writes.append((o2 + tot) & 0xFFFFFFFF)
+                words[0] = 0
+    return writes, words
+
+
+@pytest.mark.parametrize("G", [1, 2, 7, 8, 9, 17, 256, 257, 1000])
+def test_call_mismatch_count_is_written_once_and_resets(G):
+    """The slot kernels' two-level mismatch count: whatever order the workgroups finish in,
+    exactly one of them writes the call's total, and every counter word is 0 afterwards (the next
+    call that takes the entry starts clean, no memset)."""
+    rng = np.random.default_rng(G)
+    counts = [int(x) for x in rng.integers(0, 600, G)]
+    for _ in range(5):
+        writes, words = call_mismatch_count(G, counts, rng.permutation(G))
+        assert writes == [sum(counts)] and words == [0] * 9
