@@ -184,6 +184,25 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     __builtin_amdgcn_sched_barrier(0);
   };
   auto load_lines = [&](u32x4 (&D)[8], u64 s, u32 E) __attribute__((always_inline)) { load_lines_at(D, s, E, li); };
+#ifdef SUBSPACE_RP2_DEBUG
+  // (A/B debug builds) REPACK2: the line this lane is about to load must be line li < n of the
+  // message of ring entry q (wave q / 32's window message q % 32); else print and load nothing
+  auto rp2_check = [&](const char* where, u64 s, u32& E, u32 li, u32 q) __attribute__((always_inline)) {
+    if (E == 0u) return;
+    const u32 w2 = q >> 5, i2 = q & 31u;
+    const u64 t02 = front_slot(blockIdx.x, gridDim.x, w2);
+    const u64 m2 = 2u * (t02 + (u64)(i2 >> 1) * nw) + (i2 & 1u);
+    u64 rs = 0, rL = 0;
+    if (m2 < count) record(m2, rs, rL);
+    const u32 n2 = (E + 127u) >> 7;
+    if (m2 >= count || rs != s || rL + (rs & 15u) != E || li >= n2) {
+      printf("RP2 %s wg %u wave %u lane %d: q %u m %llu s %llx rec %llx E %u rec %llu li %u\n", where, blockIdx.x, wid,
+             lane, q, (unsigned long long)m2, (unsigned long long)s, (unsigned long long)rs, E,
+             (unsigned long long)rL, li);
+      E = 0u;
+    }
+  };
+#endif
   // FAST path: the tile's line offset from base, computed (and pinned) before the wait for
   // the previous tile, then 8 loads at immediate offsets (the uniform kernel's issue)
   auto fast_off = [&](u32 k) __attribute__((always_inline)) {
@@ -785,10 +804,12 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       r2n = (r2E + 127u) >> 7;
       const u32 incl = wave_scan(r2n, false);
       r2x = incl - r2n;
+      // (the ballot outside the one-lane branch: inside it only lane 0 would vote)
+      const u32 nsh = (u32)__builtin_popcountll(__ballot(r2n != 0u && r2x + r2n > 64u));
       if (lane == 63) lds_st(sbase + kRp2Misc + 4u * wid, incl);
       if (lane == 0) {
         lds_st(sbase + kRp2Misc + 32u + 4u * wid, fast ? 0u : 1u);
-        lds_st(sbase + kRp2Misc + 64u + 4u * wid, (u32)__builtin_popcountll(__ballot(r2n != 0u && r2x + r2n > 64u)));
+        lds_st(sbase + kRp2Misc + 64u + 4u * wid, nsh);
       }
       if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
       if (threadIdx.x == 0) lds_st(sbase + kRp2Misc + 96u, 0u);  // the tile ticket
@@ -878,6 +899,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     load_lines_at(A, sc, rp_ext(sc, Lc, pc), (pc >> 8) & 31u);
     if (rcode0) lds_st64(sring + 8u * (u32)lane, (u64)rcode0 << 32);
   } else if (wg2 && !fast) {
+#ifdef SUBSPACE_RP2_DEBUG
+    rp2_check("local", ls, lE, lli, 32u * wid + lsrc);
+#endif
     load_lines_at(A, ls, lE, lli);  // REPACK2: the wave's local tile
   } else {
     load_lines(A, sc, ext(0, sc, Lc));  // (FAST: the same addresses as load_at's)
@@ -1010,6 +1034,10 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
           mli = live ? P - st + (m >> 26) : 0u;
           me = (u32)(sq >> 56);
           mst = st > 64u * jj ? st - 64u * jj : 0u;
+#ifdef SUBSPACE_RP2_DEBUG
+          if (live && e >= NR) printf("RP2 rank wg %u wave %u lane %d j %u e %u NR %u\n", blockIdx.x, wid, lane, j, e, NR);
+          rp2_check("shared", ms, mE, mli, me);
+#endif
         };
         u64 s_a, s_b;
         u32 E_a, li_a, e_a, st_a, E_b, li_b, e_b, st_b;
