@@ -1263,7 +1263,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u64 xcc = (u64)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
     const u64 v = lane == 0 ? pt[0] : lane == 1 ? pt[1] : lane == 2 ? pt[2] : lane == 3 ? pt[3]
                 : lane == 4 ? pt[4] : lane == 5 ? pt[5] : lane == 6 ? pt[6]
-                : (xcc | ((u64)nk << 32) | ((u64)fast << 48) | ((u64)(repack || rp2) << 49) |
+                : (xcc | ((u64)nk << 32) | ((u64)(fast && !rp2) << 48) | ((u64)(repack || rp2) << 49) |
                    ((u64)(rp2 ? r2tiles : rnt) << 52));
     if (lane < kProbeWords) r[lane] = v;
   }
