@@ -158,9 +158,10 @@ constexpr u32 kSmallRingTiles = 32;                               // tiles per r
 constexpr u32 kSmallRingBytesPerWave = kSmallRingTiles * 2u * 8u;  // (value | code << 32) per message
 // Workgroup repack of the slot kernel (crc_small.hip SLOT, G = 32, REPACK2), in the same area as
 // the per-wave rings (a workgroup runs one or the other): the workgroup's entries (8 waves x 32
-// messages; the host gives no slot wave more than 16 tiles) -- each wave's first 64 lines its
-// own local tile, the other lines laid out back to back over the workgroup's shared packed
-// tiles, which its 8 waves take from an LDS ticket.
+// messages; the host gives no slot wave more than 16 tiles) -- each wave's first Q lines its
+// own local tiles (Q: the workgroup's least wave, rounded down to whole tiles, at least 64), the
+// other lines laid out back to back over the workgroup's shared packed tiles, which its 8 waves
+// take from an LDS ticket.
 constexpr u32 kRp2Entries = 256;
 constexpr u32 kRp2MaxTiles = kRp2Entries * 32u / 64u;           // every entry at most 32 lines
 // the entries with lines, by rank: u64 first byte | ring entry << 56 (offsets and addresses are
@@ -170,10 +171,11 @@ constexpr u32 kRp2EntM = kRp2EntS + 8u * kRp2Entries;
 constexpr u32 kRp2Ring = kRp2EntM + 4u * kRp2Entries;           // u64: value (XOR of parts) | code << 32
 constexpr u32 kRp2Starts = kRp2Ring + 8u * kRp2Entries;         // u64 per packed tile: lines that start a message
 constexpr u32 kRp2First = kRp2Starts + 8u * kRp2MaxTiles;       // u32 per packed tile: rank of its line 0's entry
-// u32 [0, 8) lines per wave, [8, 16) votes (not FAST), [16, 24) entries with shared lines per wave,
-// [24] ticket; then u64 [14, 22) each wave's local start marks
+// u32 [0, 8) lines per wave, [8, 16) votes (not FAST), [24] ticket; u64 [14, 22) each wave's local
+// start marks; then per wave 16 bytes: its entries with lines past 64 (i + 1), i = 0..15
 constexpr u32 kRp2Misc = kRp2First + 4u * kRp2MaxTiles;
-constexpr u32 kRp2Bytes = kRp2Misc + 176u - kSmallRing;
+constexpr u32 kRp2Counts = kRp2Misc + 176u;
+constexpr u32 kRp2Bytes = kRp2Counts + 128u - kSmallRing;
 constexpr u32 kSmallShared = 8u * kSmallRingBytesPerWave > kRp2Bytes ? 8u * kSmallRingBytesPerWave : kRp2Bytes;
 constexpr size_t small_lds_bytes() { return kSmallRing + kSmallShared; }
 static_assert(small_lds_bytes() + 16u <= 160u * 1024u, "small-message kernel LDS (+ mismatch word) exceeds 160 KiB");

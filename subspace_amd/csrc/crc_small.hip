@@ -94,7 +94,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   constexpr bool probe = PROBE;
   if constexpr (probe) pt[0] = __builtin_amdgcn_s_memrealtime();
   LdsFill<WG, kSmallOpSlots> fill;
-  fill.load(gtab, gops);
 
   const int lane = threadIdx.x & 63;
   const u32 wid = rfl(threadIdx.x >> 6);
@@ -728,9 +727,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   };
   constexpr u32 kWinMask = W - 1u;
 
-  // Prologue: table loads, the window's records (and SLOT its prefix offsets); the LDS fill while
-  // the records are in flight; then the first window's prefix words and tile 0's lines, the
-  // barrier (tile 0's latency hides behind it), and the span terms hashed under tile 0's flight.
+  // Prologue: the window's records (and SLOT its prefix offsets), then the table loads; the
+  // records' classification while the table loads are in flight; the first window's prefix words
+  // and tile 0's lines; then the LDS fill (tile 0's latency hides behind it and the barrier), and
+  // the span terms hashed under tile 0's flight. (Round 6: the records first and the fill after
+  // tile 0's issue -- before, tile 0 was issued only after the fill's stores.)
   if constexpr (G == 32) {
     record(fmc, wS, wL);
   }
@@ -739,7 +740,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     fpre = *pp;
     asm volatile("" ::"v"(pp));
   }
-  fill.store(sbase);
+  fill.load(gtab, gops);
   if constexpr (SLOT && G < 32) {  // Z_C into its LDS slot
     if (threadIdx.x < 128u)
       lds_st(sbase + kLdsOps + 512u * (u32)kSmallOpZC + 4u * threadIdx.x,
@@ -768,52 +769,90 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // stream of the remaining lines.
   const bool wg2 = SLOT && G == 32 && ntiles <= (u64)kRp2MaxTilesPerWave * nw;
   u32 r2n = 0, r2x = 0, r2E = 0, r2code = 0;  // lines, lines of the wave's earlier entries, E, code
-  // the local tile, this lane: its entry's lane, line in the entry, E (0: none) and first byte
-  u32 lsrc = 0, lli = 0, lE = 0;
-  u64 ls = 0;
-  auto local_map = [&]() __attribute__((always_inline)) {
-    const u32 slm = sbase + kRp2Misc + 112u + 8u * wid;  // this wave's start marks
-    const bool mk = r2n != 0u && r2x < 64u;
-    if (lane == 0) lds_st64(slm, 0ull);
-    if (mk)
-      __hip_atomic_fetch_or(reinterpret_cast<lds_u64_t*>((uintptr_t)slm), 1ull << r2x, __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_WORKGROUP);
-    const u64 Sl = lds_ld64(slm);
-    // the entries with local lines by rank -> their lanes (ds_permute: rank k's lane to lane k)
-    const u64 mkb = __ballot(mk);
-    const u32 rk = (u32)__builtin_popcountll(mkb & ((1ull << lane) - 1ull));
-    const u32 r2l = (u32)__builtin_amdgcn_ds_permute((int)((mk ? rk : 32u + ((u32)lane & 31u)) << 2), lane);
-    const u32 tl = (u32)__builtin_amdgcn_readlane((int)(r2x + r2n), 63);  // the wave's lines
-    const u32 k = (u32)__builtin_popcountll(Sl & ((2ull << lane) - 1ull));
-    lsrc = bperm(k ? k - 1u : 0u, r2l) & 31u;
-    ls = ((u64)bperm(lsrc, (u32)(wS >> 32)) << 32) | (u64)bperm(lsrc, (u32)wS);
-    const u32 E = bperm(lsrc, r2E);
-    lli = (u32)lane - bperm(lsrc, r2x);
-    lE = (u32)lane < tl && k ? E : 0u;
+  // the entries with lines by rank (lane order) -> their lanes (ds_permute: rank k's lane to lane k)
+  u32 r2l = 0;
+  bool runi = false;  // the wave's entries with lines are lanes 0, 1, ... and have one line count
+  auto rank_lanes = [&]() __attribute__((always_inline)) {
+    const bool wl = r2n != 0u;
+    const u64 mwl = __ballot(wl);
+    const u32 rk = (u32)__builtin_popcountll(mwl & ((1ull << lane) - 1ull));
+    r2l = (u32)__builtin_amdgcn_ds_permute((int)((wl ? rk : 32u + ((u32)lane & 31u)) << 2), lane);
+    const u32 n0 = (u32)__builtin_amdgcn_readfirstlane((int)r2n);
+    runi = (mwl & (mwl + 1ull)) == 0ull && __ballot(wl && r2n != n0) == 0ull;
   };
+  // Local tile j of the wave (lines 64 j .. 64 j + 63 of its own stream, those below nloc), this
+  // lane: its entry's lane, line in the entry, E (0: none), first byte, and the lane where the
+  // entry's part in this tile starts. The entry is the one of rank k - 1, k = the entries with
+  // lines starting before the tile + the tile's start marks up to this lane (an LDS word per
+  // wave); one line count throughout (a fixed-size channel): rank = line / n.
+  auto local_map = [&](u32 j, u32 nloc, u32& src, u64& s_, u32& E_, u32& li_, u32& st_) __attribute__((always_inline)) {
+    const u32 P = 64u * j + (u32)lane;
+    u32 k;
+    if (runi) {
+      const u32 n0 = (u32)__builtin_amdgcn_readfirstlane((int)r2n);
+      k = n0 ? P / n0 + 1u : 0u;
+    } else {
+      const u32 slm = sbase + kRp2Misc + 112u + 8u * wid;
+      const bool mk = r2n != 0u && (r2x >> 6) == j;
+      if (lane == 0) lds_st64(slm, 0ull);
+      if (mk)
+        __hip_atomic_fetch_or(reinterpret_cast<lds_u64_t*>((uintptr_t)slm), 1ull << (r2x & 63u), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
+      const u64 Sl = lds_ld64(slm);
+      k = (u32)__builtin_popcountll(__ballot(r2n != 0u && r2x < 64u * j)) +
+          (u32)__builtin_popcountll(Sl & ((2ull << lane) - 1ull));
+    }
+    src = bperm(k ? k - 1u : 0u, r2l) & 31u;
+    s_ = ((u64)bperm(src, (u32)(wS >> 32)) << 32) | (u64)bperm(src, (u32)wS);
+    const u32 E = bperm(src, r2E), x = bperm(src, r2x);
+    li_ = P - x;
+    E_ = P < nloc && k ? E : 0u;
+    st_ = x > 64u * j ? x - 64u * j : 0u;
+  };
+  // the local tile 0 (mapped, and loaded, before the barrier)
+  u32 lsrc = 0, lli = 0, lE = 0, lst = 0;
+  u64 ls = 0;
   if constexpr (SLOT && G == 32) {
     if (wg2) {
       __builtin_amdgcn_sched_barrier(0);
-      const u64 Ew = wL + (wS & 15u);
-      r2code = !flive                 ? kCodeSkip
-             : wL > a.max_len         ? kCodeOversize
-             : Ew > (u64)kSmallMaxExt ? kCodeLong
-             : wL == 0                ? kCodeEmpty
-                                      : 0u;
-      r2E = r2code ? 0u : (u32)Ew;
-      r2n = (r2E + 127u) >> 7;
-      const u32 incl = wave_scan(r2n, false);
-      r2x = incl - r2n;
-      // (the ballot outside the one-lane branch: inside it only lane 0 would vote)
-      const u32 nsh = (u32)__builtin_popcountll(__ballot(r2n != 0u && r2x + r2n > 64u));
+      u32 incl;
+      if (fast) {  // every live entry a whole aligned 4 KiB payload (32 lines), the live lanes first
+        r2code = flive ? 0u : kCodeSkip;
+        r2E = flive ? kSmallMaxExt : 0u;
+        r2n = flive ? 32u : 0u;
+        r2x = 32u * (u32)__builtin_popcountll(__ballot(flive) & ((1ull << lane) - 1ull));
+        incl = r2x + r2n;
+      } else {
+        const u64 Ew = wL + (wS & 15u);
+        r2code = !flive                 ? kCodeSkip
+               : wL > a.max_len         ? kCodeOversize
+               : Ew > (u64)kSmallMaxExt ? kCodeLong
+               : wL == 0                ? kCodeEmpty
+                                        : 0u;
+        r2E = r2code ? 0u : (u32)Ew;
+        r2n = (r2E + 127u) >> 7;
+        incl = wave_scan(r2n, false);
+        r2x = incl - r2n;
+      }
+      // the wave's entries with lines past Q = 64 (i + 1), i = 0..15 (the workgroup picks Q after
+      // the barrier), one byte each; the ballots outside the one-lane branch (inside it only
+      // lane 0 would vote)
+      u32 cnt[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (u32 i = 0; i < 16; i++)
+        cnt[i >> 2] |= (u32)__builtin_popcountll(__ballot(r2n != 0u && r2x + r2n > 64u * (i + 1u))) << (8u * (i & 3u));
       if (lane == 63) lds_st(sbase + kRp2Misc + 4u * wid, incl);
       if (lane == 0) {
         lds_st(sbase + kRp2Misc + 32u + 4u * wid, fast ? 0u : 1u);
-        lds_st(sbase + kRp2Misc + 64u + 4u * wid, nsh);
+        lds_st4(sbase + kRp2Counts + 16u * wid, u32x4{cnt[0], cnt[1], cnt[2], cnt[3]});
       }
       if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
       if (threadIdx.x == 0) lds_st(sbase + kRp2Misc + 96u, 0u);  // the tile ticket
-      if (!fast) local_map();  // (a FAST wave's local tile is its FAST tile 0: same lanes, same loads)
+      if (!fast) {  // (a FAST wave's local tile 0 is its FAST tile 0: same lanes, same loads)
+        rank_lanes();
+        const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+        local_map(0u, tot < 64u ? tot : 64u, lsrc, ls, lE, lli, lst);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -906,6 +945,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   } else {
     load_lines(A, sc, ext(0, sc, Lc));  // (FAST: the same addresses as load_at's)
   }
+  fill.store(sbase);
   __syncthreads();
   // (nothing hoisted above the barrier: hipcc otherwise moved the span hash's first step there,
   // with a wait for tile 0's lines, so every wave of the workgroup waited for the slowest
@@ -942,26 +982,31 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   u32 k = 0;
   if (rp2) {
     if constexpr (SLOT && G == 32) {
-      // the shared stream: every wave's lines past its local tile, wave after wave; an entry's
-      // shared part (its lines from local position 64 on) gets a rank among the entries with one,
-      // its record, its first shared position and the line it starts with; the shared tiles'
-      // start marks and first entries (by rank)
+      // Q: every wave computes its first Q lines itself (local tiles), Q = the workgroup's least
+      // wave rounded down to whole tiles, at least one tile; the rest of every wave's lines form
+      // the shared stream, wave after wave. An entry's shared part (its lines from local position
+      // Q on) gets a rank among the entries with one, its record, its first shared position and
+      // the line it starts with; the shared tiles' start marks and first entries (by rank).
       const u32x4 ta = lds_ld4(sbase + kRp2Misc), tb = lds_ld4(sbase + kRp2Misc + 16u);
-      const u32x4 ca = lds_ld4(sbase + kRp2Misc + 64u), cb = lds_ld4(sbase + kRp2Misc + 80u);
       const u32 tw[8] = {rfl(ta.x), rfl(ta.y), rfl(ta.z), rfl(ta.w), rfl(tb.x), rfl(tb.y), rfl(tb.z), rfl(tb.w)};
-      const u32 cw[8] = {rfl(ca.x), rfl(ca.y), rfl(ca.z), rfl(ca.w), rfl(cb.x), rfl(cb.y), rfl(cb.z), rfl(cb.w)};
+      u32 tmin = tw[0];
+#pragma unroll
+      for (u32 w = 1; w < 8; w++) tmin = tw[w] < tmin ? tw[w] : tmin;
+      const u32 Q = tmin >= 128u ? tmin & ~63u : 64u;
+      const u32 qi = (Q >> 6) - 1u;  // (<= 15: a wave has at most 32 x 32 lines)
       u32 wbase = 0, T = 0, rbase = 0, NR = 0;
 #pragma unroll
       for (u32 w = 0; w < 8; w++) {
-        const u32 sh = tw[w] > 64u ? tw[w] - 64u : 0u;
+        const u32 sh = tw[w] > Q ? tw[w] - Q : 0u;
+        const u32 cw = (lds_ld(sbase + kRp2Counts + 16u * w + (qi & ~3u)) >> (8u * (qi & 3u))) & 0xFFu;
         wbase += w < wid ? sh : 0u;
         T += sh;
-        rbase += w < wid ? cw[w] : 0u;
-        NR += cw[w];
+        rbase += w < wid ? cw : 0u;
+        NR += cw;
       }
-      const u32 a0 = r2x > 64u ? r2x : 64u;  // the entry's first local position in the shared stream
-      const u32 shn = r2x + r2n > 64u ? r2x + r2n - a0 : 0u;
-      const u32 start = wbase + a0 - 64u;
+      const u32 a0 = r2x > Q ? r2x : Q;  // the entry's first local position in the shared stream
+      const u32 shn = r2x + r2n > Q ? r2x + r2n - a0 : 0u;
+      const u32 start = wbase + a0 - Q;
       const u32 r = rbase + (u32)__builtin_popcountll(__ballot(shn != 0u) & ((1ull << lane) - 1ull));
       if (lane < 32) {
         const u32 q = 32u * wid + (u32)lane;
@@ -999,70 +1044,85 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
           __hip_atomic_fetch_xor(reinterpret_cast<lds_u32_t*>((uintptr_t)(sbase + kRp2Ring + 8u * me)), seg,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       };
-      // the local tile (loaded before the barrier; a FAST wave's is its FAST tile 0, mapped here)
-      if (fast) local_map();
+      // local tile 0 (loaded before the barrier; a FAST wave's is its FAST tile 0, mapped here)
+      const u32 tot = tw[wid];
+      const u32 nloc = tot < Q ? tot : Q, nlt = (nloc + 63u) >> 6;  // local lines, tiles
+      if (fast) {
+        rank_lanes();
+        local_map(0u, nloc < 64u ? nloc : 64u, lsrc, ls, lE, lli, lst);
+      }
       drain_before_issue();
       stamp_tile0();
-      process2(A, ls, lE, lli, 32u * wid + lsrc, bperm(lsrc, r2x));
+      process2(A, ls, lE, lli, 32u * wid + lsrc, lst);
       r2tiles++;
       const u32 ntl = (T + 63u) >> 6;  // shared tiles of the workgroup
-      if (ntl) {
-        __syncthreads();  // the shared tables
-        const u32 tick = sbase + kRp2Misc + 96u;
-        auto grab = [&]() __attribute__((always_inline)) -> u32 {
+      if (ntl) __syncthreads();       // the shared tables
+      const u32 tick = sbase + kRp2Misc + 96u;
+      // the wave's next tile: its local tiles 1 .. nlt - 1, then shared tiles from the ticket; v
+      // false: none left (E 0: the loads read the step table)
+      u32 jl = 1;
+      auto next = [&](bool& v, u64& ms, u32& mE, u32& mli, u32& me, u32& mst) __attribute__((always_inline)) {
+        if (jl < nlt) {
+          u32 src;
+          local_map(jl, nloc, src, ms, mE, mli, mst);
+          me = 32u * wid + src;
+#ifdef SUBSPACE_RP2_DEBUG
+          rp2_check("local", ms, mE, mli, me);
+#endif
+          jl++;
+          v = true;
+          return;
+        }
+        u32 j = ntl;
+        if (ntl) {
           u32 t = 0;
           if (lane == 0)
             t = __hip_atomic_fetch_add(reinterpret_cast<lds_u32_t*>((uintptr_t)tick), 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-          return (u32)__builtin_amdgcn_readlane((int)t, 0);
-        };
-        // shared tile j, this lane: its entry's record and ring entry, its line, the entry's E (0: no
-        // line), and the lane where the entry's part in this tile starts
-        auto map2 = [&](u32 j, u64& ms, u32& mE, u32& mli, u32& me, u32& mst) __attribute__((always_inline)) {
-          const u32 jj = j < ntl ? j : ntl - 1u;
-          const u64 Sj = lds_ld64(sbase + kRp2Starts + 8u * jj);
-          const u32 fe = lds_ld(sbase + kRp2First + 4u * jj);
-          const u64 below = Sj & ((2ull << lane) - 1ull);
-          u32 e = fe + (u32)__builtin_popcountll(below) - (u32)(Sj & 1ull);
-          e = e < NR ? e : NR - 1u;
-          const u32 m = lds_ld(sbase + kRp2EntM + 4u * e);
-          const u64 sq = lds_ld64(sbase + kRp2EntS + 8u * e);
-          ms = sq & ((1ull << 56) - 1ull);
-          const u32 P = 64u * jj + (u32)lane, st = (m >> 13) & 0x1FFFu;
-          const bool live = j < ntl && P < T;
-          mE = live ? (m & 0x1FFFu) : 0u;
-          mli = live ? P - st + (m >> 26) : 0u;
-          me = (u32)(sq >> 56);
-          mst = st > 64u * jj ? st - 64u * jj : 0u;
-#ifdef SUBSPACE_RP2_DEBUG
-          if (live && e >= NR) printf("RP2 rank wg %u wave %u lane %d j %u e %u NR %u\n", blockIdx.x, wid, lane, j, e, NR);
-          rp2_check("shared", ms, mE, mli, me);
-#endif
-        };
-        u64 s_a, s_b;
-        u32 E_a, li_a, e_a, st_a, E_b, li_b, e_b, st_b;
-        u32 ja = grab();
-        map2(ja, s_a, E_a, li_a, e_a, st_a);
-        load_lines_at(A, s_a, E_a, li_a);
-        while (ja < ntl) {
-          const u32 jb = grab();
-          map2(jb, s_b, E_b, li_b, e_b, st_b);
-          issue_prio_hi();
-          drain_before_issue();
-          load_lines_at(B, s_b, E_b, li_b);
-          issue_prio_lo();
-          process2(A, s_a, E_a, li_a, e_a, st_a);
-          r2tiles++;
-          if (jb >= ntl) break;
-          ja = grab();
-          map2(ja, s_a, E_a, li_a, e_a, st_a);
-          issue_prio_hi();
-          drain_before_issue();
-          load_lines_at(A, s_a, E_a, li_a);
-          issue_prio_lo();
-          process2(B, s_b, E_b, li_b, e_b, st_b);
-          r2tiles++;
+          j = (u32)__builtin_amdgcn_readlane((int)t, 0);
         }
+        v = j < ntl;
+        // shared tile j, this lane: its entry's record and ring entry, its line, the entry's E,
+        // and the lane where the entry's part in this tile starts
+        const u32 jj = v ? j : 0u;
+        const u64 Sj = lds_ld64(sbase + kRp2Starts + 8u * jj);
+        const u32 fe = lds_ld(sbase + kRp2First + 4u * jj);
+        u32 e = fe + (u32)__builtin_popcountll(Sj & ((2ull << lane) - 1ull)) - (u32)(Sj & 1ull);
+        e = e < NR ? e : (NR ? NR - 1u : 0u);
+        const u32 m = lds_ld(sbase + kRp2EntM + 4u * e);
+        const u64 sq = lds_ld64(sbase + kRp2EntS + 8u * e);
+        ms = sq & ((1ull << 56) - 1ull);
+        const u32 P = 64u * jj + (u32)lane, st = (m >> 13) & 0x1FFFu;
+        const bool live = v && P < T;
+        mE = live ? (m & 0x1FFFu) : 0u;
+        mli = live ? P - st + (m >> 26) : 0u;
+        me = (u32)(sq >> 56);
+        mst = st > 64u * jj ? st - 64u * jj : 0u;
+#ifdef SUBSPACE_RP2_DEBUG
+        rp2_check("shared", ms, mE, mli, me);
+#endif
+      };
+      bool va, vb;
+      u64 s_a, s_b;
+      u32 E_a, li_a, e_a, st_a, E_b, li_b, e_b, st_b;
+      next(va, s_a, E_a, li_a, e_a, st_a);
+      load_lines_at(A, s_a, E_a, li_a);
+      while (va) {
+        next(vb, s_b, E_b, li_b, e_b, st_b);
+        issue_prio_hi();
+        drain_before_issue();
+        load_lines_at(B, s_b, E_b, li_b);
+        issue_prio_lo();
+        process2(A, s_a, E_a, li_a, e_a, st_a);
+        r2tiles++;
+        if (!vb) break;
+        next(va, s_a, E_a, li_a, e_a, st_a);
+        issue_prio_hi();
+        drain_before_issue();
+        load_lines_at(A, s_a, E_a, li_a);
+        issue_prio_lo();
+        process2(B, s_b, E_b, li_b, e_b, st_b);
+        r2tiles++;
       }
       drain_before_issue();
       if constexpr (probe) pt[4] = __builtin_amdgcn_s_memrealtime();

@@ -548,9 +548,12 @@ def small_kernel_repack2(starts, lengths, grid, rng):
     per workgroup, lane i < 32 of wave w holds message i of its window (entry q = 32 w + i,
     message 2 (t0 + (i / 2) nw) + i % 2); an entry of E = L + (s & 15) in [1, 4096] has n = ceil(E /
     128) lines, laid out back to back in lane order (r2x: the wave's lines before it). The wave's
-    first 64 lines are its local tile: lane P's entry is the entry of rank k - 1, k = popcount(local
-    start marks & (2 << P) - 1), ranks mapped to lanes as the kernel's ds_permute does. The other
-    lines of every wave form the shared stream (wave after wave); entries with shared lines are
+    first Q lines are its local tiles (Q: the workgroup's least wave's lines rounded down to whole
+    tiles, at least 64): lane P of local tile j takes the entry of rank k - 1, k = the entries with
+    lines starting before the tile + popcount(the tile's start marks & (2 << P) - 1), or line / n
+    when the wave's entries are lanes 0, 1, ... with one line count; ranks map to lanes as the
+    kernel's ds_permute does. The other lines of every wave form the shared stream (wave after
+    wave); entries with shared lines are
     ranked r = 0, 1, ... in the same order (record at r, ring entry in the offset's top byte,
     first shared position and first line), the shared tiles' start marks S_j and first entries
     (by rank) built as the kernel builds them, and shared tile j's lane i finds its entry as r =
@@ -593,25 +596,43 @@ def small_kernel_repack2(starts, lengths, grid, rng):
 
         def emit(lanes):
             tiles.append(lanes)
-        # local tiles
+        # local tiles: every wave's first Q lines, Q = the least wave's lines rounded down to whole
+        # tiles, at least 64; the counts of entries with lines past 64 (i + 1) checked against Q's
+        tots = [sum(n for *_, n in ents) for ents in waves]
+        tmin = min(tots)
+        Q = tmin & ~63 if tmin >= 128 else 64
         shared = []  # (q, m, E, n, first shared line) in stream order
         for ents in waves:
             r2x = [int(x) for x in np.concatenate([[0], np.cumsum([n for *_, n in ents])])[:-1]]
             tot = sum(n for *_, n in ents)
-            marks = [r2x[i] for i in range(32) if ents[i][3] and r2x[i] < 64]
-            withl = [i for i in range(32) if ents[i][3] and r2x[i] < 64]  # rank -> lane
-            lanes = {}
-            for P in range(min(tot, 64)):
-                k = sum(1 for x in marks if x <= P)
-                i = withl[k - 1]
-                q, m, E, n = ents[i]
-                lanes[P] = (q, m, E, n, P - r2x[i], r2x[i])
-            emit(lanes)
+            nloc = min(tot, Q)
+            withl = [i for i in range(32) if ents[i][3]]  # rank -> lane
+            nset = {ents[i][3] for i in withl}
+            runi = withl == list(range(len(withl))) and len(nset) <= 1
+            for j in range((nloc + 63) // 64):
+                lanes = {}
+                for lane in range(64):
+                    P = 64 * j + lane
+                    if P >= nloc:
+                        continue
+                    if runi:
+                        k = P // ents[0][3] + 1
+                    else:
+                        base = sum(1 for i in withl if r2x[i] < 64 * j)
+                        k = base + sum(1 for i in withl if 64 * j <= r2x[i] <= P)
+                    i = withl[k - 1]
+                    q, m, E, n = ents[i]
+                    lanes[lane] = (q, m, E, n, P - r2x[i], max(r2x[i] - 64 * j, 0))
+                emit(lanes)
+            cnt = sum(1 for i in range(32) if ents[i][3] and r2x[i] + ents[i][3] > Q)
+            got = 0
             for i in range(32):
                 q, m, E, n = ents[i]
-                if n and r2x[i] + n > 64:
-                    a0 = max(r2x[i], 64)
+                if n and r2x[i] + n > Q:
+                    a0 = max(r2x[i], Q)
                     shared.append((q, m, E, n, a0 - r2x[i], r2x[i] + n - a0))
+                    got += 1
+            assert got == cnt
         # shared stream
         start = [int(x) for x in np.concatenate([[0], np.cumsum([c for *_, c in shared])])[:-1]]
         T = sum(c for *_, c in shared)
@@ -1004,3 +1025,26 @@ def test_call_mismatch_count_is_written_once_and_resets(G):
     for _ in range(5):
         writes, words = call_mismatch_count(G, counts, rng.permutation(G))
         assert writes == [sum(counts)] and words == [0] * 9
+
+
+@pytest.mark.parametrize("seed,count,grid,L", [(50, 4096, 16, 1024), (51, 4000, 16, 256), (52, 2047, 8, 4096),
+                                               (53, 999, 4, 3000)])
+def test_small_kernel_repack2_fixed_sizes(seed, count, grid, L):
+    """REPACK2 on a fixed-size channel (one line count per wave: the local tiles' line / n map),
+    every line once, loads in their messages, ring words complete."""
+    rng = np.random.default_rng(seed)
+    lengths = np.full(count, L)
+    lengths[count // 2] = L - 1  # one wave not FAST when L = 4096
+    starts = np.arange(count) * ((L + 15 + 63) & ~63) + 64
+    lines, wgs = {}, 0
+    for kind, a, b, *rest in small_kernel_repack2(starts, lengths, grid, rng):
+        if kind == "wgs":
+            wgs = a
+        elif kind == "line":
+            lines[(a, b)] = lines.get((a, b), 0) + 1
+        elif kind == "load":
+            s, e = int(starts[a]), int(starts[a] + lengths[a])
+            assert b % 16 == 0 and b + 16 > s and b < e, (a, s, e, b)
+        elif kind == "ring":
+            assert b == rest[0], (a, b, rest[0])
+    assert wgs > 0 and all(v == 1 for v in lines.values())
