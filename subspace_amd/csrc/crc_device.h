@@ -540,12 +540,24 @@ __device__ __forceinline__ void reset_scan_state(u64* status, u64 nwords, u32* t
 // (u64, all 0 between calls). Workgroup b adds (1 << 32) | n to group word b % kCountGroups; the
 // workgroup that finds the rest of its group done adds the group's total to the top word and
 // resets its group word; the one that finds every other group done writes the call's total and
-// resets the top word. (One word for all workgroups serialised their 256 atomics at the end of
-// a short drain: the last workgroup of a 65,536-slot S_short call exited ~2.5 us after the
-// median, tools/small_timeline.py, round 6.)
-constexpr u32 kCountGroups = 8;
+// resets the top word. SUBSPACE_COUNT_GROUPS = 1 (the product): one word, one atomic per
+// workgroup -- the two-level form (8) did not shorten the ~2.5 us exit tail of a 65,536-slot
+// S_short call (tools/small_timeline.py, r06b vs r06h) and puts a second dependent atomic on the
+// last workgroup.
+#ifndef SUBSPACE_COUNT_GROUPS
+#define SUBSPACE_COUNT_GROUPS 1
+#endif
+constexpr u32 kCountGroups = SUBSPACE_COUNT_GROUPS;
 constexpr u32 kCountWords = 16;  // per call entry: one 128-B line
 __device__ __forceinline__ void add_call_mismatches(u64* counter, u32 n, u32* error_count) {
+  if constexpr (kCountGroups == 1) {  // one word: the workgroup that sees G - 1 done writes the total
+    const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(counter), (1ull << 32) | (u64)n);
+    if ((u32)(old >> 32) == gridDim.x - 1u) {
+      *error_count = (u32)old + n;
+      __hip_atomic_store(counter, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   const u32 G = gridDim.x, g = blockIdx.x % kCountGroups;
   const u32 ng = (G - g + kCountGroups - 1u) / kCountGroups;  // workgroups of group g
   const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(counter + 1 + g), (1ull << 32) | (u64)n);

@@ -70,7 +70,10 @@
 #ifndef SUBSPACE_SMALL_VARIANT
 #define SUBSPACE_SMALL_VARIANT 0
 #endif
-#if SUBSPACE_SMALL_VARIANT != 0 && !defined(SUBSPACE_AB_BUILD)
+#ifndef SUBSPACE_SMALL_EARLY_TILE0
+#define SUBSPACE_SMALL_EARLY_TILE0 0
+#endif
+#if (SUBSPACE_SMALL_VARIANT != 0 || SUBSPACE_SMALL_EARLY_TILE0 != 0) && !defined(SUBSPACE_AB_BUILD)
 #error "SUBSPACE_SMALL_VARIANT is a timing-only A/B knob (tools/ab_lib.sh defines SUBSPACE_AB_BUILD)"
 #endif
 
@@ -727,11 +730,12 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   };
   constexpr u32 kWinMask = W - 1u;
 
-  // Prologue: the window's records (and SLOT its prefix offsets), then the table loads; the
-  // records' classification while the table loads are in flight; the first window's prefix words
-  // and tile 0's lines; then the LDS fill (tile 0's latency hides behind it and the barrier), and
-  // the span terms hashed under tile 0's flight. (Round 6: the records first and the fill after
-  // tile 0's issue -- before, tile 0 was issued only after the fill's stores.)
+  // Prologue: table loads, the window's records (and SLOT its prefix offsets); the LDS fill while
+  // the records are in flight; then the first window's prefix words and tile 0's lines, the
+  // barrier (tile 0's latency hides behind it), and the span terms hashed under tile 0's flight.
+  // (SUBSPACE_SMALL_EARLY_TILE0, an A/B build: the records first and the fill after tile 0's
+  // issue -- measured slower on config S's list, 61.7 vs 63.0 %, r06i.)
+  if constexpr (!SUBSPACE_SMALL_EARLY_TILE0) fill.load(gtab, gops);
   if constexpr (G == 32) {
     record(fmc, wS, wL);
   }
@@ -740,7 +744,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     fpre = *pp;
     asm volatile("" ::"v"(pp));
   }
-  fill.load(gtab, gops);
+  if constexpr (SUBSPACE_SMALL_EARLY_TILE0) {
+    fill.load(gtab, gops);
+  } else {
+    fill.store(sbase);
+  }
   if constexpr (SLOT && G < 32) {  // Z_C into its LDS slot
     if (threadIdx.x < 128u)
       lds_st(sbase + kLdsOps + 512u * (u32)kSmallOpZC + 4u * threadIdx.x,
@@ -838,9 +846,15 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       // the barrier), one byte each; the ballots outside the one-lane branch (inside it only
       // lane 0 would vote)
       u32 cnt[4] = {0u, 0u, 0u, 0u};
+      if (fast) {  // (live entries 0 .. nl - 1, 32 lines each: those from 2 (i + 1) on)
+        const u32 nl = (u32)__builtin_popcountll(__ballot(flive));
 #pragma unroll
-      for (u32 i = 0; i < 16; i++)
-        cnt[i >> 2] |= (u32)__builtin_popcountll(__ballot(r2n != 0u && r2x + r2n > 64u * (i + 1u))) << (8u * (i & 3u));
+        for (u32 i = 0; i < 16; i++) cnt[i >> 2] |= (nl > 2u * i + 2u ? nl - 2u * i - 2u : 0u) << (8u * (i & 3u));
+      } else {
+#pragma unroll
+        for (u32 i = 0; i < 16; i++)
+          cnt[i >> 2] |= (u32)__builtin_popcountll(__ballot(r2n != 0u && r2x + r2n > 64u * (i + 1u))) << (8u * (i & 3u));
+      }
       if (lane == 63) lds_st(sbase + kRp2Misc + 4u * wid, incl);
       if (lane == 0) {
         lds_st(sbase + kRp2Misc + 32u + 4u * wid, fast ? 0u : 1u);
@@ -945,7 +959,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   } else {
     load_lines(A, sc, ext(0, sc, Lc));  // (FAST: the same addresses as load_at's)
   }
-  fill.store(sbase);
+  if constexpr (SUBSPACE_SMALL_EARLY_TILE0) fill.store(sbase);
   __syncthreads();
   // (nothing hoisted above the barrier: hipcc otherwise moved the span hash's first step there,
   // with a wait for tile 0's lines, so every wave of the workgroup waited for the slowest
