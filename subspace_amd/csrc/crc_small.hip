@@ -795,10 +795,13 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // wave); one line count throughout (a fixed-size channel): rank = line / n.
   auto local_map = [&](u32 j, u32 nloc, u32& src, u64& s_, u32& E_, u32& li_, u32& st_) __attribute__((always_inline)) {
     const u32 P = 64u * j + (u32)lane;
-    u32 k;
-    if (runi) {
+    u32 k, x;
+    if (runi) {  // entry = line / n, its first line = entry * n (no rank map, no marks)
       const u32 n0 = (u32)__builtin_amdgcn_readfirstlane((int)r2n);
-      k = n0 ? P / n0 + 1u : 0u;
+      const u32 e0 = n0 ? P / n0 : 0u;
+      src = e0 < 31u ? e0 : 31u;
+      k = n0 ? 1u : 0u;
+      x = src * n0;
     } else {
       const u32 slm = sbase + kRp2Misc + 112u + 8u * wid;
       const bool mk = r2n != 0u && (r2x >> 6) == j;
@@ -809,10 +812,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       const u64 Sl = lds_ld64(slm);
       k = (u32)__builtin_popcountll(__ballot(r2n != 0u && r2x < 64u * j)) +
           (u32)__builtin_popcountll(Sl & ((2ull << lane) - 1ull));
+      src = bperm(k ? k - 1u : 0u, r2l) & 31u;
+      x = bperm(src, r2x);
     }
-    src = bperm(k ? k - 1u : 0u, r2l) & 31u;
     s_ = ((u64)bperm(src, (u32)(wS >> 32)) << 32) | (u64)bperm(src, (u32)wS);
-    const u32 E = bperm(src, r2E), x = bperm(src, r2x);
+    const u32 E = bperm(src, r2E);
     li_ = P - x;
     E_ = P < nloc && k ? E : 0u;
     st_ = x > 64u * j ? x - 64u * j : 0u;
@@ -820,17 +824,35 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // the local tile 0 (mapped, and loaded, before the barrier)
   u32 lsrc = 0, lli = 0, lE = 0, lst = 0;
   u64 ls = 0;
+  // A wave's line total and its entries with lines past Q = 64 (i + 1), i = 0..15 (the workgroup
+  // picks Q after the barrier), one byte each, for the others (the ballots outside the one-lane
+  // branch: inside it only lane 0 would vote)
+  auto r2_publish = [&](u32 incl) __attribute__((always_inline)) {
+    u32 cnt[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (u32 i = 0; i < 16; i++)
+      cnt[i >> 2] |= (u32)__builtin_popcountll(__ballot(r2n != 0u && r2x + r2n > 64u * (i + 1u))) << (8u * (i & 3u));
+    if (lane == 63) lds_st(sbase + kRp2Misc + 4u * wid, incl);
+    if (lane == 0) lds_st4(sbase + kRp2Counts + 16u * wid, u32x4{cnt[0], cnt[1], cnt[2], cnt[3]});
+  };
+  // a FAST wave's entries: every live one a whole aligned 4 KiB payload, 32 lines, live lanes first
+  auto r2_fast = [&]() __attribute__((always_inline)) {
+    r2code = flive ? 0u : kCodeSkip;
+    r2E = flive ? kSmallMaxExt : 0u;
+    r2n = flive ? 32u : 0u;
+    r2x = 32u * (u32)__builtin_popcountll(__ballot(flive) & ((1ull << lane) - 1ull));
+    r2_publish(r2x + r2n);
+  };
   if constexpr (SLOT && G == 32) {
     if (wg2) {
       __builtin_amdgcn_sched_barrier(0);
-      u32 incl;
-      if (fast) {  // every live entry a whole aligned 4 KiB payload (32 lines), the live lanes first
-        r2code = flive ? 0u : kCodeSkip;
-        r2E = flive ? kSmallMaxExt : 0u;
-        r2n = flive ? 32u : 0u;
-        r2x = 32u * (u32)__builtin_popcountll(__ballot(flive) & ((1ull << lane) - 1ull));
-        incl = r2x + r2n;
-      } else {
+      // every wave votes; a FAST wave does nothing else here (its bookkeeping only if the
+      // workgroup repacks: r2_fast after the barrier), the config-S list's prologue stays short
+      if (lane == 0) lds_st(sbase + kRp2Misc + 32u + 4u * wid, fast ? 0u : 1u);
+      if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
+      if (threadIdx.x == 0) lds_st(sbase + kRp2Misc + 96u, 0u);  // the tile ticket
+      if (!fast) {
+        u32 incl;
         const u64 Ew = wL + (wS & 15u);
         r2code = !flive                 ? kCodeSkip
                : wL > a.max_len         ? kCodeOversize
@@ -841,28 +863,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
         r2n = (r2E + 127u) >> 7;
         incl = wave_scan(r2n, false);
         r2x = incl - r2n;
-      }
-      // the wave's entries with lines past Q = 64 (i + 1), i = 0..15 (the workgroup picks Q after
-      // the barrier), one byte each; the ballots outside the one-lane branch (inside it only
-      // lane 0 would vote)
-      u32 cnt[4] = {0u, 0u, 0u, 0u};
-      if (fast) {  // (live entries 0 .. nl - 1, 32 lines each: those from 2 (i + 1) on)
-        const u32 nl = (u32)__builtin_popcountll(__ballot(flive));
-#pragma unroll
-        for (u32 i = 0; i < 16; i++) cnt[i >> 2] |= (nl > 2u * i + 2u ? nl - 2u * i - 2u : 0u) << (8u * (i & 3u));
-      } else {
-#pragma unroll
-        for (u32 i = 0; i < 16; i++)
-          cnt[i >> 2] |= (u32)__builtin_popcountll(__ballot(r2n != 0u && r2x + r2n > 64u * (i + 1u))) << (8u * (i & 3u));
-      }
-      if (lane == 63) lds_st(sbase + kRp2Misc + 4u * wid, incl);
-      if (lane == 0) {
-        lds_st(sbase + kRp2Misc + 32u + 4u * wid, fast ? 0u : 1u);
-        lds_st4(sbase + kRp2Counts + 16u * wid, u32x4{cnt[0], cnt[1], cnt[2], cnt[3]});
-      }
-      if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
-      if (threadIdx.x == 0) lds_st(sbase + kRp2Misc + 96u, 0u);  // the tile ticket
-      if (!fast) {  // (a FAST wave's local tile 0 is its FAST tile 0: same lanes, same loads)
+        r2_publish(incl);
         rank_lanes();
         const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
         local_map(0u, tot < 64u ? tot : 64u, lsrc, ls, lE, lli, lst);
@@ -996,6 +997,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   u32 k = 0;
   if (rp2) {
     if constexpr (SLOT && G == 32) {
+      // the FAST waves' bookkeeping, now that the workgroup repacks
+      if (fast) r2_fast();
+      __syncthreads();
       // Q: every wave computes its first Q lines itself (local tiles), Q = the workgroup's least
       // wave rounded down to whole tiles, at least one tile; the rest of every wave's lines form
       // the shared stream, wave after wave. An entry's shared part (its lines from local position

@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--order", default="shuffled", choices=["shuffled", "ordered", "alias"],
                     help="alias: every record points at slot 0 of copy 0 (the compute-only run)")
     ap.add_argument("--mode", default="verify", choices=["verify", "publish"])
-    ap.add_argument("--sizes", default="4096", choices=["4096", "256", "mixed"])
+    ap.add_argument("--sizes", default="4096", help="4096, 256 or any fixed size <= 4096, or mixed")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ctx = gpu.CrcContext(0)
@@ -51,8 +51,8 @@ def main():
     waves = int(_lib.load_dev().subspace_crc_testutil_probe_waves(ctx._h, N))
     ps, stride = slots.compute_prefix_size(4, 0), slots.slot_stride(SIZE, 4, 0)
     rng = np.random.default_rng(0x5EED0005)
-    sizes = {"4096": np.full(N, SIZE, dtype=np.uint64), "256": np.full(N, 256, dtype=np.uint64),
-             "mixed": rng.integers(1, SIZE + 1, N).astype(np.uint64)}[a.sizes]
+    sizes = (rng.integers(1, SIZE + 1, N).astype(np.uint64) if a.sizes == "mixed"
+             else np.full(N, int(a.sizes), dtype=np.uint64))
     host = rng.integers(0, 256, stride * N, dtype=np.uint8)
     host.reshape(N, stride)[:, :ps] = slots.make_prefixes(N, sizes, checksum_size=4, metadata_size=0, seed=5)
     bufs = [torch.from_numpy(host).to(dev) for _ in range(NB)]
@@ -134,7 +134,13 @@ def main():
                "simd_pair_tiles_p50_p100": [int(np.percentile((rnt.reshape(-1, 8)[:, :4] + rnt.reshape(-1, 8)[:, 4:]), q))
                                             for q in (50, 100)],
                "cu_tiles_p50_p100": [int(np.percentile(rnt.reshape(-1, 8).sum(1), q)) for q in (50, 100)]}
+    # the last waves to exit in the last launch: their workgroup, wave, XCC and every stamp
+    t0l = lr[lr[:, 0] > 0, 0].min()
+    order_exit = np.argsort(-(lr[:, 6] * (lr[:, 0] > 0)))[:6]
+    slowest = [{"wg": int(w // 8), "wave": int(w % 8), "xcc": int(last[w, 7] & 0xFF),
+                "stamps_us": [round(float((lr[w, i] - t0l) * TICK_US), 2) for i in range(7)]} for w in order_exit]
     out = {"order": a.order, "mode": a.mode, "sizes": a.sizes, "launches": a.launches, "waves": waves,
+           "slowest_waves_last_launch": slowest,
            "fast_waves": fast, "repack": rep,
            "stamp_us_p0_p10_p50_p90_p100": {k: np.median(np.array(v), axis=0).round(2).tolist()
                                              for k, v in per.items() if v},
