@@ -467,33 +467,22 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     return (u32)__builtin_amdgcn_ds_bpermute((int)(e << 2), (int)v);
   };
   // UNIFORM FAST (no slots; G = 32 too since r05ca: 2-4 KiB messages 14-20 % faster than the
-  // repack loop): a uniform batch of messages of L bytes -- the tile's address from m * stride,
-  // one address and 8 immediate-offset loads per lane (reading C bytes per message from the
-  // 16-B block holding its first byte: past the message they are the next messages' bytes,
-  // masked). A tile holding a message whose C bytes would reach past the batch (the last few)
-  // takes the clamped loads instead. On 16-B strides every message has the padding p = C - L;
-  // on other strides (round 6, VERDICT r05 item 4: packed application buffers) message m starts
-  // mis = (m * stride) & 15 bytes into its first block, so its line 0 masks those bytes and
-  // starts from Z_mis^{-1}(init) (16 seeds, one per lane, picked by ds_bpermute), its lines keep
-  // E = L + mis bytes (keep_sel: the bytes past E are whatever follows, all masked) and its
-  // padding C - E travels with its value to the flush (the general loop's clamped loads, record
-  // arithmetic and per-tile seed inverses ran 200 / 1,000 / 1,500 / 3,000-B packed messages at
-  // 33-43 % of HBM, r05cc).
+  // repack loop): a uniform batch of messages of L <= C bytes on 16-B
+  // boundaries -- the tile's address from m * stride, one address and 8 immediate-offset loads
+  // (reading C bytes per message: past L they are the next messages' bytes, masked), one padding
+  // p = C - L for every message, no codes. A tile holding a message whose C bytes would reach
+  // past the batch (the last few) takes the clamped loads instead.
   const u64 uL = a.ulen;
   const u32 upad = C - (u32)(uL < C ? uL : C);
-  const bool ua = (a.ustride & 15u) == 0;  // every message at offset 0 of its first block
-  u32 useed = 0;  // (!ua) lane l: Z_{l & 15}^{-1}(init)
   // the last message whose C-byte read stays inside the batch (none: -1)
   const int64_t usafe = upad == 0u ? (int64_t)count - 1
                         : a.ustride == 0 ? -1
                                          : (int64_t)count - 1 - (int64_t)((upad + a.ustride - 1) / a.ustride);
-  auto u_msg = [&](u32 k) __attribute__((always_inline)) {
-    const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
-    const u64 m = msg_of(kk);
-    return m < count ? m : count - 1;
-  };
   auto u_off = [&](u32 k) __attribute__((always_inline)) {
-    u64 off = ((u_msg(k) * a.ustride) & ~(u64)15) + 128u * li;
+    const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
+    u64 m = msg_of(kk);
+    m = m < count ? m : count - 1;
+    u64 off = m * a.ustride + 128u * li;
     asm volatile("" : "+v"(off));
     return off;
   };
@@ -505,29 +494,24 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     if (u_safe(k)) {
       load_at(D, q);
     } else {
-      const u64 so = u_msg(k) * a.ustride;
-      load_lines(D, so, (u32)uL + ((u32)so & 15u));
+      const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
+      u64 m = msg_of(kk);
+      m = m < count ? m : count - 1;
+      load_lines(D, m * a.ustride, (u32)uL);
     }
   };
   auto process_u = [&](const u32x4 (&cur)[8], u32 k) __attribute__((always_inline)) {
     u32x4 d[8];
 #pragma unroll
     for (int b = 0; b < 8; b++) d[b] = cur[b];
-    const u32 mis = ua ? 0u : (u32)(msg_of(k) * a.ustride) & 15u;
-    const u32 E = (u32)uL + mis;
-    const int v0 = (int)E - 128 * (int)li;
-    const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
-    u32 seed = a.init;
-    if (ua) {
-      if (upad != 0u) keep_bytes(d, 0u, hi);  // (uniform) the bytes from L on
-    } else {
-      keep_sel(d, li == 0u ? mis : 0u, hi);
-      seed = bperm(mis, useed);
+    if (upad != 0u) {  // (uniform) the bytes from L on
+      const int v0 = (int)uL - 128 * (int)li;
+      keep_bytes(d, 0u, v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0));
     }
-    const u32 crc = G == 1 && __all(E <= 64u) ? line_crc32_lo(d, seed, lc0, lc1, z64)
-                                              : line_crc32_2chain(d, li == 0u ? seed : 0u, lc0, lc1, z64);
+    const u32 crc = G == 1 && uL <= 64u ? line_crc32_lo(d, a.init, lc0, lc1, z64)
+                                        : line_crc32_2chain(d, li == 0u ? a.init : 0u, lc0, lc1, z64);
     const u32 v = msg_value(crc);
-    const u32 code = (k < nk && msg_of(k) < count) ? C - E : kCodeSkip;
+    const u32 code = (k < nk && msg_of(k) < count) ? 0u : kCodeSkip;
     if (li == (u32)G - 1u) lds_st64(sring + 8u * ((k & (W - 1u)) * M + mj), (u64)v | ((u64)code << 32));
   };
   auto flush_u = [&](u32 kf, u32 nt) __attribute__((always_inline)) {
@@ -535,11 +519,63 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     const u32 hh = (u32)lane % M, ti = (u32)lane / M;
     const u64 e = lds_ld64(sring + 8u * (u32)lane);
     const u64 m = M * (t0 + (u64)(kf + ti) * nw) + hh;
+    const u32 r = upad ? inv_bits((u32)e, upad, kSmallInvOps) : (u32)e;
+    if (ti < nt && (u32)(e >> 32) == 0u) a.out[m] = r ^ a.final_xor;
+    wave_lds_sync();
+  };
+  // PACKED UNIFORM FAST (round 6, VERDICT r05 item 4: packed application buffers): the same loop
+  // for strides that are not multiples of 16 -- message m starts mis = (m * stride) & 15 bytes
+  // into its first block, one address and 8 immediate-offset loads per lane from that block
+  // (C >= L + 15 from the host), its line 0 masks the mis bytes and starts from Z_mis^{-1}(init)
+  // (16 seeds, one per lane, picked by ds_bpermute), its lines keep E = L + mis bytes (keep_sel:
+  // the bytes past E are whatever follows, all masked) and its padding C - E travels with its
+  // value to the flush (the general loop's clamped loads, record arithmetic and per-tile seed
+  // inverses ran 200 / 1,000 / 1,500 / 3,000-B packed messages at 33-43 % of HBM, r05cc). The
+  // 16-B-stride loop above stays as it was: sharing one body cost it 7 us per 256 MiB of 2,000 and
+  // 4,000-B messages (r06k).
+  u32 useed = 0;  // lane l: Z_{l & 15}^{-1}(init)
+  auto u_off_p = [&](u32 k) __attribute__((always_inline)) {
+    const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
+    u64 m = msg_of(kk);
+    m = m < count ? m : count - 1;
+    u64 off = ((m * a.ustride) & ~(u64)15) + 128u * li;
+    asm volatile("" : "+v"(off));
+    return off;
+  };
+  auto u_load_p = [&](u32x4 (&D)[8], u32 k, u64 q) __attribute__((always_inline)) {
+    if (u_safe(k)) {
+      load_at(D, q);
+    } else {
+      const u32 kk = k < nk ? k : (nk ? nk - 1 : 0u);
+      u64 m = msg_of(kk);
+      m = m < count ? m : count - 1;
+      const u64 so = m * a.ustride;
+      load_lines(D, so, (u32)uL + ((u32)so & 15u));
+    }
+  };
+  auto process_up = [&](const u32x4 (&cur)[8], u32 k) __attribute__((always_inline)) {
+    u32x4 d[8];
+#pragma unroll
+    for (int b = 0; b < 8; b++) d[b] = cur[b];
+    const u32 mis = (u32)(msg_of(k) * a.ustride) & 15u;
+    const u32 E = (u32)uL + mis;
+    const int v0 = (int)E - 128 * (int)li;
+    keep_sel(d, li == 0u ? mis : 0u, v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0));
+    const u32 seed = bperm(mis, useed);
+    const u32 crc = G == 1 && __all(E <= 64u) ? line_crc32_lo(d, seed, lc0, lc1, z64)
+                                              : line_crc32_2chain(d, li == 0u ? seed : 0u, lc0, lc1, z64);
+    const u32 v = msg_value(crc);
+    const u32 code = (k < nk && msg_of(k) < count) ? C - E : kCodeSkip;
+    if (li == (u32)G - 1u) lds_st64(sring + 8u * ((k & (W - 1u)) * M + mj), (u64)v | ((u64)code << 32));
+  };
+  auto flush_up = [&](u32 kf, u32 nt) __attribute__((always_inline)) {
+    wave_lds_sync();
+    const u32 hh = (u32)lane % M, ti = (u32)lane / M;
+    const u64 e = lds_ld64(sring + 8u * (u32)lane);
+    const u64 m = M * (t0 + (u64)(kf + ti) * nw) + hh;
     const u32 code = (u32)(e >> 32);
     const bool live = ti < nt && code != kCodeSkip;
-    // (a batch on 16-B strides has one padding: its bits only)
-    const u32 r = ua ? (upad ? inv_bits((u32)e, upad, kSmallInvOps) : (u32)e)
-                     : inv_bits((u32)e, live ? code : 0u, kSmallInvOps);
+    const u32 r = inv_bits((u32)e, live ? code : 0u, kSmallInvOps);
     if (live) a.out[m] = r ^ a.final_xor;
     wave_lds_sync();
   };
@@ -765,7 +801,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // r05z)
   const bool conf = !flive || (wL == (u64)kSmallMaxExt && (wS & 15u) == 0 && (!SLOT || wL <= a.max_len));
   const bool fast = G == 32 && nk <= kSmallRingTiles && __ballot(!conf) == 0;
-  const bool fastu = !SLOT && a.offsets == nullptr && a.ulen != 0 && a.ulen + ((a.ustride & 15u) ? 15u : 0u) <= (u64)C;
+  const bool ua = (a.ustride & 15u) == 0 && ((uintptr_t)base & 15u) == 0;  // 16-B strides
+  const bool fastu = !SLOT && a.offsets == nullptr && a.ulen != 0 && a.ulen + (ua ? 0u : 15u) <= (u64)C;
   bool repack = false;
   u32 rcode0 = 0;  // (REPACK) this lane's entry's code when it has no lanes, written after tile 0's loads
   // REPACK2 (slot kernel, G = 32; grid-uniform: the host gives no slot wave more than
@@ -849,8 +886,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       // every wave votes; a FAST wave does nothing else here (its bookkeeping only if the
       // workgroup repacks: r2_fast after the barrier), the config-S list's prologue stays short
       if (lane == 0) lds_st(sbase + kRp2Misc + 32u + 4u * wid, fast ? 0u : 1u);
-      if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
-      if (threadIdx.x == 0) lds_st(sbase + kRp2Misc + 96u, 0u);  // the tile ticket
       if (!fast) {
         u32 incl;
         const u64 Ew = wL + (wS & 15u);
@@ -997,8 +1032,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   u32 k = 0;
   if (rp2) {
     if constexpr (SLOT && G == 32) {
-      // the FAST waves' bookkeeping, now that the workgroup repacks
+      // the FAST waves' bookkeeping, now that the workgroup repacks; the shared tiles' start
+      // marks and the ticket zeroed (before any wave sets them, after the barrier below)
       if (fast) r2_fast();
+      if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
+      if (threadIdx.x == 0) lds_st(sbase + kRp2Misc + 96u, 0u);  // the tile ticket
       __syncthreads();
       // Q: every wave computes its first Q lines itself (local tiles), Q = the workgroup's least
       // wave rounded down to whole tiles, at least one tile; the rest of every wave's lines form
@@ -1235,7 +1273,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       stamp_tile0();
       process_rp(A, sc, Lc, pc);
     }
-  } else if (fastu) {
+  } else if (fastu && ua) {
     // the general loop's schedule (windows of W tiles) with the FAST loop's loads and compute
     for (; k + 1 < nk; k += 2) {
       const u64 qB = u_off(k + 1);
@@ -1260,6 +1298,32 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       stamp_tile0();
       if (k && (k & kWinMask) == 0u) flush_u(k - W, W);
       process_u(A, k);
+    }
+  } else if (fastu && !ua) {
+    // (packed strides: the same schedule)
+    for (; k + 1 < nk; k += 2) {
+      const u64 qB = u_off_p(k + 1);
+      issue_prio_hi();
+      drain_before_issue();  // tile k's lines
+      stamp_tile0();
+      u_load_p(B, k + 1, qB);
+      issue_prio_lo();
+      if (k && (k & kWinMask) == 0u) flush_up(k - W, W);
+      process_up(A, k);
+      const u64 qA = u_off_p(k + 2);
+      issue_prio_hi();
+      drain_before_issue();
+      stamp_tile0();
+      u_load_p(A, k + 2, qA);
+      issue_prio_lo();
+      if constexpr (W == 1) flush_up(k, 1u);
+      process_up(B, k + 1);
+    }
+    if (k < nk) {
+      drain_before_issue();
+      stamp_tile0();
+      if (k && (k & kWinMask) == 0u) flush_up(k - W, W);
+      process_up(A, k);
     }
   } else {
     // Ping-pong line buffers, loop unrolled by two, records one tile ahead of the lines; the
@@ -1309,7 +1373,10 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       flush_fast(nk);
     } else if (fastu) {
       const u32 kf = (nk - 1u) & ~kWinMask;
-      flush_u(kf, nk - kf);
+      if (ua)
+        flush_u(kf, nk - kf);
+      else
+        flush_up(kf, nk - kf);
     } else {
       const u32 kf = (nk - 1u) & ~kWinMask;  // the last window, not flushed yet
       flush(kf, nk - kf);
