@@ -244,7 +244,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // S (prefix + 48) and whether the flag was set. Prefixes are 8-B aligned (the C ABI's rule):
   // 8-B loads.
   constexpr u32 kW = kSlotFusedMaxMeta / 4 + 2;
-  auto span_load = [&](const uint8_t* pfx, u32 (&w)[14], u32 (&W1)[kW]) __attribute__((always_inline)) {
+  auto span_load = [&](const uint8_t* pfx, u32 (&w)[14]) __attribute__((always_inline)) {
     const u64* q = reinterpret_cast<const u64*>(pfx);
 #pragma unroll
     for (int i = 0; i < 7; i++) {
@@ -252,18 +252,12 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       w[2 * i] = (u32)x;
       w[2 * i + 1] = (u32)(x >> 32);
     }
-#pragma unroll
-    for (u32 j = 0; j < kW; j++) W1[j] = 0u;
-    if (a.metadata_size) {  // wave-uniform: span 1 after the checksum area (crc_uniform.hip)
-      const u32 o1 = 48u + a.checksum_size, sh = o1 & 3u, ms = a.metadata_size;
-      const u32 nwords = (sh + ms + 3u) >> 2;
-      const u32* p1 = reinterpret_cast<const u32*>(pfx + (o1 & ~3u));
-#pragma unroll
-      for (u32 j = 0; j < kW; j++)
-        if (j < nwords) W1[j] = p1[j];
-    }
+    asm volatile("" ::"v"(q));  // (the address lives past the loads: no load's destination, load_at)
   };
-  auto span_hash = [&](u32 (&w)[14], const u32 (&W1)[kW], u32& F, u32& S, bool& has) __attribute__((always_inline))
+  // (span 1, the metadata, is loaded by the hash itself: the prologue keeps only the 14 prefix
+  // words live across its barrier; r06: with kW more, the slot kernel spilled VGPRs to scratch
+  // and the reload after the barrier waited for every load, tile 0's lines included)
+  auto span_hash = [&](const uint8_t* pfx, u32 (&w)[14], u32& F, u32& S, bool& has) __attribute__((always_inline))
       -> u32 {
     // w[0] (the padding) and w[13] (not hashed) stay live until here: hipcc reuses a dead
     // destination of a pending prefix load for other values, and the reuse waits for that load
@@ -276,8 +270,14 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     u32 hh = 0xFFFFFFFFu;
 #pragma unroll
     for (int i = 1; i < 12; i++) hh = step4(hh ^ w[i], lc0, lc1);
-    if (a.metadata_size) {  // realigned with a uniform byte shift; full words by step4, the tail by bytes
+    if (a.metadata_size) {  // wave-uniform: span 1 after the checksum area (crc_uniform.hip),
+                            // realigned with a uniform byte shift; full words by step4, the tail by bytes
       const u32 o1 = 48u + a.checksum_size, sh = o1 & 3u, ms = a.metadata_size;
+      const u32 nwords = (sh + ms + 3u) >> 2;
+      const u32* p1 = reinterpret_cast<const u32*>(pfx + (o1 & ~3u));
+      u32 W1[kW];
+#pragma unroll
+      for (u32 j = 0; j < kW; j++) W1[j] = j < nwords ? p1[j] : 0u;
       u32 tail = 0;
 #pragma unroll
       for (u32 j = 0; j + 1 < kW; j++) {
@@ -290,9 +290,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     return hh;
   };
   auto span_crc = [&](const uint8_t* pfx, u32& F, u32& S, bool& has) __attribute__((always_inline)) -> u32 {
-    u32 w[14], W1[kW];
-    span_load(pfx, w, W1);
-    return span_hash(w, W1, F, S, has);
+    u32 w[14];
+    span_load(pfx, w);
+    return span_hash(pfx, w, F, S, has);
   };
 
   // A message longer than a half-tile, by the whole wave (s, L, P wave-uniform): 8 KiB chunks
@@ -685,7 +685,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // next tile's loads are issued (flush_issue), so the flush's reads wait for neither a record
   // round trip nor that tile (vmcnt retires in order); flush_any(..., true) hashes them.
   u64 Pn = 0, Pc = 0;  // the next / current window's prefix offset of this lane's entry
-  u32 fw[14], fW1[kW];
+  u32 fw[14];
   auto win_pref = [&](u32 kf) __attribute__((always_inline)) -> u64 {
     const u32 ti = (u32)lane / M, hh = (u32)lane % M;
     const u64 m = M * (t0 + (u64)(kf + ti) * nw) + hh;
@@ -694,7 +694,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   auto flush_issue = [&](u32 kf) __attribute__((always_inline)) {
     if (kf != 0) {
       Pc = Pn;
-      span_load(base + Pc - a.pdelta, fw, fW1);
+      span_load(base + Pc - a.pdelta, fw);
     }
     Pn = win_pref(kf + W);
   };
@@ -730,7 +730,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
                                    : safe;  // (a read-only block)
       u32 F = eF, S = eS, H = eH;
       bool has = ehas;
-      if (kf != 0 && SUBSPACE_SMALL_VARIANT != 3) H = pre ? span_hash(fw, fW1, F, S, has) : span_crc(pfx, F, S, has);
+      if (kf != 0 && SUBSPACE_SMALL_VARIANT != 3) H = pre ? span_hash(pfx, fw, F, S, has) : span_crc(pfx, F, S, has);
       // Z_p(crc_raw(H, payload)) = Z_C(Z_mis^{-1}(H)) ^ V, then Z_p undone
       const u32 Hm = inv_bits(H, half ? (code >> 12) & 15u : 0u, 4);
       const u32 X = opmul(sbase, G == 32 ? kUniSlotOpZ4096 : kSmallOpZC, Hm) ^ v;
@@ -974,9 +974,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     fetch(0, sA, LA);
     fetch(1, sB, LB);
   }
-  u32 pwords[14], pmeta[kW];
+  u32 pwords[14];
   if constexpr (SLOT) {
-    if (SUBSPACE_SMALL_VARIANT != 1) span_load(flive ? base + fpre - a.pdelta : safe, pwords, pmeta);
+    if (SUBSPACE_SMALL_VARIANT != 1) span_load(flive ? base + fpre - a.pdelta : safe, pwords);
     __builtin_amdgcn_sched_barrier(0);
   }
   u32x4 A[8], B[8];
@@ -987,13 +987,19 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     rp_rec(pc, sc, Lc);
     load_lines_at(A, sc, rp_ext(sc, Lc, pc), (pc >> 8) & 31u);
     if (rcode0) lds_st64(sring + 8u * (u32)lane, (u64)rcode0 << 32);
-  } else if (wg2 && !fast) {
-#ifdef SUBSPACE_RP2_DEBUG
-    rp2_check("local", ls, lE, lli, 32u * wid + lsrc);
-#endif
-    load_lines_at(A, ls, lE, lli);  // REPACK2: the wave's local tile
   } else {
-    load_lines(A, sc, ext(0, sc, Lc));  // (FAST: the same addresses as load_at's)
+    // REPACK2: the wave's local tile; else tile 0 (FAST: the same addresses as load_at's). One
+    // load site: with two, hipcc's wait counts merged at the join lost track of the prologue's
+    // prefix loads and waited for all of them before tile 0's addresses (r06)
+    const bool lt = wg2 && !fast;
+    u32 E0 = ext(0, sc, Lc);
+    if (lt) {
+#ifdef SUBSPACE_RP2_DEBUG
+      rp2_check("local", ls, lE, lli, 32u * wid + lsrc);
+#endif
+      E0 = lE;
+    }
+    load_lines_at(A, lt ? ls : sc, E0, lt ? lli : li);
   }
   if constexpr (SUBSPACE_SMALL_EARLY_TILE0) fill.store(sbase);
   __syncthreads();
@@ -1002,7 +1008,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // wave's tile 0 -- ~1 us per slot-list call, r05bm)
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (probe) pt[2] = __builtin_amdgcn_s_memrealtime();
-  if constexpr (SLOT && SUBSPACE_SMALL_VARIANT != 1) eH = span_hash(pwords, pmeta, eF, eS, ehas);
+  if constexpr (SLOT && SUBSPACE_SMALL_VARIANT != 1) eH = span_hash(flive ? base + fpre - a.pdelta : safe, pwords, eF, eS, ehas);
   if (fastu && !ua) useed = inv_bits(a.init, (u32)lane & 15u, 4);  // the 16 head seeds, one per lane
 
   // REPACK2 after the barrier: a workgroup whose waves are not all FAST packs its messages as one
@@ -1032,9 +1038,48 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   u32 k = 0;
   if (rp2) {
     if constexpr (SLOT && G == 32) {
-      // the FAST waves' bookkeeping, now that the workgroup repacks; the shared tiles' start
-      // marks and the ticket zeroed (before any wave sets them, after the barrier below)
-      if (fast) r2_fast();
+      auto process2 = [&](const u32x4 (&cur)[8], u64 ms, u32 mE, u32 mli, u32 me, u32 mst)
+                          __attribute__((always_inline)) {
+        const u32 mis = (u32)ms & 15u;
+        u32x4 d[8];
+#pragma unroll
+        for (int b = 0; b < 8; b++) d[b] = cur[b];
+        const bool head = mE != 0u && mis != 0u && mli == 0u;
+        const int v0 = (int)mE - 128 * (int)mli;
+        const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
+        if (__any(head || hi < 128u)) keep_sel(d, head ? mis : 0u, hi);
+        u32 seed = a.init;
+        if (seed != 0u && __any(head)) seed = inv_bits(seed, mis, 4);
+        const u32 crc = line_crc32_2chain(d, mli == 0u ? seed : 0u, lc0, lc1, z64);
+        const u32 n = (mE + 127u) >> 7;
+        u32 v = lane_shift(sbase + kLdsOps + 4u * ((n - 1u - mli) & 31u), crc);
+        v = mE ? v : 0u;
+        const u32 P = wave_scan(v, true);
+        const u32 pv = bperm(mst ? mst - 1u : 0u, P);
+        const u32 seg = P ^ (mst ? pv : 0u);
+        if (mE != 0u && (mli == n - 1u || lane == 63))
+          __hip_atomic_fetch_xor(reinterpret_cast<lds_u32_t*>((uintptr_t)(sbase + kRp2Ring + 8u * me)), seg,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      };
+      // the FAST waves' bookkeeping, now that the workgroup repacks; every wave's ring entries
+      // (codes, values 0) and its local tile 0 (loaded before the barrier; a FAST wave's is its
+      // FAST tile 0, mapped here; Q >= 64, so the tile does not depend on Q) while the others
+      // finish theirs; the shared tiles' start marks and the ticket zeroed (before any wave sets
+      // them, after the barrier below)
+      if (fast) {
+        r2_fast();
+        rank_lanes();
+        const u32 t0l = (u32)__builtin_amdgcn_readlane((int)(r2x + r2n), 63);
+        local_map(0u, t0l < 64u ? t0l : 64u, lsrc, ls, lE, lli, lst);
+      }
+      if (lane < 32) {
+        const u32 code = r2code ? r2code : ((128u * r2n - r2E) | (((u32)wS & 15u) << 12) | (r2n << 16));
+        lds_st64(sbase + kRp2Ring + 8u * (32u * wid + (u32)lane), (u64)code << 32);
+      }
+      drain_before_issue();
+      stamp_tile0();
+      process2(A, ls, lE, lli, 32u * wid + lsrc, lst);
+      r2tiles++;
       if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
       if (threadIdx.x == 0) lds_st(sbase + kRp2Misc + 96u, 0u);  // the tile ticket
       __syncthreads();
@@ -1066,8 +1111,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       const u32 r = rbase + (u32)__builtin_popcountll(__ballot(shn != 0u) & ((1ull << lane) - 1ull));
       if (lane < 32) {
         const u32 q = 32u * wid + (u32)lane;
-        const u32 code = r2code ? r2code : ((128u * r2n - r2E) | (((u32)wS & 15u) << 12) | (r2n << 16));
-        lds_st64(sbase + kRp2Ring + 8u * q, (u64)code << 32);
         if (shn) {
           lds_st64(sbase + kRp2EntS + 8u * r, wS | ((u64)q << 56));
           lds_st(sbase + kRp2EntM + 4u * r, r2E | (start << 13) | ((a0 - r2x) << 26));
@@ -1077,40 +1120,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
           if (64u * jb < start + shn) lds_st(sbase + kRp2First + 4u * jb, r);
         }
       }
-      auto process2 = [&](const u32x4 (&cur)[8], u64 ms, u32 mE, u32 mli, u32 me, u32 mst)
-                          __attribute__((always_inline)) {
-        const u32 mis = (u32)ms & 15u;
-        u32x4 d[8];
-#pragma unroll
-        for (int b = 0; b < 8; b++) d[b] = cur[b];
-        const bool head = mE != 0u && mis != 0u && mli == 0u;
-        const int v0 = (int)mE - 128 * (int)mli;
-        const u32 hi = v0 <= 0 ? 0u : (v0 >= 128 ? 128u : (u32)v0);
-        if (__any(head || hi < 128u)) keep_sel(d, head ? mis : 0u, hi);
-        u32 seed = a.init;
-        if (seed != 0u && __any(head)) seed = inv_bits(seed, mis, 4);
-        const u32 crc = line_crc32_2chain(d, mli == 0u ? seed : 0u, lc0, lc1, z64);
-        const u32 n = (mE + 127u) >> 7;
-        u32 v = lane_shift(sbase + kLdsOps + 4u * ((n - 1u - mli) & 31u), crc);
-        v = mE ? v : 0u;
-        const u32 P = wave_scan(v, true);
-        const u32 pv = bperm(mst ? mst - 1u : 0u, P);
-        const u32 seg = P ^ (mst ? pv : 0u);
-        if (mE != 0u && (mli == n - 1u || lane == 63))
-          __hip_atomic_fetch_xor(reinterpret_cast<lds_u32_t*>((uintptr_t)(sbase + kRp2Ring + 8u * me)), seg,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      };
-      // local tile 0 (loaded before the barrier; a FAST wave's is its FAST tile 0, mapped here)
       const u32 tot = tw[wid];
       const u32 nloc = tot < Q ? tot : Q, nlt = (nloc + 63u) >> 6;  // local lines, tiles
-      if (fast) {
-        rank_lanes();
-        local_map(0u, nloc < 64u ? nloc : 64u, lsrc, ls, lE, lli, lst);
-      }
-      drain_before_issue();
-      stamp_tile0();
-      process2(A, ls, lE, lli, 32u * wid + lsrc, lst);
-      r2tiles++;
       const u32 ntl = (T + 63u) >> 6;  // shared tiles of the workgroup
       if (ntl) __syncthreads();       // the shared tables
       const u32 tick = sbase + kRp2Misc + 96u;
