@@ -73,7 +73,14 @@
 #ifndef SUBSPACE_SMALL_EARLY_TILE0
 #define SUBSPACE_SMALL_EARLY_TILE0 0
 #endif
-#if (SUBSPACE_SMALL_VARIANT != 0 || SUBSPACE_SMALL_EARLY_TILE0 != 0) && !defined(SUBSPACE_AB_BUILD)
+#ifndef SUBSPACE_SMALL_AB_T0SITE
+#define SUBSPACE_SMALL_AB_T0SITE 0
+#endif
+#ifndef SUBSPACE_SMALL_AB_T0WAIT
+#define SUBSPACE_SMALL_AB_T0WAIT 0
+#endif
+#if (SUBSPACE_SMALL_VARIANT != 0 || SUBSPACE_SMALL_EARLY_TILE0 != 0 || SUBSPACE_SMALL_AB_T0SITE != 0 || \
+     SUBSPACE_SMALL_AB_T0WAIT != 0) && !defined(SUBSPACE_AB_BUILD)
 #error "SUBSPACE_SMALL_VARIANT is a timing-only A/B knob (tools/ab_lib.sh defines SUBSPACE_AB_BUILD)"
 #endif
 
@@ -992,6 +999,12 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     // load site: with two, hipcc's wait counts merged at the join lost track of the prologue's
     // prefix loads and waited for all of them before tile 0's addresses (r06)
     const bool lt = wg2 && !fast;
+#if SUBSPACE_SMALL_AB_T0SITE
+    if (lt)
+      load_lines_at(A, ls, lE, lli);
+    else
+      load_lines(A, sc, ext(0, sc, Lc));
+#else
     u32 E0 = ext(0, sc, Lc);
     if (lt) {
 #ifdef SUBSPACE_RP2_DEBUG
@@ -1000,6 +1013,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       E0 = lE;
     }
     load_lines_at(A, lt ? ls : sc, E0, lt ? lli : li);
+#endif
   }
   if constexpr (SUBSPACE_SMALL_EARLY_TILE0) fill.store(sbase);
   __syncthreads();
@@ -1008,6 +1022,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // wave's tile 0 -- ~1 us per slot-list call, r05bm)
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (probe) pt[2] = __builtin_amdgcn_s_memrealtime();
+  if constexpr (SLOT && SUBSPACE_SMALL_AB_T0WAIT) drain_before_issue();
   if constexpr (SLOT && SUBSPACE_SMALL_VARIANT != 1) eH = span_hash(flive ? base + fpre - a.pdelta : safe, pwords, eF, eS, ehas);
   if (fastu && !ua) useed = inv_bits(a.init, (u32)lane & 15u, 4);  // the 16 head seeds, one per lane
 
@@ -1069,15 +1084,27 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       if (fast) {
         r2_fast();
         rank_lanes();
-        const u32 t0l = (u32)__builtin_amdgcn_readlane((int)(r2x + r2n), 63);
-        local_map(0u, t0l < 64u ? t0l : 64u, lsrc, ls, lE, lli, lst);
       }
+      const u32 tot0 = (u32)__builtin_amdgcn_readlane((int)(r2x + r2n), 63);  // the wave's lines
+      if (fast) local_map(0u, tot0 < 64u ? tot0 : 64u, lsrc, ls, lE, lli, lst);
       if (lane < 32) {
         const u32 code = r2code ? r2code : ((128u * r2n - r2E) | (((u32)wS & 15u) << 12) | (r2n << 16));
         lds_st64(sbase + kRp2Ring + 8u * (32u * wid + (u32)lane), (u64)code << 32);
       }
+      // local tile 1 on speculation (the wave's lines 64 .. 127; they are local when Q >= 128,
+      // known after the barrier below): its loads go out before tile 0's compute, as the loop's
+      // next tile does (a fixed-size list: every wave's tiles local, none waits a round trip here)
+      u32 s1src = 0, E1 = 0, li1 = 0, st1 = 0;
+      u64 s1 = 0;
+      local_map(1u, tot0 < 128u ? tot0 : 128u, s1src, s1, E1, li1, st1);
+#ifdef SUBSPACE_RP2_DEBUG
+      rp2_check("local1", s1, E1, li1, 32u * wid + s1src);
+#endif
+      issue_prio_hi();
       drain_before_issue();
       stamp_tile0();
+      load_lines_at(B, s1, E1, li1);
+      issue_prio_lo();
       process2(A, ls, lE, lli, 32u * wid + lsrc, lst);
       r2tiles++;
       if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
@@ -1127,7 +1154,8 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       const u32 tick = sbase + kRp2Misc + 96u;
       // the wave's next tile: its local tiles 1 .. nlt - 1, then shared tiles from the ticket; v
       // false: none left (E 0: the loads read the step table)
-      u32 jl = 1;
+      const bool use1 = Q >= 128u;  // B holds local tile 1
+      u32 jl = use1 ? 2u : 1u;
       auto next = [&](bool& v, u64& ms, u32& mE, u32& mli, u32& me, u32& mst) __attribute__((always_inline)) {
         if (jl < nlt) {
           u32 src;
@@ -1169,19 +1197,26 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
         rp2_check("shared", ms, mE, mli, me);
 #endif
       };
-      bool va, vb;
-      u64 s_a, s_b;
-      u32 E_a, li_a, e_a, st_a, E_b, li_b, e_b, st_b;
-      next(va, s_a, E_a, li_a, e_a, st_a);
-      load_lines_at(A, s_a, E_a, li_a);
-      while (va) {
-        next(vb, s_b, E_b, li_b, e_b, st_b);
-        issue_prio_hi();
-        drain_before_issue();
-        load_lines_at(B, s_b, E_b, li_b);
-        issue_prio_lo();
-        process2(A, s_a, E_a, li_a, e_a, st_a);
-        r2tiles++;
+      bool va = false, vb = use1;
+      u64 s_a = 0, s_b = s1;
+      u32 E_a = 0, li_a = 0, e_a = 0, st_a = 0, E_b = E1, li_b = li1, e_b = 32u * wid + s1src, st_b = st1;
+      if (!use1) {  // (B's lines are the shared stream's: dropped)
+        next(va, s_a, E_a, li_a, e_a, st_a);
+        load_lines_at(A, s_a, E_a, li_a);
+      }
+      bool inB = use1;  // the ping-pong enters at its second half
+      for (;;) {
+        if (!inB) {
+          if (!va) break;
+          next(vb, s_b, E_b, li_b, e_b, st_b);
+          issue_prio_hi();
+          drain_before_issue();
+          load_lines_at(B, s_b, E_b, li_b);
+          issue_prio_lo();
+          process2(A, s_a, E_a, li_a, e_a, st_a);
+          r2tiles++;
+        }
+        inB = false;
         if (!vb) break;
         next(va, s_a, E_a, li_a, e_a, st_a);
         issue_prio_hi();

@@ -552,7 +552,8 @@ def small_kernel_repack2(starts, lengths, grid, rng):
     tiles, at least 64): lane P of local tile j takes the entry of rank k - 1, k = the entries with
     lines starting before the tile + popcount(the tile's start marks & (2 << P) - 1), or line / n
     when the wave's entries are lanes 0, 1, ... with one line count; ranks map to lanes as the
-    kernel's ds_permute does. The other lines of every wave form the shared stream (wave after
+    kernel's ds_permute does; when Q = 64 the wave's lines 64 .. 127, loaded on speculation before
+    Q is known, are loads only. The other lines of every wave form the shared stream (wave after
     wave); entries with shared lines are
     ranked r = 0, 1, ... in the same order (record at r, ring entry in the offset's top byte,
     first shared position and first line), the shared tiles' start marks S_j and first entries
@@ -602,6 +603,7 @@ def small_kernel_repack2(starts, lengths, grid, rng):
         tmin = min(tots)
         Q = tmin & ~63 if tmin >= 128 else 64
         shared = []  # (q, m, E, n, first shared line) in stream order
+        spec = []  # (message, block) loads of a speculative local tile 1 the workgroup dropped
         for ents in waves:
             r2x = [int(x) for x in np.concatenate([[0], np.cumsum([n for *_, n in ents])])[:-1]]
             tot = sum(n for *_, n in ents)
@@ -624,6 +626,18 @@ def small_kernel_repack2(starts, lengths, grid, rng):
                     q, m, E, n = ents[i]
                     lanes[lane] = (q, m, E, n, P - r2x[i], max(r2x[i] - 64 * j, 0))
                 emit(lanes)
+            if Q < 128:  # local tile 1 loaded on speculation (lines 64 .. min(tot, 128)), then dropped
+                for P in range(64, min(tot, 128)):
+                    if runi:
+                        k = P // ents[0][3] + 1
+                    else:
+                        k = sum(1 for i in withl if r2x[i] <= P)
+                    i = withl[k - 1]
+                    q, m, E, n = ents[i]
+                    li = P - r2x[i]
+                    assert 0 <= li < n
+                    for blk in range(8):
+                        spec.append((m, (int(starts[m]) & ~15) + min(128 * li + 16 * blk, (E - 1) & ~15)))
             cnt = sum(1 for i in range(32) if ents[i][3] and r2x[i] + ents[i][3] > Q)
             got = 0
             for i in range(32):
@@ -672,6 +686,8 @@ def small_kernel_repack2(starts, lengths, grid, rng):
             for i, (q, m, E, n, li, mst) in lanes.items():
                 if li == n - 1 or i == 63:
                     ring[q] ^= scan[i] ^ (scan[mst - 1] if mst else 0)
+        for m, addr in spec:
+            yield "load", m, addr
         for ents in waves:
             for q, m, E, n in ents:
                 if n:
