@@ -73,14 +73,7 @@
 #ifndef SUBSPACE_SMALL_EARLY_TILE0
 #define SUBSPACE_SMALL_EARLY_TILE0 0
 #endif
-#ifndef SUBSPACE_SMALL_AB_T0SITE
-#define SUBSPACE_SMALL_AB_T0SITE 0
-#endif
-#ifndef SUBSPACE_SMALL_AB_T0WAIT
-#define SUBSPACE_SMALL_AB_T0WAIT 0
-#endif
-#if (SUBSPACE_SMALL_VARIANT != 0 || SUBSPACE_SMALL_EARLY_TILE0 != 0 || SUBSPACE_SMALL_AB_T0SITE != 0 || \
-     SUBSPACE_SMALL_AB_T0WAIT != 0) && !defined(SUBSPACE_AB_BUILD)
+#if (SUBSPACE_SMALL_VARIANT != 0 || SUBSPACE_SMALL_EARLY_TILE0 != 0) && !defined(SUBSPACE_AB_BUILD)
 #error "SUBSPACE_SMALL_VARIANT is a timing-only A/B knob (tools/ab_lib.sh defines SUBSPACE_AB_BUILD)"
 #endif
 
@@ -893,6 +886,11 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       // every wave votes; a FAST wave does nothing else here (its bookkeeping only if the
       // workgroup repacks: r2_fast after the barrier), the config-S list's prologue stays short
       if (lane == 0) lds_st(sbase + kRp2Misc + 32u + 4u * wid, fast ? 0u : 1u);
+      // the shared tiles' start marks and the tile ticket, zeroed before any wave sets them
+      // (after the barrier; the FAST waves' rings, the only other users of this LDS, start after
+      // it too and do not overlap them)
+      if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
+      if (threadIdx.x == 0) lds_st(sbase + kRp2Misc + 96u, 0u);
       if (!fast) {
         u32 incl;
         const u64 Ew = wL + (wS & 15u);
@@ -995,25 +993,17 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     load_lines_at(A, sc, rp_ext(sc, Lc, pc), (pc >> 8) & 31u);
     if (rcode0) lds_st64(sring + 8u * (u32)lane, (u64)rcode0 << 32);
   } else {
-    // REPACK2: the wave's local tile; else tile 0 (FAST: the same addresses as load_at's). One
-    // load site: with two, hipcc's wait counts merged at the join lost track of the prologue's
-    // prefix loads and waited for all of them before tile 0's addresses (r06)
-    const bool lt = wg2 && !fast;
-#if SUBSPACE_SMALL_AB_T0SITE
-    if (lt)
-      load_lines_at(A, ls, lE, lli);
-    else
-      load_lines(A, sc, ext(0, sc, Lc));
-#else
-    u32 E0 = ext(0, sc, Lc);
-    if (lt) {
+    // REPACK2: the wave's local tile; else tile 0 (FAST: the same addresses as load_at's). (One
+    // load site with selected arguments measured slower on config S's list: 54.8 against 53.3 us
+    // per call, r06n)
+    if (wg2 && !fast) {
 #ifdef SUBSPACE_RP2_DEBUG
       rp2_check("local", ls, lE, lli, 32u * wid + lsrc);
 #endif
-      E0 = lE;
+      load_lines_at(A, ls, lE, lli);
+    } else {
+      load_lines(A, sc, ext(0, sc, Lc));
     }
-    load_lines_at(A, lt ? ls : sc, E0, lt ? lli : li);
-#endif
   }
   if constexpr (SUBSPACE_SMALL_EARLY_TILE0) fill.store(sbase);
   __syncthreads();
@@ -1022,7 +1012,6 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // wave's tile 0 -- ~1 us per slot-list call, r05bm)
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (probe) pt[2] = __builtin_amdgcn_s_memrealtime();
-  if constexpr (SLOT && SUBSPACE_SMALL_AB_T0WAIT) drain_before_issue();
   if constexpr (SLOT && SUBSPACE_SMALL_VARIANT != 1) eH = span_hash(flive ? base + fpre - a.pdelta : safe, pwords, eF, eS, ehas);
   if (fastu && !ua) useed = inv_bits(a.init, (u32)lane & 15u, 4);  // the 16 head seeds, one per lane
 
@@ -1037,12 +1026,13 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
   // the tile give the message's part in this tile, which the part's last lane XORs into the
   // message's LDS ring entry (two parts when the message straddles tiles). The entry then holds
   // V = Z_p(crc_raw(init, D)) with p = 128 n - E < 128, one padding for 7 bits at most.
-  bool rp2 = false;
+  bool rp2 = false, allv = false;  // (allv: every wave voted, none is FAST)
   u32 r2tiles = 0;  // (PROBE) packed tiles this wave computed
   if constexpr (SLOT && G == 32) {
     if (wg2) {
       const u32x4 va = lds_ld4(sbase + kRp2Misc + 32u), vb = lds_ld4(sbase + kRp2Misc + 48u);
       rp2 = rfl(va.x | va.y | va.z | va.w | vb.x | vb.y | vb.z | vb.w) != 0u;
+      allv = rfl((u32)(va.x && va.y && va.z && va.w && vb.x && vb.y && vb.z && vb.w)) != 0u;
     }
   }
   // PROBE: tile 0 landed (the first wait of whichever loop form runs; stamped once)
@@ -1078,9 +1068,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       };
       // the FAST waves' bookkeeping, now that the workgroup repacks; every wave's ring entries
       // (codes, values 0) and its local tile 0 (loaded before the barrier; a FAST wave's is its
-      // FAST tile 0, mapped here; Q >= 64, so the tile does not depend on Q) while the others
-      // finish theirs; the shared tiles' start marks and the ticket zeroed (before any wave sets
-      // them, after the barrier below)
+      // FAST tile 0, mapped here; Q >= 64, so the tile does not depend on Q)
       if (fast) {
         r2_fast();
         rank_lanes();
@@ -1091,36 +1079,49 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
         const u32 code = r2code ? r2code : ((128u * r2n - r2E) | (((u32)wS & 15u) << 12) | (r2n << 16));
         lds_st64(sbase + kRp2Ring + 8u * (32u * wid + (u32)lane), (u64)code << 32);
       }
-      // local tile 1 on speculation (the wave's lines 64 .. 127; they are local when Q >= 128,
-      // known after the barrier below): its loads go out before tile 0's compute, as the loop's
-      // next tile does (a fixed-size list: every wave's tiles local, none waits a round trip here)
+      // Q: every wave computes its first Q lines itself (local tiles), Q = the workgroup's least
+      // wave rounded down to whole tiles, at least one tile; the rest of every wave's lines form
+      // the shared stream, wave after wave. Known now when every wave voted (their totals and
+      // counts went to LDS before the prologue barrier); else after the FAST waves' bookkeeping
+      // barrier below.
+      u32 tw[8], Q = 64u;
+      auto read_q = [&]() __attribute__((always_inline)) {
+        const u32x4 ta = lds_ld4(sbase + kRp2Misc), tb = lds_ld4(sbase + kRp2Misc + 16u);
+        tw[0] = rfl(ta.x), tw[1] = rfl(ta.y), tw[2] = rfl(ta.z), tw[3] = rfl(ta.w);
+        tw[4] = rfl(tb.x), tw[5] = rfl(tb.y), tw[6] = rfl(tb.z), tw[7] = rfl(tb.w);
+        u32 tmin = tw[0];
+#pragma unroll
+        for (u32 w = 1; w < 8; w++) tmin = tw[w] < tmin ? tw[w] : tmin;
+        Q = tmin >= 128u ? tmin & ~63u : 64u;
+      };
+      if (allv) read_q();
+      // local tile 1 (the wave's lines 64 .. 127): its loads go out before tile 0's compute, as the
+      // loop's next tile does -- known local when every wave voted (Q >= 128), else on speculation
+      // for a wave with more than one tile of lines (local iff Q >= 128, known after the barrier)
+      bool use1 = allv ? Q >= 128u : tot0 > 64u;
       u32 s1src = 0, E1 = 0, li1 = 0, st1 = 0;
       u64 s1 = 0;
-      local_map(1u, tot0 < 128u ? tot0 : 128u, s1src, s1, E1, li1, st1);
+      if (use1) {
+        local_map(1u, tot0 < 128u ? tot0 : 128u, s1src, s1, E1, li1, st1);
 #ifdef SUBSPACE_RP2_DEBUG
-      rp2_check("local1", s1, E1, li1, 32u * wid + s1src);
+        rp2_check("local1", s1, E1, li1, 32u * wid + s1src);
 #endif
+      }
       issue_prio_hi();
       drain_before_issue();
       stamp_tile0();
-      load_lines_at(B, s1, E1, li1);
+      if (use1) load_lines_at(B, s1, E1, li1);
       issue_prio_lo();
       process2(A, ls, lE, lli, 32u * wid + lsrc, lst);
       r2tiles++;
-      if (threadIdx.x < 2u * kRp2MaxTiles) lds_st(sbase + kRp2Starts + 4u * threadIdx.x, 0u);
-      if (threadIdx.x == 0) lds_st(sbase + kRp2Misc + 96u, 0u);  // the tile ticket
-      __syncthreads();
-      // Q: every wave computes its first Q lines itself (local tiles), Q = the workgroup's least
-      // wave rounded down to whole tiles, at least one tile; the rest of every wave's lines form
-      // the shared stream, wave after wave. An entry's shared part (its lines from local position
-      // Q on) gets a rank among the entries with one, its record, its first shared position and
-      // the line it starts with; the shared tiles' start marks and first entries (by rank).
-      const u32x4 ta = lds_ld4(sbase + kRp2Misc), tb = lds_ld4(sbase + kRp2Misc + 16u);
-      const u32 tw[8] = {rfl(ta.x), rfl(ta.y), rfl(ta.z), rfl(ta.w), rfl(tb.x), rfl(tb.y), rfl(tb.z), rfl(tb.w)};
-      u32 tmin = tw[0];
-#pragma unroll
-      for (u32 w = 1; w < 8; w++) tmin = tw[w] < tmin ? tw[w] : tmin;
-      const u32 Q = tmin >= 128u ? tmin & ~63u : 64u;
+      if (!allv) {
+        __syncthreads();  // the FAST waves' totals and counts
+        read_q();
+        use1 = use1 && Q >= 128u;
+      }
+      // An entry's shared part (its lines from local position Q on) gets a rank among the entries
+      // with one, its record, its first shared position and the line it starts with; the shared
+      // tiles' start marks and first entries (by rank).
       const u32 qi = (Q >> 6) - 1u;  // (<= 15: a wave has at most 32 x 32 lines)
       u32 wbase = 0, T = 0, rbase = 0, NR = 0;
 #pragma unroll
@@ -1154,8 +1155,7 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       const u32 tick = sbase + kRp2Misc + 96u;
       // the wave's next tile: its local tiles 1 .. nlt - 1, then shared tiles from the ticket; v
       // false: none left (E 0: the loads read the step table)
-      const bool use1 = Q >= 128u;  // B holds local tile 1
-      u32 jl = use1 ? 2u : 1u;
+      u32 jl = use1 ? 2u : 1u;  // (use1: B holds local tile 1)
       auto next = [&](bool& v, u64& ms, u32& mE, u32& mli, u32& me, u32& mst) __attribute__((always_inline)) {
         if (jl < nlt) {
           u32 src;

@@ -552,8 +552,8 @@ def small_kernel_repack2(starts, lengths, grid, rng):
     tiles, at least 64): lane P of local tile j takes the entry of rank k - 1, k = the entries with
     lines starting before the tile + popcount(the tile's start marks & (2 << P) - 1), or line / n
     when the wave's entries are lanes 0, 1, ... with one line count; ranks map to lanes as the
-    kernel's ds_permute does; when Q = 64 the wave's lines 64 .. 127, loaded on speculation before
-    Q is known, are loads only. The other lines of every wave form the shared stream (wave after
+    kernel's ds_permute does; when Q = 64 in a workgroup with FAST waves, a wave's lines 64 ..
+    127, loaded on speculation before Q is known, are loads only. The other lines of every wave form the shared stream (wave after
     wave); entries with shared lines are
     ranked r = 0, 1, ... in the same order (record at r, ring entry in the offset's top byte,
     first shared position and first line), the shared tiles' start marks S_j and first entries
@@ -571,10 +571,12 @@ def small_kernel_repack2(starts, lengths, grid, rng):
     for b in range(grid):
         waves = []  # per wave: [(q, message or None, E, n)] for lanes 0..31
         fast_all = True
+        fast_w = []  # per wave: FAST (every live entry a whole aligned 4 KiB payload)
         for wid in range(8):
             t0 = front_slot(b, grid, wid)
             nk = (ntiles - t0 + nw - 1) // nw if t0 < ntiles else 0
             ents = []
+            fw = True
             for i in range(32):
                 m = 2 * (t0 + (i // 2) * nw) + i % 2
                 live = i // 2 < nk and m < count
@@ -582,7 +584,9 @@ def small_kernel_repack2(starts, lengths, grid, rng):
                 ok = live and int(lengths[m]) != 0 and E <= 4096
                 if live and not (int(lengths[m]) == 4096 and int(starts[m]) % 16 == 0):
                     fast_all = False
+                    fw = False
                 ents.append((32 * wid + i, m if live else None, E if ok else 0, (E + 127) >> 7 if ok else 0))
+            fast_w.append(fw)
             waves.append(ents)
         if fast_all:
             continue
@@ -626,7 +630,9 @@ def small_kernel_repack2(starts, lengths, grid, rng):
                     q, m, E, n = ents[i]
                     lanes[lane] = (q, m, E, n, P - r2x[i], max(r2x[i] - 64 * j, 0))
                 emit(lanes)
-            if Q < 128:  # local tile 1 loaded on speculation (lines 64 .. min(tot, 128)), then dropped
+            if Q < 128 and any(fast_w) and tot > 64:
+                # local tile 1 loaded on speculation (lines 64 .. min(tot, 128)) before Q is known
+                # (a workgroup with FAST waves), then dropped
                 for P in range(64, min(tot, 128)):
                     if runi:
                         k = P // ents[0][3] + 1
@@ -710,6 +716,45 @@ def test_small_kernel_repack2_packs_every_line_once(seed, count, grid, top):
     starts = np.cumsum(np.concatenate([[0], lengths[:-1] + rng.integers(0, 40, count - 1)])) + 3
     starts = starts - (starts & 15) * (rng.random(count) < 0.5)
     lines, covered, want_cov = {}, {}, {}
+    wgs = 0
+    for kind, a, b, *rest in small_kernel_repack2(starts, lengths, grid, rng):
+        if kind == "wgs":
+            wgs = a
+        elif kind == "line":
+            lines[(a, b)] = lines.get((a, b), 0) + 1
+        elif kind == "load":
+            s, e = int(starts[a]), int(starts[a] + lengths[a])
+            assert b % 16 == 0 and b + 16 > s and b < e, (a, s, e, b)
+            covered.setdefault(a, set()).update(range(max(b, s), min(b + 16, e)))
+        elif kind == "ring":
+            assert b == rest[0], (a, b, rest[0])
+    assert wgs > 0 and all(v == 1 for v in lines.values())
+    for m, cov in covered.items():
+        assert cov == set(range(int(starts[m]), int(starts[m] + lengths[m]))), m
+
+
+@pytest.mark.parametrize("seed,count,grid,top", [(50, 4096, 16, 200), (51, 4096, 16, 4096), (52, 2048, 8, 600)])
+def test_small_kernel_repack2_with_fast_waves(seed, count, grid, top):
+    """REPACK2 in workgroups where waves 0 and 4 are FAST (every message a whole aligned 4 KiB
+    payload) and the others are not: the FAST waves' bookkeeping comes after the prologue barrier,
+    so the others' local tile 1 is loaded on speculation before Q is known (dropped when Q = 64).
+    Same properties as test_small_kernel_repack2_packs_every_line_once."""
+    rng = np.random.default_rng(seed)
+    nw = 8 * grid
+    fastm = np.zeros(count, dtype=bool)
+    for m in range(count):
+        t0 = (m // 2) % nw
+        wid = 2 * ((t0 >> 1) // grid) + (t0 & 1)
+        fastm[m] = wid % 4 == 0
+    lengths = np.where(fastm, 4096, rng.integers(0, top + 1, count))
+    starts, cur = [], 3
+    for m in range(count):
+        if fastm[m]:
+            cur = (cur + 15) & ~15
+        starts.append(cur)
+        cur += int(lengths[m]) + int(rng.integers(0, 40))
+    starts = np.array(starts, dtype=np.int64)
+    lines, covered = {}, {}
     wgs = 0
     for kind, a, b, *rest in small_kernel_repack2(starts, lengths, grid, rng):
         if kind == "wgs":
