@@ -1200,30 +1200,49 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       bool va = false, vb = use1;
       u64 s_a = 0, s_b = s1;
       u32 E_a = 0, li_a = 0, e_a = 0, st_a = 0, E_b = E1, li_b = li1, e_b = 32u * wid + s1src, st_b = st1;
-      if (!use1) {  // (B's lines are the shared stream's: dropped)
+      if (!use1) {  // (B's lines, if loaded, are the shared stream's: dropped)
         next(va, s_a, E_a, li_a, e_a, st_a);
-        load_lines_at(A, s_a, E_a, li_a);
+        if (va) load_lines_at(A, s_a, E_a, li_a);
       }
-      bool inB = use1;  // the ping-pong enters at its second half
+      // the ping-pong (entered at its second half when B holds local tile 1); a wave's last tile
+      // is computed after the loop with no load in flight (loading an empty tile instead put an
+      // L2 round trip in front of every wave's flush)
+      bool inB = use1, last = false, lastA = false;
       for (;;) {
         if (!inB) {
           if (!va) break;
           next(vb, s_b, E_b, li_b, e_b, st_b);
           issue_prio_hi();
           drain_before_issue();
+          if (!vb) {
+            last = lastA = true;
+            break;
+          }
           load_lines_at(B, s_b, E_b, li_b);
           issue_prio_lo();
           process2(A, s_a, E_a, li_a, e_a, st_a);
           r2tiles++;
         }
         inB = false;
-        if (!vb) break;
         next(va, s_a, E_a, li_a, e_a, st_a);
         issue_prio_hi();
         drain_before_issue();
+        if (!va) {
+          last = true;
+          break;
+        }
         load_lines_at(A, s_a, E_a, li_a);
         issue_prio_lo();
         process2(B, s_b, E_b, li_b, e_b, st_b);
+        r2tiles++;
+      }
+      issue_prio_lo();
+      if (last) {
+        u32x4 L[8];
+#pragma unroll
+        for (int b = 0; b < 8; b++) L[b] = lastA ? A[b] : B[b];
+        process2(L, lastA ? s_a : s_b, lastA ? E_a : E_b, lastA ? li_a : li_b, lastA ? e_a : e_b,
+                 lastA ? st_a : st_b);
         r2tiles++;
       }
       drain_before_issue();
