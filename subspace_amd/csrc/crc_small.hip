@@ -1080,8 +1080,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
         lds_st64(sbase + kRp2Ring + 8u * (32u * wid + (u32)lane), (u64)code << 32);
       }
       // Q: every wave computes its first Q lines itself (local tiles), Q = the workgroup's least
-      // wave rounded down to whole tiles, at least one tile; the rest of every wave's lines form
-      // the shared stream, wave after wave. Known now when every wave voted (their totals and
+      // wave rounded down to whole tiles, at least one tile (or its largest wave rounded up, when
+      // that is at most one tile more); the rest of every wave's lines form the shared stream,
+      // wave after wave. Known now when every wave voted (their totals and
       // counts went to LDS before the prologue barrier); else after the FAST waves' bookkeeping
       // barrier below.
       u32 tw[8], Q = 64u;
@@ -1089,16 +1090,23 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
         const u32x4 ta = lds_ld4(sbase + kRp2Misc), tb = lds_ld4(sbase + kRp2Misc + 16u);
         tw[0] = rfl(ta.x), tw[1] = rfl(ta.y), tw[2] = rfl(ta.z), tw[3] = rfl(ta.w);
         tw[4] = rfl(tb.x), tw[5] = rfl(tb.y), tw[6] = rfl(tb.z), tw[7] = rfl(tb.w);
-        u32 tmin = tw[0];
+        u32 tmin = tw[0], tmax = tw[0];
 #pragma unroll
-        for (u32 w = 1; w < 8; w++) tmin = tw[w] < tmin ? tw[w] : tmin;
+        for (u32 w = 1; w < 8; w++) {
+          tmin = tw[w] < tmin ? tw[w] : tmin;
+          tmax = tw[w] > tmax ? tw[w] : tmax;
+        }
         Q = tmin >= 128u ? tmin & ~63u : 64u;
+        // no shared stream when no wave has more than one tile beyond Q: its tables, barrier and
+        // a shared tile's round trip after them cost more than one wave's extra local tile
+        const u32 tm = (tmax + 63u) & ~63u;
+        if (tm <= Q + 64u) Q = tm > 64u ? tm : 64u;
       };
       if (allv) read_q();
       // local tile 1 (the wave's lines 64 .. 127): its loads go out before tile 0's compute, as the
       // loop's next tile does -- known local when every wave voted (Q >= 128), else on speculation
       // for a wave with more than one tile of lines (local iff Q >= 128, known after the barrier)
-      bool use1 = allv ? Q >= 128u : tot0 > 64u;
+      bool use1 = tot0 > 64u && (!allv || Q >= 128u);
       u32 s1src = 0, E1 = 0, li1 = 0, st1 = 0;
       u64 s1 = 0;
       if (use1) {

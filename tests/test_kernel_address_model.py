@@ -549,7 +549,7 @@ def small_kernel_repack2(starts, lengths, grid, rng):
     message 2 (t0 + (i / 2) nw) + i % 2); an entry of E = L + (s & 15) in [1, 4096] has n = ceil(E /
     128) lines, laid out back to back in lane order (r2x: the wave's lines before it). The wave's
     first Q lines are its local tiles (Q: the workgroup's least wave's lines rounded down to whole
-    tiles, at least 64): lane P of local tile j takes the entry of rank k - 1, k = the entries with
+    tiles, at least 64, or its largest wave's rounded up when that is at most 64 more): lane P of local tile j takes the entry of rank k - 1, k = the entries with
     lines starting before the tile + popcount(the tile's start marks & (2 << P) - 1), or line / n
     when the wave's entries are lanes 0, 1, ... with one line count; ranks map to lanes as the
     kernel's ds_permute does; when Q = 64 in a workgroup with FAST waves, a wave's lines 64 ..
@@ -606,6 +606,9 @@ def small_kernel_repack2(starts, lengths, grid, rng):
         tots = [sum(n for *_, n in ents) for ents in waves]
         tmin = min(tots)
         Q = tmin & ~63 if tmin >= 128 else 64
+        tm = (max(tots) + 63) & ~63
+        if tm <= Q + 64:  # at most one tile beyond Q: no shared stream
+            Q = max(tm, 64)
         shared = []  # (q, m, E, n, first shared line) in stream order
         spec = []  # (message, block) loads of a speculative local tile 1 the workgroup dropped
         for ents in waves:
