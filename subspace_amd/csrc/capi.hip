@@ -25,6 +25,8 @@ struct TileDesc;
 struct TileDesc8;
 __global__ void crc32_ragged_count_desc_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
                                                u64*, u32*, u64, TileDesc8*, u32*, FaultRef);
+__global__ void crc32_ragged_count_desc16_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
+                                                 u64*, u32*, u64, TileDesc*, u32*, FaultRef);
 __global__ void crc32_ragged_count_scan_kernel(const u64*, u32, const u64*, u32, u64, u32, u32, u64*, u32*, u32*,
                                                u64*, u32*, u32*, FaultRef);
 __global__ void tile_segment_scan_kernel(const u32*, u32, u32, u32, const u64*, u64, u32*, u32*);
@@ -326,10 +328,19 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   // descriptors itself (crc32_ragged_count_desc_kernel); a many-long-message batch (few
   // messages per tile: config D) keeps the separate kernel, whose rows share the long messages
   const bool fused = c->fused_prep && arena != 0 && arena <= (1ull << kDesc8StartBits) && cap / count <= 64;
+  // absolute addresses (arena 0: slot lists past the small kernel's 4 KiB, S_large) with few
+  // tiles per message: the same fused scan with 16-B descriptors (round 6)
+  const bool fused16 = c->fused_prep && arena == 0 && cap / count <= 64;
   if (fused) {
     crc32_ragged_count_desc_kernel<<<(unsigned)ceil_div(n1, kCountTile), 1024, 0, st>>>(
         offsets, ostride, lengths, lstride, count, init, final_xor, c->d_tbase, out, c->zero_word, c->d_scan_state + 1,
         reinterpret_cast<u32*>(c->d_scan_state), cap, reinterpret_cast<TileDesc8*>(c->d_desc), c->d_overflow, fr);
+    c->zero_word = nullptr;
+    HIP_TRY(hipGetLastError());
+  } else if (fused16) {
+    crc32_ragged_count_desc16_kernel<<<(unsigned)ceil_div(n1, kCountTile), 1024, 0, st>>>(
+        offsets, ostride, lengths, lstride, count, init, final_xor, c->d_tbase, out, c->zero_word, c->d_scan_state + 1,
+        reinterpret_cast<u32*>(c->d_scan_state), cap, reinterpret_cast<TileDesc*>(c->d_desc), c->d_overflow, fr);
     c->zero_word = nullptr;
     HIP_TRY(hipGetLastError());
   } else {

@@ -249,18 +249,25 @@ __global__ __launch_bounds__(kScanThreads) void crc32_ragged_count_scan_kernel(
 constexpr int kFusedThreads = 1024;
 constexpr int kFusedItems = (int)(kCountTile / kFusedThreads);
 static_assert(kCountTile % kFusedThreads == 0, "fused scan: whole items per thread");
-__global__ __launch_bounds__(kFusedThreads) void crc32_ragged_count_desc_kernel(
-    const u64* __restrict__ offsets, u32 ostride, const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
-    u32 final_xor, u64* __restrict__ tile_base, u32* __restrict__ out, u32* __restrict__ zero_word,
-    u64* __restrict__ status, u32* __restrict__ ticket, u64 capacity, TileDesc8* __restrict__ desc8,
-    u32* __restrict__ overflow, FaultRef fault) {
+// WIDE (round 6): batches of absolute addresses (slot lists of 32 KiB slots:
+// subspace_crc32_slots past the small kernel's 4 KiB) get the same fused scan with 16-B
+// descriptors (descw_wave) and flag the batch wide (overflow[1]) for the main kernel, instead of
+// the separate tile-count scan and descriptor kernels (S_large: 15.5 + 18.9 us per call).
+template <bool WIDE>
+__device__ __forceinline__ void count_desc_body(const u64* __restrict__ offsets, u32 ostride,
+                                                const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
+                                                u32 final_xor, u64* __restrict__ tile_base, u32* __restrict__ out,
+                                                u32* __restrict__ zero_word, u64* __restrict__ status,
+                                                u32* __restrict__ ticket, u64 capacity, void* __restrict__ desc,
+                                                u32* __restrict__ overflow, FaultRef fault) {
   __shared__ u64 sx[kCountTile];
-  __shared__ u32 sw[kFusedThreads / 64][kDesc8WaveWords][64];
+  __shared__ u32 sw[WIDE ? 1 : kFusedThreads / 64][kDesc8WaveWords][64];
   bool stale;
   const u64 tile = scan_ticket(ticket, fault, &stale, true);
   if (stale) return;
   const u64 base = tile * kCountTile;
   const int tid = threadIdx.x;
+  if (WIDE && tid == 0) overflow[1] = 1u;  // (the final kernel clears it for the next call)
   u64 so[kFusedItems], L[kFusedItems], nt[kFusedItems];
   bool bad = false;
 #pragma unroll
@@ -272,7 +279,8 @@ __global__ __launch_bounds__(kFusedThreads) void crc32_ragged_count_desc_kernel(
       L[j] = lengths[i * lstride];
       nt[j] = msg_tiles(so[j], L[j]);
       out[i] = nt[j] == 0 ? init ^ final_xor : 0u;
-      if (nt[j] && ((((so[j] & ~(u64)15) + ((nt[j] - 1) << 13)) >> kDesc8StartBits) | ((nt[j] - 1) >> kDesc8AfterBits)))
+      if (!WIDE && nt[j] &&
+          ((((so[j] & ~(u64)15) + ((nt[j] - 1) << 13)) >> kDesc8StartBits) | ((nt[j] - 1) >> kDesc8AfterBits)))
         bad = true;
     } else if (i == count && zero_word) {
       *zero_word = 0u;  // a slot batch's mismatch count (no separate memset)
@@ -295,8 +303,29 @@ __global__ __launch_bounds__(kFusedThreads) void crc32_ragged_count_desc_kernel(
     if (i <= count) tile_base[i] = tb;
     if (i == count) overflow[0] = tb > capacity ? 1u : 0u;
     // the wave's 64 consecutive messages i (j fixed): their descriptors below the capacity
-    desc8_wave(desc8, capacity, tb, nt[j], so[j], L[j], 0u, 64u, sw[tid >> 6], true);
+    if constexpr (WIDE)
+      descw_wave(static_cast<TileDesc*>(desc), capacity, tb, nt[j], so[j], L[j]);
+    else
+      desc8_wave(static_cast<TileDesc8*>(desc), capacity, tb, nt[j], so[j], L[j], 0u, 64u, sw[tid >> 6], true);
   }
+}
+
+__global__ __launch_bounds__(kFusedThreads) void crc32_ragged_count_desc_kernel(
+    const u64* __restrict__ offsets, u32 ostride, const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
+    u32 final_xor, u64* __restrict__ tile_base, u32* __restrict__ out, u32* __restrict__ zero_word,
+    u64* __restrict__ status, u32* __restrict__ ticket, u64 capacity, TileDesc8* __restrict__ desc8,
+    u32* __restrict__ overflow, FaultRef fault) {
+  count_desc_body<false>(offsets, ostride, lengths, lstride, count, init, final_xor, tile_base, out, zero_word, status,
+                         ticket, capacity, desc8, overflow, fault);
+}
+
+__global__ __launch_bounds__(kFusedThreads) void crc32_ragged_count_desc16_kernel(
+    const u64* __restrict__ offsets, u32 ostride, const u64* __restrict__ lengths, u32 lstride, u64 count, u32 init,
+    u32 final_xor, u64* __restrict__ tile_base, u32* __restrict__ out, u32* __restrict__ zero_word,
+    u64* __restrict__ status, u32* __restrict__ ticket, u64 capacity, TileDesc* __restrict__ desc,
+    u32* __restrict__ overflow, FaultRef fault) {
+  count_desc_body<true>(offsets, ostride, lengths, lstride, count, init, final_xor, tile_base, out, zero_word, status,
+                        ticket, capacity, desc, overflow, fault);
 }
 
 // Tiles present: the batch's total (device value, ragged path) or a host count (long path),

@@ -136,4 +136,35 @@ __device__ __forceinline__ void desc8_wave(TileDesc8* __restrict__ desc8, u64 li
   }
 }
 
+// The 16-B descriptors of the tiles of one wave's 64 messages (the fused tile-count scan's form
+// for batches of absolute addresses, beyond the 8-B form's 2^37-byte range): each lane stores its
+// message's first kLaneTilesW tiles, then longer messages one after the other, 64 tiles per
+// store (as crc32_ragged_desc_kernel's wide batches). Tiles at or past `limit` are not stored.
+constexpr u32 kLaneTilesW = 8;
+__device__ __forceinline__ void descw_tile(TileDesc* __restrict__ desc, u64 limit, u64 so, u64 L, u64 t0, u64 nt,
+                                           u64 j) {
+  if (t0 + j >= limit) return;
+  const u32 mis = (u32)(so & 15);
+  const u64 rest = L + mis - (j << 13);
+  TileDesc d;
+  d.tile_start = (so & ~(u64)15) + (j << 13);
+  d.after = (u32)(nt - 1 - j) | (j == 0 ? kFirstTile : 0u);
+  d.len = (rest < 8192 ? (u32)rest : 8192u) | (mis << 16);
+  desc[t0 + j] = d;
+}
+__device__ __forceinline__ void descw_wave(TileDesc* __restrict__ desc, u64 limit, u64 t0, u64 nt, u64 so, u64 L) {
+  const u32 lane = threadIdx.x & 63u;
+#pragma unroll
+  for (u32 j = 0; j < kLaneTilesW; j++)
+    if (j < nt) descw_tile(desc, limit, so, L, t0, nt, j);
+  u64 big = __ballot(nt > kLaneTilesW);
+  while (big) {  // wave-uniform
+    const int src = __ffsll((unsigned long long)big) - 1;
+    big &= big - 1;
+    const u64 bt0 = __shfl(t0, src, 64), bnt = __shfl(nt, src, 64);
+    const u64 bso = __shfl(so, src, 64), bL = __shfl(L, src, 64);
+    for (u64 j = kLaneTilesW + lane; j < bnt; j += 64) descw_tile(desc, limit, bso, bL, bt0, bnt, j);
+  }
+}
+
 }  // namespace subspace_amd

@@ -252,6 +252,47 @@ def desc_kernel_stores(ntiles, capacity, lane_tiles=2, rows=1):
     return owner, stores, tb
 
 
+def descw_stores(ntiles, capacity, lane_tiles=8):
+    """Replays crc_desc.h descw_wave (the wide fused tile-count scan + descriptor kernel,
+    crc_combine.hip crc32_ragged_count_desc16_kernel: absolute-address batches): each lane stores
+    its message's first kLaneTilesW tiles, then every message with more, one after the other, 64
+    tiles per round (tile j = kLaneTilesW + lane + 64 r); no tile at or past the capacity."""
+    count = len(ntiles)
+    tb = np.concatenate([[0], np.cumsum(ntiles, dtype=np.int64)])
+    stores = collections.Counter()
+    owner = {}
+    for w0 in range(0, count, 64):
+        for m in range(w0, min(w0 + 64, count)):
+            nt = int(ntiles[m])
+            js = list(range(min(nt, lane_tiles)))
+            if nt > lane_tiles:  # the wave's long messages, in lane order
+                for r0 in range(lane_tiles, nt, 64):
+                    js += [j for j in range(r0, min(r0 + 64, nt))]
+            for j in js:
+                if int(tb[m]) + j < capacity:
+                    owner[int(tb[m]) + j] = (m, j)
+                    stores[int(tb[m]) + j] += 1
+    return owner, stores, tb
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_wide_fused_desc_stores_every_tile_once(seed):
+    rng = np.random.default_rng(100 + seed)
+    parts = []
+    for _ in range(40):
+        parts.append(np.zeros(int(rng.integers(0, 50)), dtype=np.int64))
+        parts.append(rng.integers(1, 6, int(rng.integers(1, 200))))       # S_large: 1 .. 5 tiles
+        parts.append(rng.integers(6, 200, int(rng.integers(0, 3))))       # longer messages
+    ntiles = np.concatenate(parts).astype(np.int64)
+    total = int(ntiles.sum())
+    for capacity in (total, total + 1000, total - 7):
+        owner, stores, tb = descw_stores(ntiles, capacity)
+        assert sorted(owner) == list(range(min(total, capacity)))
+        assert set(stores.values()) == {1}
+        for tau, (m, j) in owner.items():
+            assert tb[m] <= tau < tb[m + 1] and tau == tb[m] + j
+
+
 @pytest.mark.parametrize("seed,rows", [(s, 1) for s in range(6)] + [(6, 3), (7, 64)])
 def test_desc_kernel_stores_every_tile_once(seed, rows):
     rng = np.random.default_rng(seed)
