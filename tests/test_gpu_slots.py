@@ -600,3 +600,64 @@ def test_large_slot_list_latency_channel_shape(gpu_ctx, oracle, mode):
         want = oracle.verify_slots(host, po[order], yo[order], sizes[order], cs, ms)
         assert np.array_equal(got, want)
         assert int(err.item()) == int((want == 1).sum()) > 0
+
+
+@pytest.mark.parametrize("mode", ["publish", "verify"])
+def test_large_slot_list_statuses(gpu_ctx, oracle, mode):
+    """Slot lists past 4 KiB (the ragged path at absolute addresses, finished by its last
+    kernel: crc_slots.hip crc32_ragged_final_slot_kernel) with a metadata span, empty payloads,
+    sizes past max_message_size (OVERSIZE, nothing stored or compared), and for verify every
+    status the oracle gives: mismatches in the payload, metadata, span 0 and stored checksum,
+    uncovered bytes changed, and slots without kMessageHasChecksum."""
+    count, area, max_len, cs, ms = 1200, 32768, 20000, 4, 16
+    rng = np.random.default_rng(0x5A2A + (mode == "verify"))
+    sizes = rng.integers(0, max_len + 1, count).astype(np.uint64)
+    sizes[:6] = [0, 1, 8192, max_len, max_len + 1, area]
+    sizes[rng.choice(count, 40, replace=False)] = rng.integers(max_len + 1, area + 1, 40).astype(np.uint64)
+    big = sizes > max_len
+    host, ps, stride = build_channel(count, area, cs, ms, sizes, seed=0x5A2B)
+    po, yo = offsets(count, stride, ps)
+    kinds = rng.integers(0, 8, count)
+    if mode == "verify":
+        oracle.publish_slots(host, po, yo, sizes, cs, ms)
+        for i, k in enumerate(kinds):
+            b, n = int(po[i]), int(sizes[i])
+            if k == 1 and n:
+                host[b + ps + rng.integers(0, n)] ^= np.uint8(1 << rng.integers(0, 8))
+            elif k == 2:
+                host[b + 48 + cs + rng.integers(0, ms)] ^= 0x10
+            elif k == 3:
+                host[b + 4 + rng.integers(0, 44)] ^= 0x01
+            elif k == 4:
+                host[b + 48 + rng.integers(0, 4)] ^= 0x80
+            elif k == 5:
+                host[b:b + 4] ^= 0xFF
+            elif k == 6:
+                host[b + 32] &= 0xFB
+    before = host.copy()
+    dev = torch.from_numpy(host).to(DEV)
+    order = rng.permutation(count)
+    base = np.uint64(dev.data_ptr())
+    rec = slots.slot_records(base + po[order], base + yo[order], sizes[order])
+    d_rec = torch.from_numpy(rec.view(np.int64)).to(DEV)
+    status = torch.full((count,), 7, dtype=torch.int32, device=DEV)
+    err = torch.full((1,), 12345, dtype=torch.int32, device=DEV)
+    gmode = gpu.SLOT_CALCULATE if mode == "publish" else gpu.SLOT_VERIFY
+    gpu_ctx.crc32_slots(d_rec, max_message_size=max_len, checksum_size=cs, metadata_size=ms, mode=gmode,
+                        status=status, error_count=err)
+    torch.cuda.synchronize()
+    got = status.cpu().numpy().view(np.uint32)
+    bo = big[order]
+    assert (got[bo] == gpu.SLOT_OVERSIZE).all()
+    if mode == "publish":
+        assert (got[~bo] == 0).all() and int(err.item()) == 0
+        want = before.copy()
+        keep = ~big
+        oracle.publish_slots(want, po[keep], yo[keep], sizes[keep], cs, ms)
+        assert np.array_equal(dev.cpu().numpy(), want)  # oversize slots untouched
+    else:
+        want = oracle.verify_slots(host, po[order], yo[order], sizes[order], cs, ms)
+        assert set(np.unique(want[~bo])) == {0, 1, 2}
+        assert np.array_equal(got[~bo], want[~bo])
+        assert int(err.item()) == int((want[~bo] == 1).sum())
+        assert np.array_equal(dev.cpu().numpy(), before)  # verify never writes the channel
