@@ -892,7 +892,9 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
     // absolute addresses; the slots finished by the ragged path's last kernel (its tile-count
     // kernel zeroes the mismatch count)
     const u64 cap = count * ((max_message_size + 15 + 8191) / 8192) + 1;
-    const SlotFin fin{rec, max_message_size, checksum_size, metadata_size, mode, dev_status, dev_error_count};
+    // (a list's records carry their sizes: max_message_size sizes the workspace, it is no
+    // oversize bound -- as on the small-kernel path)
+    const SlotFin fin{rec, ~0ull, checksum_size, metadata_size, mode, dev_status, dev_error_count};
     rc = ragged_run(c, nullptr, cap, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st, 0, &fin);
     const bool zeroed = was_zeroed(c, dev_error_count);
     if (rc) return rc;

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kSlotWG) void crc32_slot_finish_kernel(
 // ragged path's final kernel and the slot finish in one (round 6). Thread m combines message m's
 // payload CRC from its tiles' XOR prefix (crc_ragged.hip crc32_ragged_final_kernel: P(t1 - 1) ^
 // P(t0 - 1), the padding undone over the LDS inverse tables; init 0, no final XOR) and finishes
-// slot m as crc32_slot_finish_kernel does; its prefix words load with its record and tile range,
+// slot m as crc32_slot_finish_kernel does (max_len: ~0 for lists); its prefix words load with its record and tile range,
 // before the prefix gathers, instead of one launch and two dependent round trips later
 // (S_large: final 8.7 + finish 12.5 us per call, r06s).
 __global__ __launch_bounds__(1024) void crc32_ragged_final_slot_kernel(

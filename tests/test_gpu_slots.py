@@ -605,16 +605,16 @@ def test_large_slot_list_latency_channel_shape(gpu_ctx, oracle, mode):
 @pytest.mark.parametrize("mode", ["publish", "verify"])
 def test_large_slot_list_statuses(gpu_ctx, oracle, mode):
     """Slot lists past 4 KiB (the ragged path at absolute addresses, finished by its last
-    kernel: crc_slots.hip crc32_ragged_final_slot_kernel) with a metadata span, empty payloads,
-    sizes past max_message_size (OVERSIZE, nothing stored or compared), and for verify every
-    status the oracle gives: mismatches in the payload, metadata, span 0 and stored checksum,
-    uncovered bytes changed, and slots without kMessageHasChecksum."""
+    kernel: crc_slots.hip crc32_ragged_final_slot_kernel) with a metadata span, empty payloads
+    and records longer than max_message_size (a list's records carry their sizes: computed
+    whole, as on the small-kernel path), and for verify every status the oracle gives:
+    mismatches in the payload, metadata, span 0 and stored checksum, uncovered bytes changed,
+    and slots without kMessageHasChecksum."""
     count, area, max_len, cs, ms = 1200, 32768, 20000, 4, 16
     rng = np.random.default_rng(0x5A2A + (mode == "verify"))
     sizes = rng.integers(0, max_len + 1, count).astype(np.uint64)
-    sizes[:6] = [0, 1, 8192, max_len, max_len + 1, area]
     sizes[rng.choice(count, 40, replace=False)] = rng.integers(max_len + 1, area + 1, 40).astype(np.uint64)
-    big = sizes > max_len
+    sizes[:6] = [0, 1, 8192, max_len, max_len + 1, area]
     host, ps, stride = build_channel(count, area, cs, ms, sizes, seed=0x5A2B)
     po, yo = offsets(count, stride, ps)
     kinds = rng.integers(0, 8, count)
@@ -647,17 +647,13 @@ def test_large_slot_list_statuses(gpu_ctx, oracle, mode):
                         status=status, error_count=err)
     torch.cuda.synchronize()
     got = status.cpu().numpy().view(np.uint32)
-    bo = big[order]
-    assert (got[bo] == gpu.SLOT_OVERSIZE).all()
     if mode == "publish":
-        assert (got[~bo] == 0).all() and int(err.item()) == 0
-        want = before.copy()
-        keep = ~big
-        oracle.publish_slots(want, po[keep], yo[keep], sizes[keep], cs, ms)
-        assert np.array_equal(dev.cpu().numpy(), want)  # oversize slots untouched
+        assert (got == 0).all() and int(err.item()) == 0
+        oracle.publish_slots(before, po, yo, sizes, cs, ms)
+        assert np.array_equal(dev.cpu().numpy(), before)
     else:
         want = oracle.verify_slots(host, po[order], yo[order], sizes[order], cs, ms)
-        assert set(np.unique(want[~bo])) == {0, 1, 2}
-        assert np.array_equal(got[~bo], want[~bo])
-        assert int(err.item()) == int((want[~bo] == 1).sum())
+        assert set(np.unique(want)) == {0, 1, 2}
+        assert np.array_equal(got, want)
+        assert int(err.item()) == int((want == 1).sum())
         assert np.array_equal(dev.cpu().numpy(), before)  # verify never writes the channel
