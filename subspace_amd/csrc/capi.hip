@@ -390,7 +390,7 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   const u64 fb = SUBSPACE_FINAL_BLOCKS_PER_CU ? std::min<u64>(ceil_div(count, 1024), (u64)SUBSPACE_FINAL_BLOCKS_PER_CU * c->num_cus)
                                               : ceil_div(count, 1024);
   if (fin)  // (slot lists: init 0, no final XOR, out = the overflow path's accumulators)
-    crc32_ragged_final_slot_kernel<<<(unsigned)fb, 1024, 0, st>>>(
+    crc32_ragged_final_slot_kernel<<<(unsigned)std::min<u64>(ceil_div(count, 256), 16ull * c->num_cus), 256, 0, st>>>(
         c->d_tbase, fin->slots, count, c->d_local, c->d_segx, (u32)g.nw, (u32)g.nwb, c->d_overflow, c->d_rops, out,
         c->d_scan_state + 1 + c->scan_a_words, ceil_div(g.nseg, kScanTile), tickets + 1, fr, fin->max_len, fin->cs,
         fin->ms, fin->mode, c->d_tab, c->d_pow2, fin->status, fin->err);
