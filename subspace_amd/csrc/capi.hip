@@ -41,9 +41,6 @@ __global__ void crc32_ragged_final_kernel(const u64*, const u64*, u32, const u64
                                           u32, u32, u32*, const u32*, u32, u32*, u64*, u64, u32*, FaultRef);
 __global__ void crc32_slot_finish_kernel(const u64*, uint8_t*, u64, const u64*, u64, u64, u64, int, int, u32,
                                          const u32*, const u32*, const u32*, u32*, u32*, u32*);
-__global__ void crc32_ragged_final_slot_kernel(const u64*, const u64*, u64, const u32*, const u32*, u32, u32, u32*,
-                                               const u32*, const u32*, u64*, u64, u32*, FaultRef, u64, int, int, u32,
-                                               const u32*, const u32*, u32*, u32*);
 __global__ void slot_payload_offsets_kernel(u64, u64, u64, u64*, const u64*, u64, u64*);
 __global__ void uniform_offsets_kernel(u64 stride, u64 length, u64 count, u64* offsets, u64* lengths);
 template <int WG>
@@ -312,19 +309,8 @@ int grid_for(subspace_crc_ctx* c, u64 work_units, int waves_per_block) {
 // Ragged path: per-message tile counts -> scan -> tile descriptors -> main kernel.
 // Offsets/lengths are read with element strides (1 = plain arrays, 3 = slot records).
 // `cap` sizes the descriptor workspace; a batch with more tiles takes the search path.
-// A slot list's finish, run by the ragged path's last kernel (ragged_run's `fin`).
-struct SlotFin {
-  const u64* slots;  // records (prefix, payload, size)
-  u64 max_len;
-  int32_t cs, ms;
-  u32 mode;
-  u32* status;
-  u32* err;  // zeroed by the call's tile-count kernel (want_zeroed)
-};
-
 int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* offsets, u32 ostride, const u64* lengths,
-               u32 lstride, u64 count, u32 init, u32 final_xor, u32* out, hipStream_t st, u64 arena,
-               const SlotFin* fin = nullptr) {
+               u32 lstride, u64 count, u32 init, u32 final_xor, u32* out, hipStream_t st, u64 arena) {
   int rc = use_workspace(c, st);
   if (rc) return rc;
   cap = clamp_capacity(c, cap, count);
@@ -389,16 +375,10 @@ int ragged_run(subspace_crc_ctx* c, const uint8_t* base, u64 cap, const u64* off
   if (rc) return rc;
   const u64 fb = SUBSPACE_FINAL_BLOCKS_PER_CU ? std::min<u64>(ceil_div(count, 1024), (u64)SUBSPACE_FINAL_BLOCKS_PER_CU * c->num_cus)
                                               : ceil_div(count, 1024);
-  if (fin)  // (slot lists: init 0, no final XOR, out = the overflow path's accumulators)
-    crc32_ragged_final_slot_kernel<<<(unsigned)std::min<u64>(ceil_div(count, 256), 16ull * c->num_cus), 256, 0, st>>>(
-        c->d_tbase, fin->slots, count, c->d_local, c->d_segx, (u32)g.nw, (u32)g.nwb, c->d_overflow, c->d_rops, out,
-        c->d_scan_state + 1 + c->scan_a_words, ceil_div(g.nseg, kScanTile), tickets + 1, fr, fin->max_len, fin->cs,
-        fin->ms, fin->mode, c->d_tab, c->d_pow2, fin->status, fin->err);
-  else
-    crc32_ragged_final_kernel<<<(unsigned)fb, 1024, 0, st>>>(
-        c->d_tbase, offsets, ostride, lengths, lstride, count, c->d_local, c->d_segx, (u32)g.nw, (u32)g.nwb,
-        c->d_overflow, c->d_rops, final_xor, out, c->d_scan_state + 1 + c->scan_a_words, ceil_div(g.nseg, kScanTile),
-        tickets + 1, fr);
+  crc32_ragged_final_kernel<<<(unsigned)fb, 1024, 0, st>>>(
+      c->d_tbase, offsets, ostride, lengths, lstride, count, c->d_local, c->d_segx, (u32)g.nw, (u32)g.nwb,
+      c->d_overflow, c->d_rops, final_xor, out, c->d_scan_state + 1 + c->scan_a_words, ceil_div(g.nseg, kScanTile),
+      tickets + 1, fr);
   HIP_TRY(hipGetLastError());
   c->scan_dirty = false;
   return SUBSPACE_CRC_OK;
@@ -889,17 +869,8 @@ int subspace_crc32_slots(subspace_crc_ctx* c, const subspace_crc_slot* dev_slots
     rc = small_run(c, nullptr, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st, nullptr,
                    small_lanes(max_message_size));
   } else {
-    // absolute addresses; the slots finished by the ragged path's last kernel (its tile-count
-    // kernel zeroes the mismatch count)
     const u64 cap = count * ((max_message_size + 15 + 8191) / 8192) + 1;
-    // (a list's records carry their sizes: max_message_size sizes the workspace, it is no
-    // oversize bound -- as on the small-kernel path)
-    const SlotFin fin{rec, ~0ull, checksum_size, metadata_size, mode, dev_status, dev_error_count};
-    rc = ragged_run(c, nullptr, cap, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st, 0, &fin);
-    const bool zeroed = was_zeroed(c, dev_error_count);
-    if (rc) return rc;
-    if (dev_error_count && !zeroed) return fail(SUBSPACE_CRC_EINVAL, "internal: mismatch count not zeroed");
-    return SUBSPACE_CRC_OK;
+    rc = ragged_run(c, nullptr, cap, rec + 1, 3, rec + 2, 3, count, 0u, 0u, c->d_crc0, st, 0);  // absolute addresses
   }
   const bool zeroed = was_zeroed(c, dev_error_count);
   if (rc) return rc;

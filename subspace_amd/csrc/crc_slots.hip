@@ -103,115 +103,6 @@ __global__ __launch_bounds__(kSlotWG) void crc32_slot_finish_kernel(
   }
 }
 
-// Slot lists past the small kernel's 4 KiB (subspace_crc32_slots, S_large: 32 KiB slots): the
-// ragged path's final kernel and the slot finish in one (round 6). Thread m combines message m's
-// payload CRC from its tiles' XOR prefix (crc_ragged.hip crc32_ragged_final_kernel: P(t1 - 1) ^
-// P(t0 - 1), the padding undone over the LDS inverse tables; init 0, no final XOR) and finishes
-// slot m as crc32_slot_finish_kernel does (max_len: ~0 for lists); its prefix words load with its record and tile range,
-// before the prefix gathers, instead of one launch and two dependent round trips later
-// (S_large: final 8.7 + finish 12.5 us per call, r06s).
-constexpr int kFinSlotWG = 256;
-constexpr int kFinPowLds = 16;  // Z_{2^k}, k < 16, staged in LDS (a payload below 64 KiB)
-__global__ __launch_bounds__(kFinSlotWG) void crc32_ragged_final_slot_kernel(
-    const u64* __restrict__ tile_base, const u64* __restrict__ slots, u64 count, const u32* __restrict__ local,
-    const u32* __restrict__ segx, u32 nw, u32 nwb, u32* __restrict__ overflow, const u32* __restrict__ gops,
-    const u32* __restrict__ acc, u64* scan_status, u64 scan_words, u32* scan_ticket, FaultRef fault, u64 max_len,
-    int checksum_size, int metadata_size, u32 mode, const u32* __restrict__ gtab, const u32* __restrict__ gpow2,
-    u32* __restrict__ status, u32* __restrict__ error_count) {
-  reset_scan_state(scan_status, scan_words, scan_ticket);  // the segment scan is done
-  if (blockIdx.x == 0 && threadIdx.x == 0) overflow[1] = overflow[2] = 0u;  // (as the final kernel)
-  if (scan_faulted(fault)) return;
-  // (256-thread workgroups, one per 256 slots: the slot's dependent chain -- record, prefix
-  // words, prefix gathers, the shift by its length -- is latency-bound; a 1,024-thread grid
-  // of count / 1,024 workgroups ran 29.5 us for S_large against 21.2 for the two kernels, r06u)
-  __shared__ u32 inv[(kNumNibInvOps + 1) * 128];
-  __shared__ u32 t[1024];
-  __shared__ u32 pw2[kFinPowLds * 128];
-  for (u32 i = threadIdx.x; i < kNumNibInvOps * 128u; i += blockDim.x) inv[i] = gops[kRagNibInvOps + i];
-  for (u32 i = threadIdx.x; i < 128u; i += blockDim.x) inv[kNumNibInvOps * 128 + i] = gops[kRagInvOps + 128 * 12 + i];
-  for (u32 i = threadIdx.x; i < 1024u; i += blockDim.x) t[i] = gtab[i];
-  for (u32 i = threadIdx.x; i < kFinPowLds * 128u; i += blockDim.x) pw2[i] = gpow2[i];
-  __syncthreads();
-  // Z_n(v): Z_{2^k} for k < kFinPowLds from LDS, above from global memory (shift_zeros)
-  auto shift = [&](u32 v, u64 n) {
-    for (int k = 0; n; k++, n >>= 1) {
-      if (!(n & 1u)) continue;
-      const u32* op = k < kFinPowLds ? pw2 + 128 * k : gpow2 + 128 * k;
-      u32 r = 0;
-#pragma unroll
-      for (int j = 0; j < 8; j++) r ^= op[16 * j + ((v >> (4 * j)) & 15u)];
-      v = r;
-    }
-    return v;
-  };
-  auto undo = [&](u32 slot, u32 x) {
-    const u32* op = inv + 128 * slot;
-    u32 r = op[x & 15u];
-#pragma unroll
-    for (int k = 1; k < 8; k++) r ^= op[16 * k + ((x >> (4 * k)) & 15u)];
-    return r;
-  };
-  const bool ovf = *overflow != 0u;
-  const bool calc = mode == 0u;
-  const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 m0 = (u64)blockIdx.x * blockDim.x; m0 < count; m0 += stride) {
-    const u64 m = m0 + threadIdx.x;
-    const bool live = m < count;
-    // the record, the tile range and (a slot to finish) its prefix words, all at once
-    const u64 t0 = live ? tile_base[m] : 0, t1 = live ? tile_base[m + 1] : 0;
-    uint8_t* prefix = live ? reinterpret_cast<uint8_t*>(slots[3 * m]) : nullptr;
-    const u64 sm = live ? slots[3 * m + 1] : 0, Lm = live ? slots[3 * m + 2] : 0;
-    const bool fin = live && Lm <= max_len;
-    u32* pw = reinterpret_cast<u32*>(prefix);  // 8-B aligned (int64 fields)
-    u32 w[12];
-#pragma unroll
-    for (int k = 1; k < 12; k++) w[k] = fin ? pw[k] : 0u;
-    const u32 pe = (!ovf && live && t1) ? tile_prefix(local, segx, nw, nwb, t1 - 1) : 0u;
-    u32 pb = (u32)__shfl_up((int)pe, 1, 64);
-    if ((threadIdx.x & 63u) == 0u) pb = (!ovf && live && t0) ? tile_prefix(local, segx, nw, nwb, t0 - 1) : 0u;
-    if (!live) continue;
-    if (!fin) {
-      if (status) status[m] = 4u;  // SUBSPACE_CRC_SLOT_OVERSIZE
-      continue;
-    }
-    u32 crc0 = 0;  // crc_raw(0, payload): 0 for an empty payload
-    if (t1 != t0) {
-      u32 v = ovf ? acc[m] : pe ^ pb;
-      const u32 pad = (u32)(0 - (Lm + (sm & 15))) & 8191u;
-#pragma unroll
-      for (u32 k = 0; k < 3; k++) {
-        const u32 d = (pad >> (4 * k)) & 15u;
-        if (d) v = undo(15 * k + d - 1, v);
-      }
-      if (pad & 0x1000u) v = undo(kNumNibInvOps, v);
-      crc0 = v;
-    }
-    // the slot (crc32_slot_finish_kernel)
-    const bool has = (w[8] & kHasChecksum) != 0u;
-    if (calc && !has) {
-      w[8] |= kHasChecksum;
-      pw[8] = w[8];
-    }
-    if (!calc && !has) {
-      if (status) status[m] = 2u;
-      continue;
-    }
-    u32 h = 0xFFFFFFFFu;
-#pragma unroll
-    for (int k = 1; k < 12; k++) h = tab_step4(t, h ^ w[k]);
-    if (metadata_size > 0) h = crc_bytes(t, h, prefix + 48 + checksum_size, (u64)metadata_size);
-    const u32 crc = ~(shift(h, Lm) ^ crc0);
-    if (calc) {
-      pw[12] = crc;
-      if (status) status[m] = 0u;
-    } else {
-      const bool ok = pw[12] == crc;
-      if (status) status[m] = ok ? 0u : 1u;
-      if (!ok && error_count) atomicAdd(error_count, 1u);
-    }
-  }
-}
-
 // Payload offsets of the contiguous layout (relative to the first prefix), and the per-slot
 // sizes the payload kernels read: a size beyond the slot's payload area (max_len) as 0, so no
 // kernel reads an oversize slot's bytes (crc32_slot_finish_kernel labels it OVERSIZE).
