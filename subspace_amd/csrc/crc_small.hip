@@ -970,7 +970,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+#ifndef SUBSPACE_PROBE_PREBAR
   if constexpr (probe) pt[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   u64 sA, LA, sB, LB;
   if constexpr (G == 32) {
     win_rec(0, sA, LA);
@@ -1006,6 +1008,9 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
     }
   }
   if constexpr (SUBSPACE_SMALL_EARLY_TILE0) fill.store(sbase);
+#ifdef SUBSPACE_PROBE_PREBAR  // (A/B timelines: stamp 1 = the wave reaches the barrier)
+  if constexpr (probe) pt[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   __syncthreads();
   // (nothing hoisted above the barrier: hipcc otherwise moved the span hash's first step there,
   // with a wait for tile 0's lines, so every wave of the workgroup waited for the slowest
