@@ -6,8 +6,8 @@
 // final XOR (crc0 = crc_raw(0, payload)). This kernel finishes each slot with one thread:
 //   h   = crc_raw(0xFFFFFFFF, span0 || span1)         (44 + metadata_size prefix bytes)
 //   crc = ~(Z_L(h) ^ crc0),  L = message_size          (linearity, crc_math.h)
-// Z_L is applied by binary decomposition over Z_{2^k} nibble operators (gpow2, 64 ops,
-// global memory: a 4 KiB payload needs one). The prefix bytes go through slice-by-4
+// Z_L is applied by binary decomposition over Z_{2^k} nibble operators (gpow2, 64 ops; the
+// first 16 staged in LDS per workgroup, the rest read from global memory). The prefix bytes go through slice-by-4
 // tables staged in LDS (4 KiB per workgroup).
 #include "crc_device.h"
 
@@ -34,19 +34,6 @@ __device__ u32 crc_bytes(const u32* __restrict__ t, u32 crc, const uint8_t* p, u
   p = reinterpret_cast<const uint8_t*>(q);
   while (n--) crc = tab_step1(t, crc, *p++);
   return crc;
-}
-
-// Z_n(v) for any 64-bit n: gpow2 holds Z_{2^k}, k = 0..63, as 8x16 nibble tables.
-__device__ u32 shift_zeros(const u32* __restrict__ gpow2, u32 v, u64 n) {
-  for (int k = 0; n; k++, n >>= 1) {
-    if (!(n & 1u)) continue;
-    const u32* op = gpow2 + 128 * k;
-    u32 r = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) r ^= op[16 * j + ((v >> (4 * j)) & 15u)];
-    v = r;
-  }
-  return v;
 }
 
 // Slot i: prefix = slots ? slots[3i] : buf + i*stride; payload size = slots ? slots[3i+2]
