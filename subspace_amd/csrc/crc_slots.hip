@@ -7,8 +7,8 @@
 //   h   = crc_raw(0xFFFFFFFF, span0 || span1)         (44 + metadata_size prefix bytes)
 //   crc = ~(Z_L(h) ^ crc0),  L = message_size          (linearity, crc_math.h)
 // Z_L is applied by binary decomposition over Z_{2^k} nibble operators (gpow2, 64 ops; the
-// first 16 staged in LDS per workgroup, the rest read from global memory). The prefix bytes go through slice-by-4
-// tables staged in LDS (4 KiB per workgroup).
+// first 16 staged in LDS per workgroup, the rest read from global memory). The prefix bytes
+// go through slice-by-4 tables staged in LDS (4 KiB per workgroup).
 #include "crc_device.h"
 
 namespace subspace_amd {
