@@ -73,8 +73,10 @@
 #ifndef SUBSPACE_SMALL_EARLY_TILE0
 #define SUBSPACE_SMALL_EARLY_TILE0 0
 #endif
-#if (SUBSPACE_SMALL_VARIANT != 0 || SUBSPACE_SMALL_EARLY_TILE0 != 0) && !defined(SUBSPACE_AB_BUILD)
-#error "SUBSPACE_SMALL_VARIANT is a timing-only A/B knob (tools/ab_lib.sh defines SUBSPACE_AB_BUILD)"
+#if (SUBSPACE_SMALL_VARIANT != 0 || SUBSPACE_SMALL_EARLY_TILE0 != 0 || defined(SUBSPACE_RP2_DEBUG) || \
+     defined(SUBSPACE_PROBE_PREBAR)) &&                                                                 \
+    !defined(SUBSPACE_AB_BUILD)
+#error "timing / debug A/B knobs build only with tools/ab_lib.sh (which defines SUBSPACE_AB_BUILD)"
 #endif
 
 namespace subspace_amd {
