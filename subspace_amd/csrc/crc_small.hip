@@ -1192,9 +1192,14 @@ __global__ __launch_bounds__(WG) void crc32_small_kernel(const u32* __restrict__
           j = (u32)__builtin_amdgcn_readlane((int)t, 0);
         }
         v = j < ntl;
+        if (!v) {  // (wave-uniform: none left -- no table reads; the caller loads nothing)
+          ms = 0;
+          mE = mli = me = mst = 0u;
+          return;
+        }
         // shared tile j, this lane: its entry's record and ring entry, its line, the entry's E,
         // and the lane where the entry's part in this tile starts
-        const u32 jj = v ? j : 0u;
+        const u32 jj = j;
         const u64 Sj = lds_ld64(sbase + kRp2Starts + 8u * jj);
         const u32 fe = lds_ld(sbase + kRp2First + 4u * jj);
         u32 e = fe + (u32)__builtin_popcountll(Sj & ((2ull << lane) - 1ull)) - (u32)(Sj & 1ull);
