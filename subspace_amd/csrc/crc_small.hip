@@ -26,8 +26,10 @@
 //    -- measured 2.3-3.4 us slower per 65,536-slot list, with or without loop padding:
 //    profiles/r04/README.md.)
 //  * G = 32: a wave whose window holds only whole aligned 4 KiB messages runs the FAST loop
-//    (the uniform kernel's loads); any other wave packs its window by message size, 2^c lanes
-//    per message (REPACK, below), so a short message takes a few lanes rather than a half-tile.
+//    (the uniform kernel's loads). Slot lists: a workgroup with any other wave packs all 256 of
+//    its messages as one stream of exact 128-B lines (n = ceil(E / 128) per message) that its
+//    8 waves share (REPACK2, below; the padding left is p = 128 n - E < 128). Other batches: a
+//    wave packs its own window by message size, 2^c lanes per message (REPACK).
 //  * Every line load stays inside its message: block b of lane l is read from s0 +
 //    min(128 l + 16 b, last block), so the lanes past the end re-read the last block (one
 //    cache line) instead of branching around loads, and a half with nothing to read (no
