@@ -153,3 +153,15 @@ def test_both_launch_forms_give_ranks_the_same_environment():
     again = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--print-rank-env"],
                            capture_output=True, text=True, timeout=120, env=env, cwd=str(ROOT))
     assert _rank_envs(again.stdout) == a
+
+
+def test_default_secondary_configs_cover_every_row():
+    """the driver's default line carries Cu (config C at unaligned
+    offsets) and S_large (the reference's 32 KiB checksum channel) beside the other rows."""
+    import re
+    src = (Path(__file__).resolve().parent.parent / "bench.py").read_text()
+    m = re.search(r'cfg_names = args\.configs if args\.configs is not None else \("([^"]+)"', src)
+    assert m, "default config list not found"
+    names = m.group(1).split(",")
+    for want in ("C", "Cu", "D", "Du", "S", "Usmall", "S_short", "S_mixed", "S_large"):
+        assert want in names, want
